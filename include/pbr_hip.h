@@ -1,0 +1,225 @@
+/*
+ * pbr_hip.h — C-ABI drop-in boundary for the MI355X render path.
+ *
+ * The reference (G0T-cha/PysicalBasedRaytracer) has no FFI: its hot path is reached through the
+ * C++ virtual `Integrator::Render(const Scene&, double&)` (Integrator/Integrator.h:14) after the
+ * scene has been assembled from `GeometricPrimitive`s (Core/Primitive.h:30-33), a `BVHAccel`
+ * (Accelerator/BVHAccel.h:19-21), lights (Light/Light.h:50-61), a `HaltonSampler`
+ * (Sampler/Halton.h:18) and a `PerspectiveCamera` (Camera/Perspective.cpp:84-104).
+ * The C++ host mirror in include/pbr/ keeps those class names and constructors; underneath, every
+ * one of them flattens into the POD descriptors below and crosses into the HIP runtime through the
+ * five `pbr_hip_*` entry points.  Nothing here uses torch or STL types: plain pointers and sizes.
+ *
+ * Entry point ↔ reference interface it replaces:
+ *   pbr_hip_create        — (none; the reference has one implicit CPU "device")
+ *   pbr_hip_upload_scene  — Scene::Scene (Core/Scene.cpp:7-17) + BVHAccel::BVHAccel
+ *                           (Accelerator/BVHAccel.cpp:57-87) + TriangleMesh ctor (Shape/Triangle.cpp:12-44)
+ *                           + HaltonSampler ctor (Sampler/Halton.cpp:30-58)
+ *   pbr_hip_render        — SamplerIntegrator::Render (Integrator/Integrator.cpp:280-356), which
+ *                           drives {Whitted,Path,VolPath}Integrator::Li per sample
+ *   pbr_hip_destroy       — scene/integrator destructors
+ *   pbr_hip_last_error    — (none; the reference fails silently)
+ *
+ * Errors: every call returns 0 on success, a negative PBR_E_* code otherwise; the message is
+ * kept per context and returned by pbr_hip_last_error.  Calls on one context are not thread-safe;
+ * different contexts (one per device) are independent.
+ */
+#ifndef PBR_HIP_H
+#define PBR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBR_HIP_ABI_VERSION 1
+
+/* ---- status codes ---- */
+enum {
+    PBR_OK = 0,
+    PBR_E_INVALID = -1,   /* bad argument / descriptor */
+    PBR_E_HIP = -2,       /* a HIP runtime call failed */
+    PBR_E_NOSCENE = -3,   /* render before upload */
+    PBR_E_UNSUPPORTED = -4,
+    PBR_E_NODEVICE = -5
+};
+
+/* ---- enums mirroring the reference's class families ---- */
+enum pbr_shape_type { PBR_SHAPE_TRIANGLE_MESH = 0, PBR_SHAPE_SPHERE = 1 };
+enum pbr_material_type {
+    PBR_MAT_NONE = 0,     /* GeometricPrimitive with material == nullptr (medium boundary) */
+    PBR_MAT_MATTE = 1,    /* Material/MatteMaterial.cpp:13-28 */
+    PBR_MAT_MIRROR = 2,   /* Material/Mirror.cpp:5-15 */
+    PBR_MAT_GLASS = 3,    /* Material/GlassMaterial.cpp:9-57 */
+    PBR_MAT_METAL = 4,    /* Material/MetalMaterial.cpp:25-43 */
+    PBR_MAT_PLASTIC = 5   /* Material/PlasticMaterial.cpp:8-30 */
+};
+enum pbr_light_type {
+    PBR_LIGHT_POINT = 0,        /* Light/PointLight.cpp */
+    PBR_LIGHT_DIFFUSE_AREA = 1, /* Light/DiffuseLight.cpp */
+    PBR_LIGHT_SKYBOX = 2        /* Light/SkyBoxLight.cpp */
+};
+enum pbr_integrator_type {
+    PBR_INTEGRATOR_WHITTED = 0, /* Integrator/WhittedIntegrator.cpp:11-65 */
+    PBR_INTEGRATOR_PATH = 1,    /* Integrator/PathIntegrator.cpp:32-110 */
+    PBR_INTEGRATOR_VOLPATH = 2  /* Integrator/VolPathIntegrator.cpp:21-107 */
+};
+enum pbr_sampler_type { PBR_SAMPLER_HALTON = 0, PBR_SAMPLER_SOBOL = 1 };
+enum pbr_light_strategy { PBR_LIGHTS_UNIFORM = 0, PBR_LIGHTS_POWER = 1 };
+
+/* A reference Transform holds both m and mInv (Core/Transform.h:49-60); so do we. Row-major. */
+typedef struct pbr_transform {
+    float m[16];
+    float m_inv[16];
+} pbr_transform;
+
+/* One Shape family instance. Primitives are enumerated in shape order, triangles in index order:
+ * this is the `prims` vector order the reference hands to BVHAccel (Main/main.cpp:279-282). */
+typedef struct pbr_shape_desc {
+    int type;                   /* pbr_shape_type */
+    pbr_transform object_to_world;
+    int reverse_orientation;
+    /* triangle mesh (Shape/Triangle.h:11-24) */
+    int n_triangles;
+    int n_vertices;
+    const int32_t* indices;     /* 3*n_triangles */
+    const float* P;             /* 3*n_vertices, object space */
+    const float* N;             /* optional 3*n_vertices per-vertex normals, or NULL */
+    const float* UV;            /* optional 2*n_vertices, or NULL (default (0,0),(1,0),(1,1)) */
+    /* sphere (Shape/Sphere.h) */
+    float radius;
+    /* GeometricPrimitive fields (Core/Primitive.h:30-33) */
+    int material;               /* index into materials, -1 = nullptr */
+    int area_light_first;       /* triangle t carries lights[area_light_first + t]; -1 = none */
+    int medium_inside;          /* MediumInterface, -1 = nullptr */
+    int medium_outside;
+} pbr_shape_desc;
+
+typedef struct pbr_material_desc {
+    int type;                   /* pbr_material_type */
+    float Kd[3];                /* matte Kd, plastic Kd */
+    float sigma;                /* matte sigma (degrees) */
+    float Kr[3];                /* mirror Kr, glass Kr */
+    float Kt[3];                /* glass Kt */
+    float Ks[3];                /* plastic Ks */
+    float eta;                  /* glass index */
+    float metal_eta[3];         /* metal eta */
+    float metal_k[3];           /* metal k */
+    float roughness;            /* metal roughness / plastic roughness */
+    float uroughness;           /* glass/metal u roughness (metal: used when has_uv_roughness) */
+    float vroughness;
+    int has_uv_roughness;       /* metal: uRoughness/vRoughness textures present */
+    int remap_roughness;
+} pbr_material_desc;
+
+typedef struct pbr_light_desc {
+    int type;                   /* pbr_light_type */
+    pbr_transform light_to_world;
+    float I[3];                 /* point intensity */
+    float Le[3];                /* area emission */
+    int shape;                  /* area light: index of the mesh shape ... */
+    int triangle;               /* ... and the triangle in it */
+    int two_sided;
+    int n_samples;
+    int medium_inside, medium_outside;
+    /* SkyBoxLight (Light/SkyBoxLight.h): env data as stbi_loadf returns it with vertical flip */
+    float world_center[3];
+    float world_radius;
+    int env_width, env_height, env_components;
+    const float* env_data;      /* env_width*env_height*env_components, or NULL → black */
+} pbr_light_desc;
+
+typedef struct pbr_medium_desc {   /* Media/HomogeneousMedium.h */
+    float sigma_a[3];
+    float sigma_s[3];
+    float g;
+} pbr_medium_desc;
+
+typedef struct pbr_scene_desc {
+    int abi_version;            /* PBR_HIP_ABI_VERSION */
+    int n_shapes;
+    const pbr_shape_desc* shapes;
+    int n_materials;
+    const pbr_material_desc* materials;
+    int n_lights;
+    const pbr_light_desc* lights;
+    int n_media;
+    const pbr_medium_desc* media;
+    int max_prims_in_node;      /* BVHAccel maxPrimsInNode (main.cpp:385 uses 1) */
+} pbr_scene_desc;
+
+/* CreatePerspectiveCamera (Camera/Perspective.cpp:84-104) inputs. */
+typedef struct pbr_camera_desc {
+    int width, height;          /* raster resolution */
+    pbr_transform camera_to_world;
+    int use_look_at;            /* if set, camera_to_world = Inverse(LookAt(eye, look, up)) */
+    float eye[3], look[3], up[3];
+    float fov;                  /* degrees; the reference fixes 90 */
+    float lens_radius;          /* the reference fixes 0 */
+    float focal_distance;
+    int medium;                 /* camera medium (dropped by CameraToWorld, F12) */
+} pbr_camera_desc;
+
+typedef struct pbr_tile {
+    int x0, y0, x1, y1;         /* half-open pixel rectangle */
+} pbr_tile;
+
+typedef struct pbr_render_desc {
+    int integrator;             /* pbr_integrator_type */
+    int max_depth;
+    float rr_threshold;
+    int light_strategy;         /* pbr_light_strategy ("spatial" falls back to uniform, LightDistrib.cpp:10-21) */
+    int sampler;                /* pbr_sampler_type */
+    int spp;
+    pbr_camera_desc camera;
+    /* pixels to render; n_tiles == 0 → whole frame. Output is packed tile after tile, each tile
+     * row-major, 3 floats (linear RGB = colObj/spp) and 4 bytes (RGBA8) per pixel. */
+    int n_tiles;
+    const pbr_tile* tiles;
+    int outputs_on_device;      /* 1: rgb_out/rgba_out are device pointers (e.g. torch tensors) */
+    void* stream;               /* hipStream_t to launch on (NULL = context stream) */
+    int collect_stats;          /* 1: also count BVH node visits / triangle tests (slower) */
+} pbr_render_desc;
+
+typedef struct pbr_render_stats {
+    double seconds;             /* wall time of the render call (incl. launch + sync) */
+    double kernel_ms;           /* device time of the integrator kernel(s), HIP events */
+    double film_ms;             /* device time of the film/output kernel */
+    uint64_t samples;           /* pixels * spp rendered */
+    uint64_t rays;              /* rays traced (closest + any hit), if collect_stats */
+    uint64_t node_visits;       /* LinearBVHNode visits, if collect_stats */
+    uint64_t prim_tests;        /* primitive intersection tests, if collect_stats */
+    uint64_t shading_events;    /* surface/medium interactions shaded, if collect_stats */
+    int n_launches;
+} pbr_render_stats;
+
+typedef struct pbr_hip_ctx pbr_hip_ctx;
+
+int pbr_hip_create(int device, pbr_hip_ctx** out);
+int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* scene);
+int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* desc,
+                   float* rgb_out, uint8_t* rgba_out, pbr_render_stats* stats);
+int pbr_hip_destroy(pbr_hip_ctx* ctx);
+const char* pbr_hip_last_error(const pbr_hip_ctx* ctx);
+
+/* ---- introspection used by the parity tests (no reference counterpart) ---- */
+/* Flattened BVH after upload: 32-B LinearBVHNode records (BVHAccel.cpp:46-55) and the ordered
+ * primitive ids (position in the `prims` vector).  Pass NULL buffers to query counts. */
+int pbr_hip_get_bvh(pbr_hip_ctx* ctx, void* nodes_out, int* n_nodes, int32_t* prim_ids_out, int* n_prims);
+/* Halton/Sobol samples computed ON THE DEVICE for (pixel, sample, dim) triples. */
+int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height, int spp,
+                           int n, const int32_t* px_py_sample_dim, float* out);
+/* Camera rays computed on the device for raster samples (pFilm.x, pFilm.y): out = o.xyz, d.xyz */
+int pbr_hip_camera_rays(pbr_hip_ctx* ctx, const pbr_camera_desc* cam, int n, const float* pfilm, float* out);
+/* Closest-hit queries on the device: rays = o.xyz d.xyz tmax; out = {hit, t, prim_id, b1, b2} as floats */
+int pbr_hip_intersect(pbr_hip_ctx* ctx, int n, const float* rays, float* out, int any_hit);
+/* Device build info: ABI version, gfx arch string. */
+int pbr_hip_abi_version(void);
+const char* pbr_hip_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBR_HIP_H */

@@ -1,0 +1,568 @@
+// orc_core.h — TEST INFRASTRUCTURE ONLY. Part of the CPU restatement used as the parity checker.
+// Math core, transforms, sampler, camera, shapes and BVH of the reference, restated op for op.
+// Every function cites the reference file:line it follows (paths relative to the reference root).
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+namespace orc {
+
+// ---------------------------------------------------------------- constants (Core/PBR.h:12-24)
+static constexpr float Pi = 3.14159265358979323846;
+static constexpr float InvPi = 0.31830988618379067154;
+static constexpr float Inv2Pi = 0.15915494309189533577;
+static constexpr float Inv4Pi = 0.07957747154594766788;
+static constexpr float PiOver2 = 1.57079632679489661923;
+static constexpr float PiOver4 = 0.78539816339744830961;
+static constexpr float ShadowEpsilon = 0.0001f;                       // Core/PBR.h:45
+static constexpr float OneMinusEpsilon = 0.99999994f;                 // Sampler/RNG.h:13,19
+static const float Infinity = std::numeric_limits<float>::infinity();
+static const float MaxFloat = std::numeric_limits<float>::max();
+// gamma(n) is evaluated in double and narrowed once (Core/PBR.h:21-24).
+inline float gamma(int n) {
+    const double eps = std::numeric_limits<float>::epsilon() * 0.5;
+    return (float)((n * eps) / (1 - n * eps));
+}
+
+// Transcendentals: correctly rounded convention (see pbr_oracle.h header).
+inline float t_sin(float x) { return (float)std::sin((double)x); }
+inline float t_cos(float x) { return (float)std::cos((double)x); }
+inline float t_tan(float x) { return (float)std::tan((double)x); }
+inline float t_exp(float x) { return (float)std::exp((double)x); }
+inline float t_log(float x) { return (float)std::log((double)x); }
+inline float t_pow(float x, float y) { return (float)std::pow((double)x, (double)y); }
+inline float t_atan2(float y, float x) { return (float)std::atan2((double)y, (double)x); }
+inline float t_asin(float x) { return (float)std::asin((double)x); }
+
+// std::min / std::max / Clamp semantics (NaN-sensitive order), Core/PBR.h:183-191
+inline float fmin_(float a, float b) { return (b < a) ? b : a; }
+inline float fmax_(float a, float b) { return (a < b) ? b : a; }
+inline float Clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+inline int Clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+inline uint32_t FloatToBits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+inline float BitsToFloat(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+// Core/PBR.h:142-154
+inline float NextFloatUp(float v) {
+    if (std::isinf(v) && v > 0.) return v;
+    if (v == -0.f) v = 0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v >= 0) ++ui; else --ui;
+    return BitsToFloat(ui);
+}
+// Core/PBR.h:155-165
+inline float NextFloatDown(float v) {
+    if (std::isinf(v) && v < 0.) return v;
+    if (v == 0.f) v = -0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v > 0) --ui; else ++ui;
+    return BitsToFloat(ui);
+}
+
+// ---------------------------------------------------------------- vectors (Core/Geometry.h)
+// One type stands for Vector3f / Point3f / Normal3f: the reference's three classes share the same
+// per-component arithmetic, only their conversions differ.
+struct V3 {
+    float x = 0, y = 0, z = 0;
+    V3() {}
+    V3(float a, float b, float c) : x(a), y(b), z(c) {}
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    float& operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+};
+inline V3 operator+(V3 a, V3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline V3 operator-(V3 a, V3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline V3 operator-(V3 a) { return V3(-a.x, -a.y, -a.z); }
+inline V3 operator*(V3 a, float s) { return V3(s * a.x, s * a.y, s * a.z); }   // Geometry.h:209-212
+inline V3 operator*(float s, V3 a) { return V3(s * a.x, s * a.y, s * a.z); }
+// Vector3::operator/ multiplies by a float reciprocal (Geometry.h:222-227)
+inline V3 operator/(V3 a, float f) { float inv = (float)1 / f; return V3(a.x * inv, a.y * inv, a.z * inv); }
+inline float Dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }          // Geometry.h:684-688
+inline float AbsDot(V3 a, V3 b) { return std::abs(Dot(a, b)); }
+inline V3 Abs(V3 a) { return V3(std::abs(a.x), std::abs(a.y), std::abs(a.z)); }
+// Cross in double, one narrowing per component (Geometry.h:705-714, F14)
+inline V3 Cross(V3 v1, V3 v2) {
+    double v1x = v1.x, v1y = v1.y, v1z = v1.z, v2x = v2.x, v2y = v2.y, v2z = v2.z;
+    return V3((float)((v1y * v2z) - (v1z * v2y)), (float)((v1z * v2x) - (v1x * v2z)),
+              (float)((v1x * v2y) - (v1y * v2x)));
+}
+inline float LengthSquared(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+inline float Length(V3 a) { return std::sqrt(LengthSquared(a)); }
+inline V3 Normalize(V3 a) { return a / Length(a); }                                  // Geometry.h:735-738
+inline float MaxComponent(V3 v) { return fmax_(v.x, fmax_(v.y, v.z)); }
+inline int MaxDimension(V3 v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
+inline V3 Permute(V3 v, int x, int y, int z) { return V3(v[x], v[y], v[z]); }
+inline float DistanceSquared(V3 a, V3 b) { return LengthSquared(a - b); }
+inline V3 Faceforward(V3 n, V3 v) { return (Dot(n, v) < 0.f) ? -n : n; }           // Geometry.h:1005-1009
+inline V3 Vmin(V3 a, V3 b) { return V3(fmin_(a.x, b.x), fmin_(a.y, b.y), fmin_(a.z, b.z)); }
+inline V3 Vmax(V3 a, V3 b) { return V3(fmax_(a.x, b.x), fmax_(a.y, b.y), fmax_(a.z, b.z)); }
+inline bool IsZero(V3 n) { return n.x == 0 && n.y == 0 && n.z == 0; }
+// Geometry.h:770-777
+inline void CoordinateSystem(V3 v1, V3* v2, V3* v3) {
+    if (std::abs(v1.x) > std::abs(v1.y))
+        *v2 = V3(-v1.z, 0, v1.x) / std::sqrt(v1.x * v1.x + v1.z * v1.z);
+    else
+        *v2 = V3(0, v1.z, -v1.y) / std::sqrt(v1.y * v1.y + v1.z * v1.z);
+    *v3 = Cross(v1, *v2);
+}
+// Geometry.h:1518-1522
+inline V3 SphericalDirection(float sinTheta, float cosTheta, float phi, V3 x, V3 y, V3 z) {
+    return sinTheta * t_cos(phi) * x + sinTheta * t_sin(phi) * y + cosTheta * z;
+}
+
+struct P2 { float x = 0, y = 0; P2() {} P2(float a, float b) : x(a), y(b) {} };
+
+// ---------------------------------------------------------------- bounds (Geometry.h:1204-1468)
+struct Bounds3 {
+    V3 pMin, pMax;
+    Bounds3() {
+        float lo = std::numeric_limits<float>::lowest(), hi = std::numeric_limits<float>::max();
+        pMin = V3(hi, hi, hi); pMax = V3(lo, lo, lo);
+    }
+    Bounds3(V3 p1, V3 p2) : pMin(Vmin(p1, p2)), pMax(Vmax(p1, p2)) {}
+    const V3& operator[](int i) const { return i == 0 ? pMin : pMax; }
+    float SurfaceArea() const { V3 d = pMax - pMin; return 2 * (d.x * d.y + d.x * d.z + d.y * d.z); }
+    int MaximumExtent() const {
+        V3 d = pMax - pMin;
+        if (d.x > d.y && d.x > d.z) return 0; else if (d.y > d.z) return 1; else return 2;
+    }
+    V3 Offset(V3 p) const {
+        V3 o = p - pMin;
+        if (pMax.x > pMin.x) o.x /= pMax.x - pMin.x;
+        if (pMax.y > pMin.y) o.y /= pMax.y - pMin.y;
+        if (pMax.z > pMin.z) o.z /= pMax.z - pMin.z;
+        return o;
+    }
+};
+inline Bounds3 Union(const Bounds3& b, V3 p) { Bounds3 r; r.pMin = Vmin(b.pMin, p); r.pMax = Vmax(b.pMax, p); return r; }
+inline Bounds3 Union(const Bounds3& a, const Bounds3& b) { Bounds3 r; r.pMin = Vmin(a.pMin, b.pMin); r.pMax = Vmax(a.pMax, b.pMax); return r; }
+
+struct Ray {   // Geometry.h:1360-1376 (differentials are dead for shading, F5)
+    V3 o, d;
+    mutable float tMax = Infinity;
+    int medium = -1;
+    Ray() {}
+    Ray(V3 o_, V3 d_, float t = Infinity, int med = -1) : o(o_), d(d_), tMax(t), medium(med) {}
+    V3 at(float t) const { return o + d * t; }
+};
+
+// Geometry.h:1438-1468 — no tMax widening (F8)
+inline bool BoundsIntersectP(const Bounds3& b, const Ray& ray, V3 invDir, const int dirIsNeg[3]) {
+    float tMin = (b[dirIsNeg[0]].x - ray.o.x) * invDir.x;
+    float tMax = (b[1 - dirIsNeg[0]].x - ray.o.x) * invDir.x;
+    float tyMin = (b[dirIsNeg[1]].y - ray.o.y) * invDir.y;
+    float tyMax = (b[1 - dirIsNeg[1]].y - ray.o.y) * invDir.y;
+    if (tMin > tyMax || tyMin > tMax) return false;
+    if (tyMin > tMin) tMin = tyMin;
+    if (tyMax < tMax) tMax = tyMax;
+    float tzMin = (b[dirIsNeg[2]].z - ray.o.z) * invDir.z;
+    float tzMax = (b[1 - dirIsNeg[2]].z - ray.o.z) * invDir.z;
+    if (tMin > tzMax || tzMin > tMax) return false;
+    if (tzMin > tMin) tMin = tzMin;
+    if (tzMax < tMax) tMax = tzMax;
+    return (tMin < ray.tMax) && (tMax > 0);
+}
+
+// Geometry.h:1470-1484
+inline V3 OffsetRayOrigin(V3 p, V3 pError, V3 n, V3 w) {
+    float d = Dot(Abs(n), pError);
+    V3 offset = d * n;
+    if (Dot(w, n) < 0) offset = -offset;
+    V3 po = p + offset;
+    for (int i = 0; i < 3; ++i) {
+        if (offset[i] > 0) po[i] = NextFloatUp(po[i]);
+        else if (offset[i] < 0) po[i] = NextFloatDown(po[i]);
+    }
+    return po;
+}
+
+// ---------------------------------------------------------------- transforms (Core/Transform.*)
+struct M4 {
+    float m[4][4];
+    M4() { for (int i = 0; i < 4; ++i) for (int j = 0; j < 4; ++j) m[i][j] = (i == j) ? 1.f : 0.f; }
+    static M4 rows(const float* a) { M4 r; std::memcpy(r.m, a, 64); return r; }
+};
+// Transform.h:39-46
+inline M4 Mul(const M4& a, const M4& b) {
+    M4 r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            r.m[i][j] = a.m[i][0] * b.m[0][j] + a.m[i][1] * b.m[1][j] + a.m[i][2] * b.m[2][j] + a.m[i][3] * b.m[3][j];
+    return r;
+}
+// Gauss-Jordan with full pivoting (Transform.cpp:59-130)
+inline M4 Inverse(const M4& mat) {
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    float minv[4][4];
+    std::memcpy(minv, mat.m, 64);
+    for (int i = 0; i < 4; i++) {
+        int irow = 0, icol = 0;
+        float big = 0.f;
+        for (int j = 0; j < 4; j++) {
+            if (ipiv[j] != 1) {
+                for (int k = 0; k < 4; k++) {
+                    if (ipiv[k] == 0) {
+                        if (std::abs(minv[j][k]) >= big) { big = float(std::abs(minv[j][k])); irow = j; icol = k; }
+                    }
+                }
+            }
+        }
+        ++ipiv[icol];
+        if (irow != icol) for (int k = 0; k < 4; ++k) std::swap(minv[irow][k], minv[icol][k]);
+        indxr[i] = irow;
+        indxc[i] = icol;
+        float pivinv = 1. / minv[icol][icol];
+        minv[icol][icol] = 1.;
+        for (int j = 0; j < 4; j++) minv[icol][j] *= pivinv;
+        for (int j = 0; j < 4; j++) {
+            if (j != icol) {
+                float save = minv[j][icol];
+                minv[j][icol] = 0;
+                for (int k = 0; k < 4; k++) minv[j][k] -= minv[icol][k] * save;
+            }
+        }
+    }
+    for (int j = 3; j >= 0; j--) {
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) std::swap(minv[k][indxr[j]], minv[k][indxc[j]]);
+    }
+    M4 r; std::memcpy(r.m, minv, 64); return r;
+}
+struct Xform {
+    M4 m, mInv;
+    Xform() {}
+    Xform(const M4& a, const M4& b) : m(a), mInv(b) {}
+    explicit Xform(const M4& a) : m(a), mInv(Inverse(a)) {}
+    // Transform.h:139-151
+    V3 point(V3 p) const {
+        float x = p.x, y = p.y, z = p.z;
+        float xp = m.m[0][0] * x + m.m[0][1] * y + m.m[0][2] * z + m.m[0][3];
+        float yp = m.m[1][0] * x + m.m[1][1] * y + m.m[1][2] * z + m.m[1][3];
+        float zp = m.m[2][0] * x + m.m[2][1] * y + m.m[2][2] * z + m.m[2][3];
+        float wp = m.m[3][0] * x + m.m[3][1] * y + m.m[3][2] * z + m.m[3][3];
+        if (wp == 1) return V3(xp, yp, zp);
+        float inv = (float)1 / wp;                         // Point3::operator/ (Geometry.h:458-463)
+        return V3(inv * xp, inv * yp, inv * zp);
+    }
+    // Transform.h:152-158
+    V3 vector(V3 v) const {
+        float x = v.x, y = v.y, z = v.z;
+        return V3(m.m[0][0] * x + m.m[0][1] * y + m.m[0][2] * z, m.m[1][0] * x + m.m[1][1] * y + m.m[1][2] * z,
+                  m.m[2][0] * x + m.m[2][1] * y + m.m[2][2] * z);
+    }
+    // Transform.h:159-164
+    V3 normal(V3 n) const {
+        float x = n.x, y = n.y, z = n.z;
+        return V3(mInv.m[0][0] * x + mInv.m[1][0] * y + mInv.m[2][0] * z,
+                  mInv.m[0][1] * x + mInv.m[1][1] * y + mInv.m[2][1] * z,
+                  mInv.m[0][2] * x + mInv.m[1][2] * y + mInv.m[2][2] * z);
+    }
+    bool SwapsHandedness() const {   // Transform.cpp:144-150
+        float det = m.m[0][0] * (m.m[1][1] * m.m[2][2] - m.m[1][2] * m.m[2][1]) -
+                    m.m[0][1] * (m.m[1][0] * m.m[2][2] - m.m[1][2] * m.m[2][0]) +
+                    m.m[0][2] * (m.m[1][0] * m.m[2][1] - m.m[1][1] * m.m[2][0]);
+        return det < 0;
+    }
+};
+inline Xform operator*(const Xform& a, const Xform& b) { return Xform(Mul(a.m, b.m), Mul(b.mInv, a.mInv)); }  // Transform.cpp:151-154
+inline Xform InverseX(const Xform& t) { return Xform(t.mInv, t.m); }
+inline Xform Scale(float x, float y, float z) {   // Transform.cpp:164-169
+    M4 a, b;
+    a.m[0][0] = x; a.m[1][1] = y; a.m[2][2] = z;
+    b.m[0][0] = 1 / x; b.m[1][1] = 1 / y; b.m[2][2] = 1 / z;
+    return Xform(a, b);
+}
+inline Xform Translate(V3 d) {   // Transform.cpp:156-163
+    M4 a, b;
+    a.m[0][3] = d.x; a.m[1][3] = d.y; a.m[2][3] = d.z;
+    b.m[0][3] = -d.x; b.m[1][3] = -d.y; b.m[2][3] = -d.z;
+    return Xform(a, b);
+}
+inline float Radians(float deg) { return (Pi / 180) * deg; }
+inline Xform Perspective(float fov, float n, float f) {   // Transform.cpp:257-264
+    M4 persp;
+    persp.m[2][2] = f / (f - n); persp.m[2][3] = -f * n / (f - n);
+    persp.m[3][2] = 1; persp.m[3][3] = 0;
+    float invTanAng = 1 / t_tan(Radians(fov) / 2);
+    return Scale(invTanAng, invTanAng, 1) * Xform(persp);
+}
+// Transform.cpp:208-239 — returns world-to-camera; callers invert it (main.cpp:202-203)
+inline Xform LookAt(V3 pos, V3 look, V3 up) {
+    M4 c;
+    c.m[0][3] = pos.x; c.m[1][3] = pos.y; c.m[2][3] = pos.z; c.m[3][3] = 1;
+    V3 dir = Normalize(look - pos);
+    if (Length(Cross(Normalize(up), dir)) == 0) return Xform();
+    V3 right = Normalize(Cross(Normalize(up), dir));
+    V3 newUp = Cross(dir, right);
+    c.m[0][0] = right.x; c.m[1][0] = right.y; c.m[2][0] = right.z; c.m[3][0] = 0.;
+    c.m[0][1] = newUp.x; c.m[1][1] = newUp.y; c.m[2][1] = newUp.z; c.m[3][1] = 0.;
+    c.m[0][2] = dir.x; c.m[1][2] = dir.y; c.m[2][2] = dir.z; c.m[3][2] = 0.;
+    return Xform(Inverse(c), c);
+}
+
+// ---------------------------------------------------------------- spectrum (Core/Spectrum.h)
+struct Spec {
+    float c[3];
+    Spec(float v = 0.f) { c[0] = c[1] = c[2] = v; }
+    Spec(float r, float g, float b) { c[0] = r; c[1] = g; c[2] = b; }
+    float operator[](int i) const { return c[i]; }
+    float& operator[](int i) { return c[i]; }
+    bool IsBlack() const { return c[0] == 0. && c[1] == 0. && c[2] == 0.; }
+    float MaxComponentValue() const { return fmax_(fmax_(c[0], c[1]), c[2]); }
+    Spec Clamp(float lo = 0, float hi = Infinity) const { return Spec(Clampf(c[0], lo, hi), Clampf(c[1], lo, hi), Clampf(c[2], lo, hi)); }
+    float y() const { return 0.212671f * c[0] + 0.715160f * c[1] + 0.072169f * c[2]; }
+};
+inline Spec operator+(Spec a, Spec b) { return Spec(a[0] + b[0], a[1] + b[1], a[2] + b[2]); }
+inline Spec operator-(Spec a, Spec b) { return Spec(a[0] - b[0], a[1] - b[1], a[2] - b[2]); }
+inline Spec operator*(Spec a, Spec b) { return Spec(a[0] * b[0], a[1] * b[1], a[2] * b[2]); }
+inline Spec operator/(Spec a, Spec b) { return Spec(a[0] / b[0], a[1] / b[1], a[2] / b[2]); }
+inline Spec operator*(Spec a, float s) { return Spec(a[0] * s, a[1] * s, a[2] * s); }
+inline Spec operator*(float s, Spec a) { return a * s; }
+inline Spec operator/(Spec a, float s) { return Spec(a[0] / s, a[1] / s, a[2] / s); }   // true division (Spectrum.h:103-109)
+inline Spec& operator+=(Spec& a, Spec b) { a = a + b; return a; }
+inline Spec& operator*=(Spec& a, Spec b) { a = a * b; return a; }
+inline Spec& operator*=(Spec& a, float s) { a = a * s; return a; }
+inline Spec& operator/=(Spec& a, float s) { a = a / s; return a; }
+inline Spec SqrtS(Spec a) { return Spec(std::sqrt(a[0]), std::sqrt(a[1]), std::sqrt(a[2])); }
+inline Spec ExpS(Spec a) { return Spec(t_exp(a[0]), t_exp(a[1]), t_exp(a[2])); }
+// Spectrum.h:219-226 (exposure arrives as float)
+inline Spec HDRtoLDR(Spec col, float exposure) {
+    float invExposure = (float)(1.0 / (1.0 - (double)exposure));
+    return Spec((float)(1.0 - (double)t_exp(-col[0] * invExposure)), (float)(1.0 - (double)t_exp(-col[1] * invExposure)),
+                (float)(1.0 - (double)t_exp(-col[2] * invExposure)));
+}
+
+// ---------------------------------------------------------------- RNG + Halton (Sampler/)
+struct PCG {   // Sampler/RNG.h:25-108
+    uint64_t state = 0x853c49e6748fea9bULL, inc = 0xda3e39cb94b95bdbULL;
+    uint32_t next() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    uint32_t bounded(uint32_t b) {
+        uint32_t threshold = (~b + 1u) % b;
+        for (;;) { uint32_t r = next(); if (r >= threshold) return r % b; }
+    }
+};
+
+std::vector<int> first_primes(int n);
+
+// Sampler/LowDiscrepancy.cpp:2284-2298 + Sampler/Sampling.h:47-54
+inline std::vector<uint16_t> RadicalInversePerms(int nPrimes) {
+    std::vector<int> primes = first_primes(nPrimes);
+    size_t total = 0;
+    for (int p : primes) total += p;
+    std::vector<uint16_t> perms(total);
+    PCG rng;
+    uint16_t* p = perms.data();
+    for (int i = 0; i < nPrimes; ++i) {
+        int count = primes[i];
+        for (int j = 0; j < count; ++j) p[j] = (uint16_t)j;
+        for (int j = 0; j < count; ++j) {
+            int other = j + (int)rng.bounded((uint32_t)(count - j));
+            std::swap(p[j], p[other]);
+        }
+        p += count;
+    }
+    return perms;
+}
+
+// LowDiscrepancy.cpp:211-225 (base 2 case: ReverseBits64 * 2^-64, narrowed from double)
+inline float RadicalInverseBase2(uint64_t a) {
+    uint64_t n = a;
+    n = (n << 32) | (n >> 32);
+    n = ((n & 0x0000ffff0000ffffULL) << 16) | ((n & 0xffff0000ffff0000ULL) >> 16);
+    n = ((n & 0x00ff00ff00ff00ffULL) << 8) | ((n & 0xff00ff00ff00ff00ULL) >> 8);
+    n = ((n & 0x0f0f0f0f0f0f0f0fULL) << 4) | ((n & 0xf0f0f0f0f0f0f0f0ULL) >> 4);
+    n = ((n & 0x3333333333333333ULL) << 2) | ((n & 0xccccccccccccccccULL) >> 2);
+    n = ((n & 0x5555555555555555ULL) << 1) | ((n & 0xaaaaaaaaaaaaaaaaULL) >> 1);
+    return (float)((double)n * 5.4210108624275222e-20);
+}
+// LowDiscrepancy.cpp:212-225 RadicalInverseSpecialized<base>
+inline float RadicalInverseB(int base, uint64_t a) {
+    const float invBase = (float)1 / (float)base;
+    uint64_t reversedDigits = 0;
+    float invBaseN = 1;
+    while (a) {
+        uint64_t next = a / base;
+        uint64_t digit = a - next * base;
+        reversedDigits = reversedDigits * base + digit;
+        invBaseN *= invBase;
+        a = next;
+    }
+    return fmin_((float)reversedDigits * invBaseN, OneMinusEpsilon);
+}
+// LowDiscrepancy.cpp:2300-2315 ScrambledRadicalInverseSpecialized<base>
+inline float ScrambledRadicalInverseB(int base, const uint16_t* perm, uint64_t a) {
+    const float invBase = (float)1 / (float)base;
+    uint64_t reversedDigits = 0;
+    float invBaseN = 1;
+    while (a) {
+        uint64_t next = a / base;
+        uint64_t digit = a - next * base;
+        reversedDigits = reversedDigits * base + perm[digit];
+        invBaseN *= invBase;
+        a = next;
+    }
+    return fmin_(invBaseN * ((float)reversedDigits + invBase * (float)perm[0] / (1 - invBase)), OneMinusEpsilon);
+}
+
+struct HaltonTables {
+    std::vector<int> primes, primeSums;
+    std::vector<uint16_t> perms;
+    void init(int nDims) {
+        primes = first_primes(nDims);
+        primeSums.resize(nDims);
+        int s = 0;
+        for (int i = 0; i < nDims; ++i) { primeSums[i] = s; s += primes[i]; }
+        perms = RadicalInversePerms(nDims);
+    }
+};
+
+// Sampler/Halton.cpp:30-92 + Sampler/Sampler.cpp:10-143 (GlobalSampler, no sample arrays)
+struct Halton {
+    const HaltonTables* tab;
+    int baseScales[2], baseExponents[2], sampleStride, multInverse[2];
+    int64_t spp;
+    // per-pixel state
+    int64_t offsetForCurrentPixel = 0, intervalSampleIndex = 0, currentPixelSampleIndex = 0;
+    int dimension = 0;
+    static void extendedGCD(uint64_t a, uint64_t b, int64_t* x, int64_t* y) {
+        if (b == 0) { *x = 1; *y = 0; return; }
+        int64_t d = a / b, xp, yp;
+        extendedGCD(b, a % b, &xp, &yp);
+        *x = yp; *y = xp - (d * yp);
+    }
+    static uint64_t multiplicativeInverse(int64_t a, int64_t n) {
+        int64_t x, y;
+        extendedGCD(a, n, &x, &y);
+        int64_t r = x - (x / n) * n;                      // Mod (Core/PBR.h:193-197)
+        return (uint64_t)((r < 0) ? r + n : r);
+    }
+    void init(const HaltonTables* t, int64_t samplesPerPixel, int resX, int resY) {
+        tab = t; spp = samplesPerPixel;
+        int res[2] = {resX, resY};
+        for (int i = 0; i < 2; ++i) {
+            int base = (i == 0) ? 2 : 3;
+            int scale = 1, exp = 0;
+            while (scale < std::min(res[i], 128)) { scale *= base; ++exp; }
+            baseScales[i] = scale; baseExponents[i] = exp;
+        }
+        sampleStride = baseScales[0] * baseScales[1];
+        multInverse[0] = (int)multiplicativeInverse(baseScales[1], baseScales[0]);
+        multInverse[1] = (int)multiplicativeInverse(baseScales[0], baseScales[1]);
+    }
+    static uint64_t InverseRadicalInverse(int base, uint64_t inverse, int nDigits) {   // LowDiscrepancy.h:28-37
+        uint64_t index = 0;
+        for (int i = 0; i < nDigits; ++i) { uint64_t digit = inverse % base; inverse /= base; index = index * base + digit; }
+        return index;
+    }
+    int64_t GetIndexForSample(int px, int py, int64_t sampleNum) {
+        int64_t off = 0;
+        if (sampleStride > 1) {
+            int pm[2] = {px % 128, py % 128};
+            if (pm[0] < 0) pm[0] += 128;
+            if (pm[1] < 0) pm[1] += 128;
+            for (int i = 0; i < 2; ++i) {
+                uint64_t dimOffset = InverseRadicalInverse(i == 0 ? 2 : 3, (uint64_t)pm[i], baseExponents[i]);
+                off += dimOffset * (sampleStride / baseScales[i]) * multInverse[i];
+            }
+            off %= sampleStride;
+        }
+        return off + sampleNum * sampleStride;
+    }
+    float SampleDimension(int64_t index, int dim) const {
+        if (dim == 0) return RadicalInverseBase2((uint64_t)(index >> baseExponents[0]));
+        if (dim == 1) return RadicalInverseB(3, (uint64_t)(index / baseScales[1]));
+        if (dim >= (int)tab->primes.size()) return 0;   // beyond PrimeTableSize: UB in the reference
+        return ScrambledRadicalInverseB(tab->primes[dim], &tab->perms[tab->primeSums[dim]], (uint64_t)index);
+    }
+    int px = 0, py = 0;
+    void StartPixel(int x, int y) {
+        px = x; py = y; currentPixelSampleIndex = 0; dimension = 0;
+        intervalSampleIndex = GetIndexForSample(px, py, 0);
+    }
+    void SetSampleNumber(int64_t s) {
+        currentPixelSampleIndex = s; dimension = 0;
+        intervalSampleIndex = GetIndexForSample(px, py, s);
+    }
+    bool StartNextSample() {
+        dimension = 0;
+        intervalSampleIndex = GetIndexForSample(px, py, currentPixelSampleIndex + 1);
+        return ++currentPixelSampleIndex < spp;
+    }
+    // GlobalSampler::Get1D/Get2D (Sampler.cpp:131-143); no sample arrays → arrayStartDim == arrayEndDim == 5
+    static constexpr int arrayStartDim = 5, arrayEndDim = 5;
+    float Get1D() {
+        if (dimension >= arrayStartDim && dimension < arrayEndDim) dimension = arrayEndDim;
+        return SampleDimension(intervalSampleIndex, dimension++);
+    }
+    P2 Get2D() {
+        if (dimension + 1 >= arrayStartDim && dimension < arrayEndDim) dimension = arrayEndDim;
+        P2 p(SampleDimension(intervalSampleIndex, dimension), SampleDimension(intervalSampleIndex, dimension + 1));
+        dimension += 2;
+        return p;
+    }
+};
+
+// ---------------------------------------------------------------- sampling (Sampler/Sampling.*)
+inline P2 ConcentricSampleDisk(P2 u) {   // Sampling.cpp:74-92
+    P2 uOffset(2.f * u.x - 1, 2.f * u.y - 1);
+    if (uOffset.x == 0 && uOffset.y == 0) return P2(0, 0);
+    float theta, r;
+    if (std::abs(uOffset.x) > std::abs(uOffset.y)) { r = uOffset.x; theta = PiOver4 * (uOffset.y / uOffset.x); }
+    else { r = uOffset.y; theta = PiOver2 - PiOver4 * (uOffset.x / uOffset.y); }
+    return P2(r * t_cos(theta), r * t_sin(theta));
+}
+inline V3 CosineSampleHemisphere(P2 u) {   // Sampling.h:57-61
+    P2 d = ConcentricSampleDisk(u);
+    float z = std::sqrt(fmax_((float)0, 1 - d.x * d.x - d.y * d.y));
+    return V3(d.x, d.y, z);
+}
+inline V3 UniformSampleSphere(P2 u) {   // Sampling.cpp:59-64
+    float z = 1 - 2 * u.x;
+    float r = std::sqrt(fmax_((float)0, (float)1 - z * z));
+    float phi = 2 * Pi * u.y;
+    return V3(r * t_cos(phi), r * t_sin(phi), z);
+}
+inline P2 UniformSampleTriangle(P2 u) {   // Sampling.cpp:116-119
+    float su0 = std::sqrt(u.x);
+    return P2(1 - su0, u.y * su0);
+}
+inline float PowerHeuristic(int nf, float fPdf, int ng, float gPdf) {   // Sampling.h:72-75
+    float f = nf * fPdf, g = ng * gPdf;
+    return (f * f) / (f * f + g * g);
+}
+// Sampling.h:77-107
+struct Distribution1D {
+    std::vector<float> func, cdf;
+    float funcInt = 0;
+    Distribution1D() {}
+    Distribution1D(const float* f, int n) : func(f, f + n), cdf(n + 1) {
+        cdf[0] = 0;
+        for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + func[i - 1] / n;
+        funcInt = cdf[n];
+        if (funcInt == 0) { for (int i = 1; i < n + 1; ++i) cdf[i] = float(i) / float(n); }
+        else { for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt; }
+    }
+    int Count() const { return (int)func.size(); }
+    int SampleDiscrete(float u, float* pdf) const {
+        int size = (int)cdf.size();
+        int first = 0, len = size;
+        while (len > 0) {   // FindInterval (Core/PBR.h:167-181)
+            int half = len >> 1, middle = first + half;
+            if (cdf[middle] <= u) { first = middle + 1; len -= half + 1; } else len = half;
+        }
+        int offset = Clampi(first - 1, 0, size - 2);
+        if (pdf) *pdf = (funcInt > 0) ? func[offset] / (funcInt * Count()) : 0;
+        return offset;
+    }
+};
+
+}  // namespace orc

@@ -1,0 +1,131 @@
+"""MI355X-native render path for the reference's per-pixel integrator loop.
+
+`HipRenderer` is the Python face of the C-ABI (include/pbr_hip.h): upload a reference-shaped scene
+(`scenes.Scene`), then `render()` runs Whitted/Path/VolPath on the GPU — the counterpart of
+`Integrator::Render(const Scene&, double&)` (Integrator/Integrator.h:14).  The C++ host mirror of
+the reference classes lives in include/pbr/ (see INTEGRATION.md).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import capi, scenes  # noqa: F401
+
+__all__ = ["HipRenderer", "capi", "scenes", "tile_grid", "tiles_for_rank"]
+
+
+class PbrError(RuntimeError):
+    pass
+
+
+class HipRenderer:
+    def __init__(self, device: int = 0):
+        self.lib = capi.load_library()
+        self.ctx = C.c_void_p()
+        rc = self.lib.pbr_hip_create(device, C.byref(self.ctx))
+        if rc != capi.PBR_OK:
+            raise PbrError(f"pbr_hip_create failed ({rc}); a GPU is required — there is no CPU fallback")
+
+    def _check(self, rc, what):
+        if rc != capi.PBR_OK:
+            raise PbrError(f"{what} failed ({rc}): {self.lib.pbr_hip_last_error(self.ctx).decode()}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.pbr_hip_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene: "scenes.Scene"):
+        self._desc = scene.desc()
+        self._scene = scene
+        self._check(self.lib.pbr_hip_upload_scene(self.ctx, C.byref(self._desc)), "upload_scene")
+
+    @staticmethod
+    def n_pixels(rdesc) -> int:
+        if rdesc.n_tiles:
+            return sum((rdesc.tiles[i].x1 - rdesc.tiles[i].x0) * (rdesc.tiles[i].y1 - rdesc.tiles[i].y0)
+                       for i in range(rdesc.n_tiles))
+        return rdesc.camera.width * rdesc.camera.height
+
+    def render(self, rdesc, rgb=True, rgba=True, stats=False):
+        """Returns (rgb float32 [n,3], rgba uint8 [n,4], RenderStats) in packed tile order."""
+        n = self.n_pixels(rdesc)
+        out_rgb = np.empty((n, 3), dtype=np.float32) if rgb else None
+        out_rgba = np.empty((n, 4), dtype=np.uint8) if rgba else None
+        st = capi.RenderStats()
+        rdesc.outputs_on_device = 0
+        rdesc.collect_stats = int(stats)
+        self._check(self.lib.pbr_hip_render(self.ctx, C.byref(rdesc),
+                                             out_rgb.ctypes.data if rgb else None,
+                                             out_rgba.ctypes.data if rgba else None, C.byref(st)), "render")
+        return out_rgb, out_rgba, st
+
+    def render_device(self, rdesc, rgb_ptr: int, rgba_ptr: int, stream: int | None = None, stats=False):
+        """Render straight into device buffers (e.g. torch tensors' data_ptr()) on `stream`."""
+        st = capi.RenderStats()
+        rdesc.outputs_on_device = 1
+        rdesc.stream = stream
+        rdesc.collect_stats = int(stats)
+        self._check(self.lib.pbr_hip_render(self.ctx, C.byref(rdesc), rgb_ptr or None, rgba_ptr or None,
+                                            C.byref(st)), "render")
+        return st
+
+    def get_bvh(self):
+        nn, npr = C.c_int(), C.c_int()
+        self._check(self.lib.pbr_hip_get_bvh(self.ctx, None, C.byref(nn), None, C.byref(npr)), "get_bvh")
+        nodes = np.empty(nn.value * 32, dtype=np.uint8)
+        ids = np.empty(npr.value, dtype=np.int32)
+        self._check(self.lib.pbr_hip_get_bvh(self.ctx, nodes.ctypes.data, C.byref(nn), capi.iptr(ids), C.byref(npr)),
+                    "get_bvh")
+        return nodes, ids
+
+    def sampler_values(self, width, height, spp, queries, sampler=capi.SAMPLER_HALTON):
+        q = np.ascontiguousarray(queries, dtype=np.int32).reshape(-1, 4)
+        out = np.empty(q.shape[0], dtype=np.float32)
+        self._check(self.lib.pbr_hip_sampler_values(self.ctx, sampler, width, height, spp, q.shape[0], capi.iptr(q),
+                                                    capi.fptr(out)), "sampler_values")
+        return out
+
+    def camera_rays(self, cam, pfilm):
+        pf = np.ascontiguousarray(pfilm, dtype=np.float32).reshape(-1, 2)
+        out = np.empty((pf.shape[0], 6), dtype=np.float32)
+        self._check(self.lib.pbr_hip_camera_rays(self.ctx, C.byref(cam), pf.shape[0], capi.fptr(pf), capi.fptr(out)),
+                    "camera_rays")
+        return out
+
+    def intersect(self, rays, any_hit=False):
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 7)
+        out = np.empty((r.shape[0], 5), dtype=np.float32)
+        self._check(self.lib.pbr_hip_intersect(self.ctx, r.shape[0], capi.fptr(r), capi.fptr(out), int(any_hit)),
+                    "intersect")
+        return out
+
+
+def tile_grid(width, height, tile=64):
+    """64×64 pixel tiles in row-major order."""
+    return [(x, y, min(x + tile, width), min(y + tile, height))
+            for y in range(0, height, tile) for x in range(0, width, tile)]
+
+
+def tiles_for_rank(width, height, rank, world, tile=64):
+    """Round-robin tile ownership `tileId mod nGPU` so heavy regions spread over ranks."""
+    return [t for i, t in enumerate(tile_grid(width, height, tile)) if i % world == rank]
+
+
+def assemble(width, height, tiles, packed, channels):
+    """Scatter a packed per-tile buffer back into a row-major frame."""
+    frame = np.zeros((height, width, channels), dtype=packed.dtype)
+    pos = 0
+    for (x0, y0, x1, y1) in tiles:
+        n = (x1 - x0) * (y1 - y0)
+        frame[y0:y1, x0:x1] = packed[pos:pos + n].reshape(y1 - y0, x1 - x0, channels)
+        pos += n
+    return frame

@@ -1,0 +1,719 @@
+// pbr_device.h — device-side geometry, BVH traversal, BSDFs, lights and media for gfx950.
+// Everything here runs per lane on 64-wide waves; data comes from the flattened HBM layout in
+// pbr_layout.h.  The float op order of each routine follows the reference function cited next
+// to it (see pbr_math.h for the numerics contract).
+#pragma once
+#include "pbr_layout.h"
+#include "pbr_math.h"
+
+namespace pbr {
+
+struct Ray { f3 o, d; float tMax; int medium; };
+PBR_HD Ray mkray(f3 o, f3 d, float tMax, int medium) { Ray r; r.o = o; r.d = d; r.tMax = tMax; r.medium = medium; return r; }
+
+struct Counters { uint32_t rays, nodes, prims, shading; };
+
+// Interaction / SurfaceInteraction / MediumInteraction collapsed to the fields the path uses.
+struct Isect {
+    f3 p, pError, wo, n;       // n == 0 → medium interaction
+    f3 sn, dpdu;               // shading normal and shading dpdu (surfaces)
+    int slot;                  // BVH-ordered primitive slot (surfaces)
+    int medIn, medOut;
+};
+PBR_HD int get_medium(const Isect& it, f3 w) { return dot(w, it.n) > 0 ? it.medOut : it.medIn; }   // Interaction.h:48-50
+PBR_HD Ray spawn_ray(const Isect& it, f3 d) {   // Interaction.h:28-31
+    f3 o = offset_ray_origin(it.p, it.pError, it.n, d);
+    return mkray(o, d, PBR_INF, get_medium(it, d));
+}
+PBR_HD Ray spawn_ray_to(const Isect& a, f3 bp, f3 bErr, f3 bn) {   // Interaction.h:38-44
+    f3 origin = offset_ray_origin(a.p, a.pError, a.n, bp - a.p);
+    f3 target = offset_ray_origin(bp, bErr, bn, origin - bp);
+    f3 d = target - origin;
+    return mkray(origin, d, 1 - kShadowEpsilon, get_medium(a, d));
+}
+
+// ---------------------------------------------------------------- BVH node test (Geometry.h:1438-1468)
+__device__ __forceinline__ bool node_hit(float4 a, float4 b, const Ray& r, f3 inv, bool n0, bool n1, bool n2) {
+    // pMin = (a.x, a.y, a.z), pMax = (a.w, b.x, b.y)
+    float tMin = ((n0 ? a.w : a.x) - r.o.x) * inv.x;
+    float tMax = ((n0 ? a.x : a.w) - r.o.x) * inv.x;
+    float tyMin = ((n1 ? b.x : a.y) - r.o.y) * inv.y;
+    float tyMax = ((n1 ? a.y : b.x) - r.o.y) * inv.y;
+    if (tMin > tyMax || tyMin > tMax) return false;
+    if (tyMin > tMin) tMin = tyMin;
+    if (tyMax < tMax) tMax = tyMax;
+    float tzMin = ((n2 ? b.y : a.z) - r.o.z) * inv.z;
+    float tzMax = ((n2 ? a.z : b.y) - r.o.z) * inv.z;
+    if (tMin > tzMax || tzMin > tMax) return false;
+    if (tzMin > tMin) tMin = tzMin;
+    if (tzMax < tMax) tMax = tzMax;
+    return (tMin < r.tMax) && (tMax > 0);
+}
+
+// ---------------------------------------------------------------- watertight triangle (Triangle.cpp:62-206)
+__device__ __forceinline__ bool tri_test(f3 p0, f3 p1, f3 p2, const Ray& ray, float* tOut, float* b0o, float* b1o, float* b2o) {
+    f3 p0t = p0 - ray.o, p1t = p1 - ray.o, p2t = p2 - ray.o;
+    int kz = maxdim(vabs(ray.d));
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    f3 d = permute(ray.d, kx, ky, kz);
+    p0t = permute(p0t, kx, ky, kz); p1t = permute(p1t, kx, ky, kz); p2t = permute(p2t, kx, ky, kz);
+    float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1.f / d.z;
+    p0t.x += Sx * p0t.z; p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z; p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z; p2t.y += Sy * p2t.z;
+    float e0 = p1t.x * p2t.y - p1t.y * p2t.x;
+    float e1 = p2t.x * p0t.y - p2t.y * p0t.x;
+    float e2 = p0t.x * p1t.y - p0t.y * p1t.x;
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        double a = (double)p2t.x * (double)p1t.y, b = (double)p2t.y * (double)p1t.x;
+        e0 = (float)(b - a);
+        a = (double)p0t.x * (double)p2t.y; b = (double)p0t.y * (double)p2t.x;
+        e1 = (float)(b - a);
+        a = (double)p1t.x * (double)p0t.y; b = (double)p1t.y * (double)p0t.x;
+        e2 = (float)(b - a);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz; p1t.z *= Sz; p2t.z *= Sz;
+    float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < ray.tMax * det)) return false;
+    else if (det > 0 && (tScaled <= 0 || tScaled > ray.tMax * det)) return false;
+    float invDet = 1 / det;
+    float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
+    float t = tScaled * invDet;
+    float maxZt = maxcomp(vabs(mk(p0t.z, p1t.z, p2t.z)));
+    float deltaZ = gamma_n(3) * maxZt;
+    float maxXt = maxcomp(vabs(mk(p0t.x, p1t.x, p2t.x)));
+    float maxYt = maxcomp(vabs(mk(p0t.y, p1t.y, p2t.y)));
+    float deltaX = gamma_n(5) * (maxXt + maxZt);
+    float deltaY = gamma_n(5) * (maxYt + maxZt);
+    float deltaE = 2 * (gamma_n(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    float maxE = maxcomp(vabs(mk(e0, e1, e2)));
+    float deltaT = 3 * (gamma_n(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * fabsf(invDet);
+    if (t <= deltaT) return false;
+    *tOut = t; *b0o = b0; *b1o = b1; *b2o = b2;
+    return true;
+}
+
+// ---------------------------------------------------------------- sphere (reference stub F2; pbrt-v3 form)
+__device__ __forceinline__ bool sphere_test(const SphereRec& s, const Ray& r, float* tOut) {
+    f3 o = xf_point(s.w2o, r.o), d = xf_vector(s.w2o, r.d);
+    double ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z, rad = s.radius;
+    double a = dx * dx + dy * dy + dz * dz;
+    double b = 2 * (dx * ox + dy * oy + dz * oz);
+    double c = ox * ox + oy * oy + oz * oz - rad * rad;
+    double disc = b * b - 4 * a * c;
+    if (disc < 0) return false;
+    double rd = sqrt(disc);
+    double q = (b < 0) ? -0.5 * (b - rd) : -0.5 * (b + rd);
+    double t0 = q / a, t1 = c / q;
+    if (t0 > t1) { double tt = t0; t0 = t1; t1 = tt; }
+    float f0 = (float)t0, f1 = (float)t1;
+    if (f0 > r.tMax || f1 <= 0) return false;
+    float t = f0;
+    if (t <= 0) { t = f1; if (t > r.tMax) return false; }
+    *tOut = t;
+    return true;
+}
+
+struct HitRec { int slot; float b0, b1, b2; };
+
+// Triangle::Intersect's SurfaceInteraction (Triangle.cpp:148-246), no shading normals
+__device__ void triangle_si(const DeviceScene& S, int slot, const Ray& ray, float b0, float b1, float b2, int flags, Isect* si) {
+    const float4* tv = S.triVerts + 3 * (size_t)slot;
+    float4 v0 = tv[0], v1 = tv[1], v2 = tv[2];
+    f3 p0 = mk(v0.x, v0.y, v0.z), p1 = mk(v1.x, v1.y, v1.z), p2 = mk(v2.x, v2.y, v2.z);
+    float u0x = 0, u0y = 0, u1x = 1, u1y = 0, u2x = 1, u2y = 1;
+    if (flags & PRIM_HAS_UV) {
+        const float2* uv = S.triUV + 3 * (size_t)slot;
+        u0x = uv[0].x; u0y = uv[0].y; u1x = uv[1].x; u1y = uv[1].y; u2x = uv[2].x; u2y = uv[2].y;
+    }
+    float d02x = u0x - u2x, d02y = u0y - u2y, d12x = u1x - u2x, d12y = u1y - u2y;
+    f3 dp02 = p0 - p2, dp12 = p1 - p2;
+    float determinant = d02x * d12y - d02y * d12x;
+    bool degenerate = (double)fabsf(determinant) < 1e-8;
+    f3 dpdu = mk(0, 0, 0);
+    if (!degenerate) {
+        float invdet = 1 / determinant;
+        dpdu = (d12y * dp02 - d02y * dp12) * invdet;
+    }
+    float xs = (fabsf(b0 * p0.x) + fabsf(b1 * p1.x) + fabsf(b2 * p2.x));
+    float ys = (fabsf(b0 * p0.y) + fabsf(b1 * p1.y) + fabsf(b2 * p2.y));
+    float zs = (fabsf(b0 * p0.z) + fabsf(b1 * p1.z) + fabsf(b2 * p2.z));
+    si->pError = gamma_n(7) * mk(xs, ys, zs);
+    si->p = b0 * p0 + b1 * p1 + b2 * p2;
+    si->wo = normalize(-ray.d);
+    f3 n = normalize(cross(dp02, dp12));
+    if (flags & PRIM_FLIP) n = -n;
+    si->n = n;
+    si->sn = n;
+    si->dpdu = dpdu;
+}
+__device__ void sphere_si(const SphereRec& s, const Ray& r, float t, Isect* si) {
+    f3 o = xf_point(s.w2o, r.o), d = xf_vector(s.w2o, r.d);
+    f3 pHit = o + d * t;
+    pHit = pHit * (s.radius / len(pHit));
+    if (pHit.x == 0 && pHit.y == 0) pHit.x = 1e-5f * s.radius;
+    const float phiMax = 2 * kPi;
+    float zRadius = sqrtf(pHit.x * pHit.x + pHit.y * pHit.y);
+    float invZRadius = 1 / zRadius;
+    float cosPhi = pHit.x * invZRadius, sinPhi = pHit.y * invZRadius;
+    float cosTheta = clampf(pHit.z / s.radius, -1, 1);
+    float sinTheta = sqrtf(mx((float)0, 1 - cosTheta * cosTheta));
+    f3 dpdu = mk(-phiMax * pHit.y, phiMax * pHit.x, 0);
+    f3 dpdv = (-kPi) * mk(pHit.z * cosPhi, pHit.z * sinPhi, -s.radius * sinTheta);
+    f3 pw = xf_point(s.o2w, pHit);
+    f3 pErrObj = gamma_n(5) * vabs(pHit);
+    si->pError = gamma_n(6) * (vabs(pw) + pErrObj);
+    si->p = pw;
+    si->wo = normalize(-r.d);
+    f3 du = xf_vector(s.o2w, dpdu), dv = xf_vector(s.o2w, dpdv);
+    f3 n = normalize(cross(du, dv));
+    if (s.flip) n = -n;
+    si->n = n;
+    si->sn = n;
+    si->dpdu = du;
+}
+
+__device__ __forceinline__ bool prim_hit(const DeviceScene& S, int slot, const Ray& r, float* t, float* b0, float* b1, float* b2) {
+    const float4* tv = S.triVerts + 3 * (size_t)slot;
+    float4 v0 = tv[0];
+    int flags = __float_as_int(v0.w);
+    if (flags & PRIM_SPHERE) return sphere_test(S.spheres[__float_as_int(v0.x)], r, t);
+    float4 v1 = tv[1], v2 = tv[2];
+    return tri_test(mk(v0.x, v0.y, v0.z), mk(v1.x, v1.y, v1.z), mk(v2.x, v2.y, v2.z), r, t, b0, b1, b2);
+}
+
+// BVHAccel::Intersect / IntersectP (BVHAccel.cpp:285-366): the same near-first order (dirIsNeg of
+// the node's split axis) so ties between primitives resolve exactly as on the CPU (F8).
+template <bool ANY, bool STATS>
+__device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
+    if (STATS) c->rays++;
+    if (S.nNodes == 0) return false;
+    f3 inv = ANY ? mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z) : mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
+    bool n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
+    int stack[64];
+    int sp = 0, cur = 0;
+    bool found = false;
+    while (true) {
+        float4 a = S.nodes[2 * cur], b = S.nodes[2 * cur + 1];
+        if (STATS) c->nodes++;
+        if (node_hit(a, b, r, inv, n0, n1, n2)) {
+            int off = __float_as_int(b.z);
+            uint32_t meta = __float_as_uint(b.w);
+            int nprim = (int)(meta & 0xffffu);
+            if (nprim > 0) {
+                for (int i = 0; i < nprim; ++i) {
+                    float t, b0, b1, b2;
+                    if (STATS) c->prims++;
+                    if (prim_hit(S, off + i, r, &t, &b0, &b1, &b2)) {
+                        if (ANY) return true;
+                        r.tMax = t;   // GeometricPrimitive::Intersect (Primitive.cpp:26)
+                        h->slot = off + i; h->b0 = b0; h->b1 = b1; h->b2 = b2;
+                        found = true;
+                    }
+                }
+                if (sp == 0) break;
+                cur = stack[--sp];
+            } else {
+                int axis = (int)((meta >> 16) & 0xffu);
+                bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+                if (neg) { stack[sp++] = cur + 1; cur = off; }
+                else { stack[sp++] = off; cur = cur + 1; }
+            }
+        } else {
+            if (sp == 0) break;
+            cur = stack[--sp];
+        }
+    }
+    return found;
+}
+
+// Scene::Intersect + SurfaceInteraction construction for the surviving primitive.
+template <bool STATS>
+__device__ bool intersect(const DeviceScene& S, Ray& r, Isect* si, Counters* c) {
+    HitRec h;
+    if (!traverse<false, STATS>(S, r, &h, c)) return false;
+    int flags = __float_as_int(S.triVerts[3 * (size_t)h.slot].w);
+    if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)h.slot].x)], r, r.tMax, si);
+    else triangle_si(S, h.slot, r, h.b0, h.b1, h.b2, flags, si);
+    si->slot = h.slot;
+    int4 info = S.primInfo[h.slot];
+    int mi = (int)(short)(info.w & 0xffff), mo = (int)(short)((info.w >> 16) & 0xffff);
+    if (mi != mo) { si->medIn = mi; si->medOut = mo; }     // Primitive.cpp:30-34
+    else { si->medIn = r.medium; si->medOut = r.medium; }
+    return true;
+}
+
+// ---------------------------------------------------------------- BSDF (Material/Reflection.*)
+PBR_HD float cos_t(f3 w) { return w.z; }
+PBR_HD float cos2_t(f3 w) { return w.z * w.z; }
+PBR_HD float abscos_t(f3 w) { return fabsf(w.z); }
+PBR_HD float sin2_t(f3 w) { return mx((float)0, (float)1 - cos2_t(w)); }
+PBR_HD float sin_t(f3 w) { return sqrtf(sin2_t(w)); }
+PBR_HD float tan_t(f3 w) { return sin_t(w) / cos_t(w); }
+PBR_HD float tan2_t(f3 w) { return sin2_t(w) / cos2_t(w); }
+PBR_HD float cos_phi(f3 w) { float s = sin_t(w); return (s == 0) ? 1 : clampf(w.x / s, -1, 1); }
+PBR_HD float sin_phi(f3 w) { float s = sin_t(w); return (s == 0) ? 0 : clampf(w.y / s, -1, 1); }
+PBR_HD float cos2_phi(f3 w) { return cos_phi(w) * cos_phi(w); }
+PBR_HD float sin2_phi(f3 w) { return sin_phi(w) * sin_phi(w); }
+PBR_HD f3 reflect_(f3 wo, f3 n) { return -wo + 2 * dot(wo, n) * n; }
+PBR_HD bool refract_(f3 wi, f3 n, float eta, f3* wt) {
+    float cosI = dot(n, wi);
+    float sin2I = mx(float(0), float(1 - cosI * cosI));
+    float sin2T = eta * eta * sin2I;
+    if (sin2T >= 1) return false;
+    float cosT = sqrtf(1 - sin2T);
+    *wt = eta * -wi + (eta * cosI - cosT) * n;
+    return true;
+}
+PBR_HD bool same_hemi(f3 w, f3 wp) { return w.z * wp.z > 0; }
+
+PBR_HD float fr_dielectric(float cosThetaI, float etaI, float etaT) {   // Fresnel.cpp:7-28
+    cosThetaI = clampf(cosThetaI, -1, 1);
+    bool entering = cosThetaI > 0.f;
+    if (!entering) { float t = etaI; etaI = etaT; etaT = t; cosThetaI = fabsf(cosThetaI); }
+    float sinThetaI = sqrtf(mx((float)0, 1 - cosThetaI * cosThetaI));
+    float sinThetaT = etaI / etaT * sinThetaI;
+    if (sinThetaT >= 1) return 1;
+    float cosThetaT = sqrtf(mx((float)0, 1 - sinThetaT * sinThetaT));
+    float Rparl = ((etaT * cosThetaI) - (etaI * cosThetaT)) / ((etaT * cosThetaI) + (etaI * cosThetaT));
+    float Rperp = ((etaI * cosThetaI) - (etaT * cosThetaT)) / ((etaI * cosThetaI) + (etaT * cosThetaT));
+    return (Rparl * Rparl + Rperp * Rperp) / 2;
+}
+PBR_HD rgb fr_conductor(float cosThetaI, rgb etai, rgb etat, rgb k) {   // Fresnel.cpp:31-54
+    cosThetaI = clampf(cosThetaI, -1, 1);
+    rgb eta = etat / etai, etak = k / etai;
+    float c2 = cosThetaI * cosThetaI;
+    float s2 = (float)(1. - (double)c2);
+    rgb eta2 = eta * eta, etak2 = etak * etak;
+    rgb t0 = eta2 - etak2 - sp(s2);
+    rgb a2plusb2 = sqrt_s(t0 * t0 + 4.f * eta2 * etak2);
+    rgb t1 = a2plusb2 + sp(c2);
+    rgb a = sqrt_s(0.5f * (a2plusb2 + t0));
+    rgb t2 = (float)2 * cosThetaI * a;
+    rgb Rs = (t1 - t2) / (t1 + t2);
+    rgb t3 = c2 * a2plusb2 + sp(s2 * s2);
+    rgb t4 = t2 * s2;
+    rgb Rp = Rs * (t3 - t4) / (t3 + t4);
+    return 0.5f * (Rp + Rs);
+}
+PBR_HD rgb ld3(const float* v) { return sp3(v[0], v[1], v[2]); }
+PBR_HD rgb fresnel_eval(const Lobe& l, float cosI) {
+    if (l.fresnel == FR_NOOP) return sp(1.f);
+    if (l.fresnel == FR_DIEL) return sp(fr_dielectric(cosI, l.fEtaI, l.fEtaT));
+    return fr_conductor(fabsf(cosI), ld3(l.cEtaI), ld3(l.cEtaT), ld3(l.cK));
+}
+// Trowbridge-Reitz (Microfacet.cpp:116-292), sampleVisibleArea = true
+PBR_HD float tr_D(const Lobe& l, f3 wh) {
+    float t2 = tan2_t(wh);
+    if (is_inf(t2)) return 0.;
+    const float c4 = cos2_t(wh) * cos2_t(wh);
+    float e = (cos2_phi(wh) / (l.ax * l.ax) + sin2_phi(wh) / (l.ay * l.ay)) * t2;
+    return 1 / (kPi * l.ax * l.ay * c4 * (1 + e) * (1 + e));
+}
+PBR_HD float tr_lambda(const Lobe& l, f3 w) {
+    float at = fabsf(tan_t(w));
+    if (is_inf(at)) return 0.;
+    float alpha = sqrtf(cos2_phi(w) * l.ax * l.ax + sin2_phi(w) * l.ay * l.ay);
+    float a2t2 = (alpha * at) * (alpha * at);
+    return (-1 + sqrtf(1.f + a2t2)) / 2;
+}
+PBR_HD float tr_G1(const Lobe& l, f3 w) { return 1 / (1 + tr_lambda(l, w)); }
+PBR_HD float tr_G(const Lobe& l, f3 wo, f3 wi) { return 1 / (1 + tr_lambda(l, wo) + tr_lambda(l, wi)); }
+PBR_HD void tr_sample11(float cosTheta, float U1, float U2, float* sx, float* sy) {
+    if ((double)cosTheta > .9999) {   // the reference's unqualified sqrt/cos/sin resolve to double
+        float r = (float)sqrt((double)(U1 / (1 - U1)));
+        float phi = (float)(6.28318530718 * (double)U2);
+        *sx = (float)((double)r * cos((double)phi));
+        *sy = (float)((double)r * sin((double)phi));
+        return;
+    }
+    float sinTheta = sqrtf(mx((float)0, (float)1 - cosTheta * cosTheta));
+    float tanTheta = sinTheta / cosTheta;
+    float a = 1 / tanTheta;
+    float G1 = 2 / (1 + sqrtf(1.f + 1.f / (a * a)));
+    float A = 2 * U1 / G1 - 1;
+    float tmp = 1.f / (A * A - 1.f);
+    if ((double)tmp > 1e10) tmp = 1e10f;
+    float B = tanTheta;
+    float D = sqrtf(mx(float(B * B * tmp * tmp - (A * A - B * B) * tmp), float(0)));
+    float s1 = B * tmp - D, s2 = B * tmp + D;
+    *sx = (A < 0 || s2 > 1.f / tanTheta) ? s1 : s2;
+    float S;
+    if (U2 > 0.5f) { S = 1.f; U2 = 2.f * (U2 - .5f); }
+    else { S = -1.f; U2 = 2.f * (.5f - U2); }
+    float z = (U2 * (U2 * (U2 * 0.27385f - 0.73369f) + 0.46341f)) /
+              (U2 * (U2 * (U2 * 0.093073f + 0.309420f) - 1.000000f) + 0.597999f);
+    *sy = S * z * sqrtf(1.f + *sx * *sx);
+}
+PBR_HD f3 tr_sample_wh(const Lobe& l, f3 wo, float u0, float u1) {
+    bool flip = wo.z < 0;
+    f3 wi = flip ? -wo : wo;
+    f3 ws = normalize(mk(l.ax * wi.x, l.ay * wi.y, wi.z));
+    float sx, sy;
+    tr_sample11(cos_t(ws), u0, u1, &sx, &sy);
+    float tmp = cos_phi(ws) * sx - sin_phi(ws) * sy;
+    sy = sin_phi(ws) * sx + cos_phi(ws) * sy;
+    sx = tmp;
+    sx = l.ax * sx;
+    sy = l.ay * sy;
+    f3 wh = normalize(mk(-sx, -sy, 1.f));
+    if (flip) wh = -wh;
+    return wh;
+}
+PBR_HD float tr_pdf(const Lobe& l, f3 wo, f3 wh) { return tr_D(l, wh) * tr_G1(l, wo) * absdot(wo, wh) / abscos_t(wo); }
+
+PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
+    switch (l.kind) {
+    case L_LAMBERT: return ld3(l.R) * kInvPi;
+    case L_OREN: {
+        float sI = sin_t(wi), sO = sin_t(wo);
+        float maxCos = 0;
+        if ((double)sI > 1e-4 && (double)sO > 1e-4) {
+            float dCos = cos_phi(wi) * cos_phi(wo) + sin_phi(wi) * sin_phi(wo);
+            maxCos = mx((float)0, dCos);
+        }
+        float sinAlpha, tanBeta;
+        if (abscos_t(wi) > abscos_t(wo)) { sinAlpha = sO; tanBeta = sI / abscos_t(wi); }
+        else { sinAlpha = sI; tanBeta = sO / abscos_t(wo); }
+        return ld3(l.R) * kInvPi * (l.A + l.B * maxCos * sinAlpha * tanBeta);
+    }
+    case L_MF_R: {
+        float cO = abscos_t(wo), cI = abscos_t(wi);
+        f3 wh = wi + wo;
+        if (cI == 0 || cO == 0) return sp(0.f);
+        if (wh.x == 0 && wh.y == 0 && wh.z == 0) return sp(0.f);
+        wh = normalize(wh);
+        rgb F = fresnel_eval(l, dot(wi, faceforward(wh, mk(0, 0, 1))));
+        return ld3(l.R) * tr_D(l, wh) * tr_G(l, wo, wi) * F / (4 * cI * cO);
+    }
+    case L_MF_T: {
+        if (same_hemi(wo, wi)) return sp(0.f);
+        float cO = cos_t(wo), cI = cos_t(wi);
+        if (cI == 0 || cO == 0) return sp(0.f);
+        float eta = cos_t(wo) > 0 ? (l.etaB / l.etaA) : (l.etaA / l.etaB);
+        f3 wh = normalize(wo + wi * eta);
+        if (wh.z < 0) wh = -wh;
+        if (dot(wo, wh) * dot(wi, wh) > 0) return sp(0.f);
+        rgb F = sp(fr_dielectric(dot(wo, wh), l.etaA, l.etaB));
+        float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+        float factor = 1 / eta;
+        return (sp(1.f) - F) * ld3(l.T) *
+               fabsf(tr_D(l, wh) * tr_G(l, wo, wi) * eta * eta * absdot(wi, wh) * absdot(wo, wh) * factor * factor /
+                     (cI * cO * sqrtDenom * sqrtDenom));
+    }
+    default: return sp(0.f);
+    }
+}
+PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
+    switch (l.kind) {
+    case L_LAMBERT: case L_OREN: return same_hemi(wo, wi) ? abscos_t(wi) * kInvPi : 0;
+    case L_MF_R: {
+        if (!same_hemi(wo, wi)) return 0;
+        f3 wh = normalize(wo + wi);
+        return tr_pdf(l, wo, wh) / (4 * dot(wo, wh));
+    }
+    case L_MF_T: {
+        if (same_hemi(wo, wi)) return 0;
+        float eta = cos_t(wo) > 0 ? (l.etaB / l.etaA) : (l.etaA / l.etaB);
+        f3 wh = normalize(wo + wi * eta);
+        if (dot(wo, wh) * dot(wi, wh) > 0) return 0;
+        float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+        float dwh = fabsf((eta * eta * dot(wi, wh)) / (sqrtDenom * sqrtDenom));
+        return tr_pdf(l, wo, wh) * dwh;
+    }
+    default: return 0;
+    }
+}
+// Sampling.cpp:74-92, Sampling.h:57-61
+PBR_HD void concentric_disk(float u0, float u1, float* dx, float* dy) {
+    float ox = 2.f * u0 - 1, oy = 2.f * u1 - 1;
+    if (ox == 0 && oy == 0) { *dx = 0; *dy = 0; return; }
+    float theta, r;
+    if (fabsf(ox) > fabsf(oy)) { r = ox; theta = kPiOver4 * (oy / ox); }
+    else { r = oy; theta = kPiOver2 - kPiOver4 * (ox / oy); }
+    *dx = r * t_cos(theta);
+    *dy = r * t_sin(theta);
+}
+PBR_HD f3 cosine_hemisphere(float u0, float u1) {
+    float dx, dy;
+    concentric_disk(u0, u1, &dx, &dy);
+    float z = sqrtf(mx((float)0, 1 - dx * dx - dy * dy));
+    return mk(dx, dy, z);
+}
+PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* pdf, int* st) {
+    switch (l.kind) {
+    case L_LAMBERT: case L_OREN: {
+        *wi = cosine_hemisphere(u0, u1);
+        if (wo.z < 0) wi->z *= -1;
+        *pdf = lobe_pdf(l, wo, *wi);
+        return lobe_f(l, wo, *wi);
+    }
+    case L_SPEC_R: {
+        *wi = mk(-wo.x, -wo.y, wo.z);
+        *pdf = 1;
+        return fresnel_eval(l, cos_t(*wi)) * ld3(l.R) / abscos_t(*wi);
+    }
+    case L_SPEC_T: {
+        bool entering = cos_t(wo) > 0;
+        float etaI = entering ? l.etaA : l.etaB, etaT = entering ? l.etaB : l.etaA;
+        if (!refract_(wo, faceforward(mk(0, 0, 1), wo), etaI / etaT, wi)) return sp(0.f);
+        *pdf = 1;
+        rgb ft = ld3(l.T) * (sp(1.f) - sp(fr_dielectric(cos_t(*wi), l.etaA, l.etaB)));
+        ft = ft * ((etaI * etaI) / (etaT * etaT));
+        return ft / abscos_t(*wi);
+    }
+    case L_FRESNEL_SPEC: {
+        float F = fr_dielectric(cos_t(wo), l.etaA, l.etaB);
+        if (u0 < F) {
+            *wi = mk(-wo.x, -wo.y, wo.z);
+            *st = BSDF_SPECULAR | BSDF_REFLECTION;
+            *pdf = F;
+            return F * ld3(l.R) / abscos_t(*wi);
+        }
+        bool entering = cos_t(wo) > 0;
+        float etaI = entering ? l.etaA : l.etaB, etaT = entering ? l.etaB : l.etaA;
+        if (!refract_(wo, faceforward(mk(0, 0, 1), wo), etaI / etaT, wi)) return sp(0.f);
+        rgb ft = ld3(l.T) * (1 - F);
+        ft = ft * ((etaI * etaI) / (etaT * etaT));
+        *st = BSDF_SPECULAR | BSDF_TRANSMISSION;
+        *pdf = 1 - F;
+        return ft / abscos_t(*wi);
+    }
+    case L_MF_R: {
+        if (wo.z == 0) return sp(0.f);
+        f3 wh = tr_sample_wh(l, wo, u0, u1);
+        if (dot(wo, wh) < 0) return sp(0.f);
+        *wi = reflect_(wo, wh);
+        if (!same_hemi(wo, *wi)) return sp(0.f);
+        *pdf = tr_pdf(l, wo, wh) / (4 * dot(wo, wh));
+        return lobe_f(l, wo, *wi);
+    }
+    case L_MF_T: {
+        if (wo.z == 0) return sp(0.f);
+        f3 wh = tr_sample_wh(l, wo, u0, u1);
+        if (dot(wo, wh) < 0) return sp(0.f);
+        float eta = cos_t(wo) > 0 ? (l.etaA / l.etaB) : (l.etaB / l.etaA);
+        if (!refract_(wo, wh, eta, wi)) return sp(0.f);
+        *pdf = lobe_pdf(l, wo, *wi);
+        return lobe_f(l, wo, *wi);
+    }
+    }
+    return sp(0.f);
+}
+
+struct BSDF {                    // Reflection.h:101-149: frame + the material's lobe template
+    f3 ns, ng, ss, ts;
+    const MatTemplate* mt;
+    PBR_HD f3 to_local(f3 v) const { return mk(dot(v, ss), dot(v, ts), dot(v, ns)); }
+    PBR_HD f3 to_world(f3 v) const {
+        return mk(ss.x * v.x + ts.x * v.y + ns.x * v.z, ss.y * v.x + ts.y * v.y + ns.y * v.z, ss.z * v.x + ts.z * v.y + ns.z * v.z);
+    }
+};
+PBR_HD bool matches(const Lobe& l, int t) { return (l.type & t) == l.type; }
+PBR_HD int num_components(const BSDF& b, int flags) {
+    int k = 0;
+    for (int i = 0; i < b.mt->nLobes; ++i) if (matches(b.mt->lobes[i], flags)) ++k;
+    return k;
+}
+PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:56-71
+    f3 wi = b.to_local(wiW), wo = b.to_local(woW);
+    if (wo.z == 0) return sp(0.f);
+    bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    rgb f = sp(0.f);
+    for (int i = 0; i < b.mt->nLobes; ++i) {
+        const Lobe& l = b.mt->lobes[i];
+        if (matches(l, flags) && ((reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION))))
+            f = f + lobe_f(l, wo, wi);
+    }
+    return f;
+}
+PBR_HD float bsdf_pdf(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:92-106
+    if (b.mt->nLobes == 0) return 0.f;
+    f3 wo = b.to_local(woW), wi = b.to_local(wiW);
+    if (wo.z == 0) return 0.f;
+    float pdf = 0.f;
+    int m = 0;
+    for (int i = 0; i < b.mt->nLobes; ++i)
+        if (matches(b.mt->lobes[i], flags)) { ++m; pdf += lobe_pdf(b.mt->lobes[i], wo, wi); }
+    return m > 0 ? pdf / m : 0.f;
+}
+// Reflection.cpp:108-164. On the wo.z == 0 early-out *pdf and *sampledType are left as they were.
+PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float* pdf, int type, int* sampledType) {
+    int m = num_components(b, type);
+    if (m == 0) { *pdf = 0; *sampledType = 0; return sp(0.f); }
+    int comp = (int)floorf(u0 * m);
+    if (comp > m - 1) comp = m - 1;
+    int chosen = -1, count = comp;
+    for (int i = 0; i < b.mt->nLobes; ++i)
+        if (matches(b.mt->lobes[i], type) && count-- == 0) { chosen = i; break; }
+    const Lobe& bx = b.mt->lobes[chosen];
+    float ur0 = mn(u0 * m - comp, kOneMinusEpsilon);
+    f3 wi, wo = b.to_local(woW);
+    if (wo.z == 0) return sp(0.f);
+    *pdf = 0;
+    int st = bx.type;
+    rgb f = lobe_sample(bx, wo, &wi, ur0, u1, pdf, &st);
+    *sampledType = st;
+    if (*pdf == 0) { *sampledType = 0; return sp(0.f); }
+    *wiW = b.to_world(wi);
+    if (!(bx.type & BSDF_SPECULAR) && m > 1)
+        for (int i = 0; i < b.mt->nLobes; ++i)
+            if (i != chosen && matches(b.mt->lobes[i], type)) *pdf += lobe_pdf(b.mt->lobes[i], wo, wi);
+    if (m > 1) *pdf /= m;
+    if (!(bx.type & BSDF_SPECULAR)) {
+        bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
+        f = sp(0.f);
+        for (int i = 0; i < b.mt->nLobes; ++i) {
+            const Lobe& l = b.mt->lobes[i];
+            if (matches(l, type) && ((reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION))))
+                f = f + lobe_f(l, wo, wi);
+        }
+    }
+    return f;
+}
+// SurfaceInteraction::ComputeScatteringFunctions → BSDF(si, eta) frame (Reflection.h:105-110)
+__device__ __forceinline__ bool make_bsdf(const DeviceScene& S, const Isect& si, bool multiLobe, BSDF* b) {
+    int mat = S.primInfo[si.slot].y;
+    if (mat < 0) return false;
+    const MatTemplate* mt = S.materials + 2 * mat + (multiLobe ? 1 : 0);
+    if (!mt->valid) return false;
+    b->mt = mt;
+    b->ns = si.sn;
+    b->ng = si.n;
+    b->ss = normalize(si.dpdu);
+    b->ts = cross(b->ns, b->ss);
+    return true;
+}
+
+// ---------------------------------------------------------------- lights (Light/*.cpp)
+PBR_HD rgb area_L(const DLight& l, f3 n, f3 w) { return (l.twoSided || dot(n, w) > 0) ? ld3(l.L) : sp(0.f); }
+PBR_HD void sphere_uv(f3 p, float* u, float* v) {   // SkyBoxLight.cpp:12-17
+    float phi = t_atan2(p.z, p.x);
+    float theta = t_asin(p.y);
+    *u = 1 - (phi + kPi) * kInv2Pi;
+    *v = (theta + kPiOver2) * kInvPi;
+}
+__device__ __forceinline__ rgb sky_value(const DeviceScene& S, const DLight& l, float u, float v) {   // SkyBoxLight.cpp:27-40
+    u = clampf(u, 0.f, 1.f);
+    v = clampf(v, 0.f, 1.f);
+    int w = u * l.envW, h = v * l.envH;
+    w = clampi(w, 0, l.envW - 1);
+    h = clampi(h, 0, l.envH - 1);
+    float4 t = S.env[w + h * l.envW];   // HDRtoLDR already applied at upload
+    return sp3(t.x, t.y, t.z);
+}
+__device__ __forceinline__ rgb light_Le(const DeviceScene& S, const DLight& l, const Ray& r) {
+    if (l.type == LT_SKY) {
+        f3 dn = normalize(r.d);
+        float u, v;
+        sphere_uv(dn, &u, &v);
+        if (l.envW > 0) return sky_value(S, l, u, v);
+        return sp(0.f);
+    }
+    return sp(0.8f);   // Light::Le default (Light.h:58, F4)
+}
+PBR_HD f3 uniform_sphere(float u0, float u1) {   // Sampling.cpp:59-64
+    float z = 1 - 2 * u0;
+    float r = sqrtf(mx((float)0, (float)1 - z * z));
+    float phi = 2 * kPi * u1;
+    return mk(r * t_cos(phi), r * t_sin(phi), z);
+}
+struct VisPt { f3 p, pError, n; int medIn, medOut; };
+__device__ __forceinline__ void tri_verts(const DeviceScene& S, int slot, f3* p0, f3* p1, f3* p2) {
+    const float4* tv = S.triVerts + 3 * (size_t)slot;
+    float4 a = tv[0], b = tv[1], c = tv[2];
+    *p0 = mk(a.x, a.y, a.z); *p1 = mk(b.x, b.y, b.z); *p2 = mk(c.x, c.y, c.z);
+}
+__device__ rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref, float u0, float u1, f3* wi, float* pdf, VisPt* v) {
+    if (l.type == LT_POINT) {   // PointLight.cpp:5-15
+        f3 pl = mk(l.p[0], l.p[1], l.p[2]);
+        *wi = normalize(pl - ref.p);
+        *pdf = 1.f;
+        v->p = pl; v->pError = mk(0, 0, 0); v->n = mk(0, 0, 0); v->medIn = l.medIn; v->medOut = l.medOut;
+        f3 dd = pl - ref.p;
+        return ld3(l.L) / len2(dd);
+    }
+    if (l.type == LT_AREA) {    // DiffuseLight.cpp:25-40, Shape.cpp:18-30, Triangle.cpp:360-387
+        f3 p0, p1, p2;
+        tri_verts(S, l.primSlot, &p0, &p1, &p2);
+        float su0 = sqrtf(u0);
+        float b0 = 1 - su0, b1 = u1 * su0;
+        f3 ip = b0 * p0 + b1 * p1 + (1 - b0 - b1) * p2;
+        f3 in = normalize(cross(p1 - p0, p2 - p0));
+        int flags = __float_as_int(S.triVerts[3 * (size_t)l.primSlot].w);
+        if (flags & PRIM_FLIP) in = in * -1.f;
+        f3 pAbs = vabs(b0 * p0) + vabs(b1 * p1) + vabs((1 - b0 - b1) * p2);
+        f3 ipErr = gamma_n(6) * pAbs;
+        float area = (float)(0.5 * (double)len(cross(p1 - p0, p2 - p0)));
+        *pdf = 1 / area;
+        f3 w = ip - ref.p;
+        if (len2(w) == 0) *pdf = 0;
+        else {
+            w = normalize(w);
+            *pdf *= len2(ref.p - ip) / absdot(in, -w);
+            if (is_inf(*pdf)) *pdf = 0.f;
+        }
+        if (*pdf == 0 || len2(ip - ref.p) == 0) { *pdf = 0; return sp(0.f); }
+        *wi = normalize(ip - ref.p);
+        v->p = ip; v->pError = ipErr; v->n = in; v->medIn = -1; v->medOut = -1;
+        return area_L(l, in, -*wi);
+    }
+    // SkyBoxLight::Sample_Li (SkyBoxLight.cpp:43-56)
+    *wi = uniform_sphere(u0, u1);
+    *pdf = 1.f / (4 * kPi);
+    v->p = ref.p + *wi * (2 * l.worldRadius); v->pError = mk(0, 0, 0); v->n = mk(0, 0, 0); v->medIn = -1; v->medOut = -1;
+    float ul, vl;
+    sphere_uv(normalize(*wi), &ul, &vl);
+    if (l.envW <= 0) return sp(0.f);
+    return sky_value(S, l, ul, vl);
+}
+// Shape::Pdf through the light's own triangle (Shape.cpp:31-42); 0 for point and skybox lights
+__device__ float pdf_li(const DeviceScene& S, const DLight& l, const Isect& ref, f3 wi) {
+    if (l.type != LT_AREA) return 0;
+    Ray ray = spawn_ray(ref, wi);
+    f3 p0, p1, p2;
+    tri_verts(S, l.primSlot, &p0, &p1, &p2);
+    float t, b0, b1, b2;
+    if (!tri_test(p0, p1, p2, ray, &t, &b0, &b1, &b2)) return 0;
+    Isect li;
+    int flags = __float_as_int(S.triVerts[3 * (size_t)l.primSlot].w);
+    triangle_si(S, l.primSlot, ray, b0, b1, b2, flags, &li);
+    float area = (float)(0.5 * (double)len(cross(p1 - p0, p2 - p0)));
+    float pdf = len2(ref.p - li.p) / (absdot(li.n, -wi) * area);
+    if (is_inf(pdf)) pdf = 0.f;
+    return pdf;
+}
+__device__ __forceinline__ rgb si_Le(const DeviceScene& S, const Isect& si, f3 w) {   // Interaction.cpp:116-119
+    int al = S.primInfo[si.slot].z;
+    return al >= 0 ? area_L(S.lights[al], si.n, w) : sp(0.f);
+}
+
+// ---------------------------------------------------------------- media (Media/*.cpp)
+PBR_HD float phase_hg(float cosTheta, float g) {   // Medium.h:24-27
+    float denom = 1 + g * g + 2 * g * cosTheta;
+    return kInv4Pi * (1 - g * g) / (denom * sqrtf(denom));
+}
+PBR_HD float hg_sample(float g, f3 wo, f3* wi, float u0, float u1) {   // Medium.cpp:9-26
+    float cosTheta;
+    if ((double)fabsf(g) < 1e-3) cosTheta = 1 - 2 * u0;
+    else {
+        float sq = (1 - g * g) / (1 + g - 2 * g * u0);
+        cosTheta = -(1 + g * g - sq * sq) / (2 * g);
+    }
+    float sinTheta = sqrtf(mx((float)0, 1 - cosTheta * cosTheta));
+    float phi = 2 * kPi * u1;
+    f3 v1, v2;
+    coordinate_system(wo, &v1, &v2);
+    *wi = spherical_direction(sinTheta, cosTheta, phi, v1, v2, wo);
+    return phase_hg(cosTheta, g);
+}
+__device__ __forceinline__ rgb medium_tr(const DeviceScene& S, int m, const Ray& ray) {   // HomogeneousMedium.cpp:10-12
+    const float* md = S.media + 10 * m;
+    return exp_s(sp3(-md[6], -md[7], -md[8]) * mn(ray.tMax * len(ray.d), kMaxFloat));
+}
+
+}  // namespace pbr

@@ -1,0 +1,878 @@
+// pbr_kernels.hip — MI355X (gfx950) render path: sampler, camera, Whitted/Path/VolPath integrators
+// and the film, behind the C-ABI of include/pbr_hip.h.
+//
+// Work decomposition.  One lane traces one camera sample (pixel, sample index); a 256-lane
+// workgroup owns a run of whole pixels (4 pixels × 64 spp at the 1080p config, i.e. one pixel per
+// wave, which keeps primary rays and their shadow rays coherent inside a wave).  Per-sample
+// radiance is staged in LDS and summed per pixel in sample order, so the float sum is
+// bit-identical to the reference's `colObj += Li` loop (Integrator.cpp:303-313), then the output
+// transform runs in the same kernel (no second pass over HBM).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/pbr_hip.h"
+#include "pbr_device.h"
+#include "pbr_scene.h"
+
+using namespace pbr;
+
+namespace {
+
+// ---------------------------------------------------------------- sampler (Sampler/Sampler.cpp)
+struct SState { uint32_t index; int dim; };
+
+__host__ __device__ __forceinline__ HaltonParams hparams(const DeviceSampler& s) {
+    HaltonParams h;
+    h.baseExp0 = s.baseExp0; h.baseExp1 = s.baseExp1; h.baseScale1 = s.baseScale1; h.stride = s.stride;
+    h.mult0 = s.mult0; h.mult1 = s.mult1; h.scaleRatio0 = s.ratio0; h.scaleRatio1 = s.ratio1;
+    return h;
+}
+
+__device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int dim) {
+    // HaltonSampler::SampleDimension (Halton.cpp:83-92)
+    if (dim == 0) return radical_inverse_2(index >> s.baseExp0);
+    if (dim == 1) return radical_inverse_b(3u, 0x55555555u, div_prime(index, (uint32_t)s.baseScale1, 0xffffffffu / (uint32_t)s.baseScale1));
+    if (dim >= 1000) return 0.f;
+    return scrambled_radical_inverse(s.primes[dim], s.recips[dim], s.perms + s.primeSums[dim], index);
+}
+// GlobalSampler::Get1D/Get2D (Sampler.cpp:131-143): with no requested sample arrays
+// arrayStartDim == arrayEndDim == 5, so only a Get2D that would straddle dimension 5 is moved.
+__device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) { return sample_dimension(s, st.index, st.dim++); }
+__device__ __forceinline__ void get2d(const DeviceSampler& s, SState& st, float* a, float* b) {
+    if (st.dim == 4) st.dim = 5;
+    *a = sample_dimension(s, st.index, st.dim);
+    *b = sample_dimension(s, st.index, st.dim + 1);
+    st.dim += 2;
+}
+
+// ---------------------------------------------------------------- camera (Perspective.cpp:44-80)
+__device__ __forceinline__ Ray camera_ray(const DeviceCamera& c, float fx, float fy, float l0, float l1) {
+    f3 pCam = xf_point(c.rasterToCamera, mk(fx, fy, 0));
+    f3 dir = normalize(pCam);
+    Ray r = mkray(mk(0, 0, 0), dir, PBR_INF, -1);
+    if (c.lensRadius > 0) {
+        float dx, dy;
+        concentric_disk(l0, l1, &dx, &dy);
+        float lx = c.lensRadius * dx, ly = c.lensRadius * dy;
+        float ft = c.focalDistance / r.d.z;
+        f3 pFocus = r.o + r.d * ft;
+        r.o = mk(lx, ly, 0);
+        r.d = normalize(pFocus - r.o);
+    }
+    // CameraToWorld drops the medium (F12)
+    return mkray(xf_point(c.cameraToWorld, r.o), xf_vector(c.cameraToWorld, r.d), r.tMax, -1);
+}
+
+struct KParams {
+    DeviceScene S;
+    DeviceSampler smp;
+    DeviceCamera cam;
+    int integrator, maxDepth;
+    float rrThreshold;
+    int spp, ppb;              // samples per pixel, pixels per workgroup
+    long long nPixels;
+    const int4* tiles;         // x0 y0 x1 y1
+    const long long* tileStart;
+    int nTiles;
+    float* rgbOut;
+    uint8_t* rgbaOut;
+    unsigned long long* stats; // rays, nodes, prims, shading
+};
+
+// ---------------------------------------------------------------- direct lighting (Integrator.cpp:46-177)
+template <bool STATS>
+__device__ bool unoccluded(const DeviceScene& S, const Isect& p0, const VisPt& p1, Counters* c) {   // Light.cpp:19-22
+    Ray r = spawn_ray_to(p0, p1.p, p1.pError, p1.n);
+    HitRec h;
+    return !traverse<true, STATS>(S, r, &h, c);
+}
+template <bool STATS>
+__device__ rgb vis_tr(const DeviceScene& S, const Isect& p0, const VisPt& p1, Counters* c) {   // Light.cpp:31-47
+    Ray ray = spawn_ray_to(p0, p1.p, p1.pError, p1.n);
+    rgb Tr = sp(1.f);
+    for (int guard = 0; guard < 256; ++guard) {
+        Isect isect;
+        bool hit = intersect<STATS>(S, ray, &isect, c);
+        if (hit && S.primInfo[isect.slot].y >= 0) return sp(0.0f);
+        if (ray.medium >= 0) Tr = Tr * medium_tr(S, ray.medium, ray);
+        if (!hit) break;
+        ray = spawn_ray_to(isect, p1.p, p1.pError, p1.n);
+    }
+    return Tr;
+}
+
+template <bool STATS>
+__device__ rgb estimate_direct(const KParams& P, const Isect& it, const BSDF* bsdf, float g, float uS0, float uS1, int li,
+                               float uL0, float uL1, bool handleMedia, Counters* c) {
+    const DeviceScene& S = P.S;
+    const DLight& light = S.lights[li];
+    const bool delta = light.type == LT_POINT;
+    const int flags = BSDF_ALL & ~BSDF_SPECULAR;
+    const bool surface = !is_zero(it.n);
+    rgb Ld = sp(0.f);
+    f3 wi = mk(0, 0, 0);
+    float lightPdf = 0, scatteringPdf = 0;
+    VisPt vis;
+    rgb Li = sample_li(S, light, it, uL0, uL1, &wi, &lightPdf, &vis);
+    if (lightPdf > 0 && !black(Li)) {
+        rgb f;
+        if (surface) {
+            f = bsdf_f(*bsdf, it.wo, wi, flags) * absdot(wi, it.sn);
+            scatteringPdf = bsdf_pdf(*bsdf, it.wo, wi, flags);
+        } else {
+            f = sp(phase_hg(dot(it.wo, wi), g));
+        }
+        if (!black(f)) {
+            if (handleMedia) Li = Li * vis_tr<STATS>(S, it, vis, c);
+            else if (!unoccluded<STATS>(S, it, vis, c)) Li = sp(0.f);
+            if (!black(Li)) {
+                if (delta) Ld = Ld + f * Li / lightPdf;
+                else {
+                    float fp = 1 * lightPdf, gp = 1 * scatteringPdf;
+                    float weight = (fp * fp) / (fp * fp + gp * gp);
+                    Ld = Ld + f * Li * weight / lightPdf;
+                }
+            }
+        }
+    }
+    if (!delta) {
+        rgb f;
+        bool sampledSpecular = false;
+        if (surface) {
+            int st = 0;
+            f = bsdf_sample(*bsdf, it.wo, &wi, uS0, uS1, &scatteringPdf, flags, &st);
+            f = f * absdot(wi, it.sn);
+            sampledSpecular = (st & BSDF_SPECULAR) != 0;
+        } else {
+            float p = hg_sample(g, it.wo, &wi, uS0, uS1);
+            f = sp(p);
+            scatteringPdf = p;
+        }
+        if (!black(f) && scatteringPdf > 0) {
+            float weight = 1;
+            if (!sampledSpecular) {
+                lightPdf = pdf_li(S, light, it, wi);
+                if (lightPdf == 0) return Ld;
+                float fp = 1 * scatteringPdf, gp = 1 * lightPdf;
+                weight = (fp * fp) / (fp * fp + gp * gp);
+            }
+            Isect lightIsect;
+            Ray ray = spawn_ray(it, wi);
+            bool found = intersect<STATS>(S, ray, &lightIsect, c);
+            rgb Li2 = sp(0.f);
+            if (found) {
+                if (S.primInfo[lightIsect.slot].z == li) Li2 = si_Le(S, lightIsect, -wi);
+            } else {
+                Li2 = light_Le(S, light, ray);
+            }
+            if (!black(Li2)) Ld = Ld + f * Li2 * weight / scatteringPdf;
+        }
+    }
+    return Ld;
+}
+
+// Distribution1D::SampleDiscrete over the lights (Sampling.h:96-107)
+__device__ __forceinline__ int sample_light(const DeviceScene& S, float u, float* pdf) {
+    int size = S.nLights + 1;
+    int first = 0, len_ = size;
+    while (len_ > 0) {
+        int half = len_ >> 1, middle = first + half;
+        if (S.lightCdf[middle] <= u) { first = middle + 1; len_ -= half + 1; }
+        else len_ = half;
+    }
+    int off = clampi(first - 1, 0, size - 2);
+    *pdf = (S.lightFuncInt > 0) ? S.lightFunc[off] / (S.lightFuncInt * S.nLights) : 0;
+    return off;
+}
+template <bool STATS>
+__device__ rgb uniform_sample_one_light(const KParams& P, const Isect& it, const BSDF* bsdf, float g, SState& st,
+                                        bool handleMedia, Counters* c) {
+    if (P.S.nLights == 0) return sp(0.f);
+    float lightPdf;
+    int li = sample_light(P.S, get1d(P.smp, st), &lightPdf);
+    if (lightPdf == 0) return sp(0.f);
+    float uL0, uL1, uS0, uS1;
+    get2d(P.smp, st, &uL0, &uL1);
+    get2d(P.smp, st, &uS0, &uS1);
+    return estimate_direct<STATS>(P, it, bsdf, g, uS0, uS1, li, uL0, uL1, handleMedia, c) / lightPdf;
+}
+
+// ---------------------------------------------------------------- Whitted (WhittedIntegrator.cpp:11-65)
+// The recursion L_k = A_k + ((f_k · L_{k+1}) · c_k) / pdf_k is unrolled into a bounded loop; the
+// per-level terms are kept and folded back deepest-first so the float result equals the
+// recursive evaluation.
+constexpr int kMaxWhittedDepth = 16;
+template <bool STATS>
+__device__ rgb whitted_li(const KParams& P, Ray ray, SState& st, Counters* c) {
+    const DeviceScene& S = P.S;
+    rgb A[kMaxWhittedDepth], F[kMaxWhittedDepth];
+    float CC[kMaxWhittedDepth], PD[kMaxWhittedDepth];
+    int depth = 0;
+    rgb Llast;
+    for (int guard = 0;; ++guard) {
+        Isect isect;
+        if (!intersect<STATS>(S, ray, &isect, c)) {
+            rgb L = sp(0.f);
+            for (int i = 0; i < S.nLights; ++i) L = L + light_Le(S, S.lights[i], ray);
+            Llast = L;
+            break;
+        }
+        if (STATS) c->shading++;
+        f3 n = isect.sn, wo = isect.wo;
+        BSDF bsdf;
+        if (!make_bsdf(S, isect, false, &bsdf)) {
+            if (guard > 1024) { Llast = sp(0.f); break; }
+            ray = spawn_ray(isect, ray.d);     // Li(isect.SpawnRay(ray.d), depth)
+            continue;
+        }
+        rgb L = sp(0.f);
+        L = L + si_Le(S, isect, wo);
+        for (int i = 0; i < S.nLights; ++i) {
+            f3 wi;
+            float pdf;
+            VisPt vis;
+            float u0, u1;
+            get2d(P.smp, st, &u0, &u1);
+            rgb Li = sample_li(S, S.lights[i], isect, u0, u1, &wi, &pdf, &vis);
+            if (black(Li) || pdf == 0) continue;
+            rgb f = bsdf_f(bsdf, wo, wi, BSDF_ALL);
+            if (!black(f) && unoccluded<STATS>(S, isect, vis, c)) L = L + f * Li * absdot(wi, n) / pdf;
+        }
+        if (depth + 1 < P.maxDepth && depth + 1 < kMaxWhittedDepth) {   // SpecularReflect (Integrator.cpp:179-222)
+            f3 wi = mk(0, 0, 0);
+            float pdf = 0;
+            int stype = 0;
+            float u0, u1;
+            get2d(P.smp, st, &u0, &u1);
+            rgb f = bsdf_sample(bsdf, wo, &wi, u0, u1, &pdf, BSDF_REFLECTION | BSDF_SPECULAR, &stype);
+            if (!black(f) && pdf > 0.f && absdot(wi, isect.sn) != 0.f) {
+                A[depth] = L; F[depth] = f; CC[depth] = absdot(wi, isect.sn); PD[depth] = pdf;
+                ray = spawn_ray(isect, wi);
+                ++depth;
+                continue;
+            }
+        }
+        Llast = L + sp(0.f);
+        break;
+    }
+    for (int k = depth - 1; k >= 0; --k) Llast = A[k] + F[k] * Llast * CC[k] / PD[k];
+    return Llast;
+}
+
+// ---------------------------------------------------------------- Path (PathIntegrator.cpp:32-110)
+template <bool STATS>
+__device__ rgb path_li(const KParams& P, Ray ray, SState& st, Counters* c) {
+    const DeviceScene& S = P.S;
+    rgb L = sp(0.f), beta = sp(1.f);
+    bool specularBounce = false;
+    float etaScale = 1;
+    for (int bounces = 0;; ++bounces) {
+        Isect isect;
+        bool found = intersect<STATS>(S, ray, &isect, c);
+        if (bounces == 0 || specularBounce) {
+            if (found) L = L + beta * si_Le(S, isect, -ray.d);
+            else for (int i = 0; i < S.nInfinite; ++i) L = L + beta * light_Le(S, S.lights[S.infinite[i]], ray);
+        }
+        if (!found || bounces >= P.maxDepth) break;
+        if (STATS) c->shading++;
+        BSDF bsdf;
+        if (!make_bsdf(S, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
+        if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0) {
+            rgb Ld = beta * uniform_sample_one_light<STATS>(P, isect, &bsdf, 0.f, st, false, c);
+            L = L + Ld;
+        }
+        f3 wo = -ray.d, wi = mk(0, 0, 0);
+        float pdf = 0;
+        int flags = 0;
+        float u0, u1;
+        get2d(P.smp, st, &u0, &u1);
+        rgb f = bsdf_sample(bsdf, wo, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
+        if (black(f) || pdf == 0.f) break;
+        beta = beta * (f * absdot(wi, isect.sn) / pdf);
+        specularBounce = (flags & BSDF_SPECULAR) != 0;
+        if ((flags & BSDF_SPECULAR) && (flags & BSDF_TRANSMISSION)) {
+            float eta = bsdf.mt->eta;
+            etaScale *= (dot(wo, isect.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+        }
+        ray = spawn_ray(isect, wi);
+        rgb rrBeta = beta * etaScale;
+        if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
+            float q = mx((float).05, 1 - maxval(rrBeta));
+            if (get1d(P.smp, st) < q) break;
+            beta = beta / (1 - q);
+        }
+    }
+    return L;
+}
+
+// ---------------------------------------------------------------- VolPath (VolPathIntegrator.cpp:21-107)
+template <bool STATS>
+__device__ rgb volpath_li(const KParams& P, Ray ray, SState& st, Counters* c) {
+    const DeviceScene& S = P.S;
+    rgb L = sp(0.f), beta = sp(1.f);
+    bool specularBounce = false;
+    float etaScale = 1;
+    for (int bounces = 0;; ++bounces) {
+        Isect isect;
+        bool found = intersect<STATS>(S, ray, &isect, c);
+        bool mediumEvent = false;
+        Isect mi;
+        float g = 0;
+        if (ray.medium >= 0) {   // HomogeneousMedium::Sample (HomogeneousMedium.cpp:15-45)
+            const float* md = S.media + 10 * ray.medium;
+            int channel = (int)(get1d(P.smp, st) * 3);
+            if (channel > 2) channel = 2;
+            float dist = -t_log(1 - get1d(P.smp, st)) / md[6 + channel];
+            float t = mn(dist / len(ray.d), ray.tMax);
+            bool sampled = t < ray.tMax;
+            if (sampled) {
+                mi.p = ray.o + ray.d * t; mi.wo = -ray.d; mi.n = mk(0, 0, 0); mi.pError = mk(0, 0, 0);
+                mi.medIn = mi.medOut = ray.medium; mi.slot = -1;
+                g = md[9];
+                mediumEvent = true;
+            }
+            rgb Tr = exp_s(sp3(-md[6], -md[7], -md[8]) * mn(t, kMaxFloat) * len(ray.d));
+            rgb density = sampled ? (sp3(md[6], md[7], md[8]) * Tr) : Tr;
+            float pdf = 0;
+            pdf += density.r; pdf += density.g; pdf += density.b;
+            pdf *= 1 / (float)3;
+            if (pdf == 0) pdf = 1;
+            beta = beta * (sampled ? (Tr * sp3(md[3], md[4], md[5]) / pdf) : (Tr / pdf));
+        }
+        if (black(beta)) break;
+        if (mediumEvent) {
+            if (bounces >= P.maxDepth) break;
+            if (STATS) c->shading++;
+            L = L + beta * uniform_sample_one_light<STATS>(P, mi, nullptr, g, st, true, c);
+            f3 wo = -ray.d, wi;
+            float u0, u1;
+            get2d(P.smp, st, &u0, &u1);
+            hg_sample(g, wo, &wi, u0, u1);
+            ray = spawn_ray(mi, wi);
+            specularBounce = false;
+        } else {
+            if (bounces == 0 || specularBounce) {
+                if (found) L = L + beta * si_Le(S, isect, -ray.d);
+                else for (int i = 0; i < S.nInfinite; ++i) L = L + beta * light_Le(S, S.lights[S.infinite[i]], ray);
+            }
+            if (!found || bounces >= P.maxDepth) break;
+            if (STATS) c->shading++;
+            BSDF bsdf;
+            if (!make_bsdf(S, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
+            L = L + beta * uniform_sample_one_light<STATS>(P, isect, &bsdf, 0.f, st, true, c);
+            f3 wo = -ray.d, wi = mk(0, 0, 0);
+            float pdf = 0;
+            int flags = 0;
+            float u0, u1;
+            get2d(P.smp, st, &u0, &u1);
+            rgb f = bsdf_sample(bsdf, wo, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
+            if (black(f) || pdf == 0.f) break;
+            beta = beta * (f * absdot(wi, isect.sn) / pdf);
+            specularBounce = (flags & BSDF_SPECULAR) != 0;
+            if ((flags & BSDF_SPECULAR) && (flags & BSDF_TRANSMISSION)) {
+                float eta = bsdf.mt->eta;
+                etaScale *= (dot(wo, isect.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+            }
+            ray = spawn_ray(isect, wi);
+        }
+        rgb rrBeta = beta * etaScale;
+        if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
+            float q = mx((float).05, 1 - maxval(rrBeta));
+            if (get1d(P.smp, st) < q) break;
+            beta = beta / (1 - q);
+        }
+    }
+    return L;
+}
+
+__device__ __forceinline__ void pixel_xy(const KParams& P, long long q, int* x, int* y) {
+    int lo = 0, hi = P.nTiles - 1;
+    while (lo < hi) {   // last tile with start <= q
+        int mid = (lo + hi + 1) >> 1;
+        if (P.tileStart[mid] <= q) lo = mid; else hi = mid - 1;
+    }
+    int4 t = P.tiles[lo];
+    long long local = q - P.tileStart[lo];
+    int w = t.z - t.x;
+    *x = t.x + (int)(local % w);
+    *y = t.y + (int)(local / w);
+}
+
+// Output transform (Integrator.cpp:313-344): average, XYZ round trip, sRGB gamma, 8-bit.
+__device__ __forceinline__ void film_out(const KParams& P, long long q, rgb col) {
+    col = col / (float)P.spp;
+    if (P.rgbOut) { P.rgbOut[3 * q] = col.r; P.rgbOut[3 * q + 1] = col.g; P.rgbOut[3 * q + 2] = col.b; }
+    if (P.rgbaOut) {
+        float X = 0.412453f * col.r + 0.357580f * col.g + 0.180423f * col.b;
+        float Y = 0.212671f * col.r + 0.715160f * col.g + 0.072169f * col.b;
+        float Z = 0.019334f * col.r + 0.119193f * col.g + 0.950227f * col.b;
+        float o[3];
+        o[0] = 3.240479f * X - 1.537150f * Y - 0.498535f * Z;
+        o[1] = -0.969256f * X + 1.875991f * Y + 0.041556f * Z;
+        o[2] = 0.055648f * X - 0.204043f * Y + 1.057311f * Z;
+        uint32_t packed = 0xff000000u;
+        for (int k = 0; k < 3; ++k) {
+            float v = o[k];
+            float gc = (v <= 0.0031308f) ? 12.92f * v : 1.055f * t_pow(v, (1.f / 2.4f)) - 0.055f;
+            float b = clampf(255.f * gc + 0.5f, 0.f, 255.f);
+            packed |= ((uint32_t)(int)b & 0xffu) << (8 * k);
+        }
+        reinterpret_cast<uint32_t*>(P.rgbaOut)[q] = packed;
+    }
+}
+
+template <int INTEGRATOR, bool STATS>
+__global__ __launch_bounds__(256) void k_render(KParams P) {
+    __shared__ float lds[256 * 3];
+    const int tid = threadIdx.x;
+    const long long pixBase = (long long)blockIdx.x * P.ppb;
+    long long rem = P.nPixels - pixBase;
+    const int npix = rem < P.ppb ? (int)rem : P.ppb;
+    if (npix <= 0) return;
+    const int spp = P.spp;
+    const int total = npix * spp;
+    Counters cnt = {0, 0, 0, 0};
+    rgb acc = sp(0.0f);
+    for (int base = 0; base < total; base += 256) {
+        int slot = base + tid;
+        rgb L = sp(0.f);
+        if (slot < total) {
+            int lp = slot / spp, s = slot - lp * spp;
+            int x, y;
+            pixel_xy(P, pixBase + lp, &x, &y);
+            // GlobalSampler::StartPixel/SetSampleNumber (Sampler.cpp:97-130)
+            SState st;
+            st.index = halton_pixel_offset(hparams(P.smp), x, y) +
+                       (uint32_t)s * (uint32_t)P.smp.stride;
+            st.dim = 0;
+            // GetCameraSample (Sampler.cpp:10-21): pFilm, time, pLens
+            float u0, u1, l0, l1;
+            get2d(P.smp, st, &u0, &u1);
+            get1d(P.smp, st);
+            get2d(P.smp, st, &l0, &l1);
+            Ray r = camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
+            if (INTEGRATOR == PBR_INTEGRATOR_WHITTED) L = whitted_li<STATS>(P, r, st, &cnt);
+            else if (INTEGRATOR == PBR_INTEGRATOR_PATH) L = path_li<STATS>(P, r, st, &cnt);
+            else L = volpath_li<STATS>(P, r, st, &cnt);
+        }
+        lds[3 * tid] = L.r; lds[3 * tid + 1] = L.g; lds[3 * tid + 2] = L.b;
+        __syncthreads();
+        if (tid < npix) {
+            int lo = tid * spp > base ? tid * spp : base;
+            int hi = (tid + 1) * spp < base + 256 ? (tid + 1) * spp : base + 256;
+            for (int k = lo; k < hi; ++k) {
+                int j = k - base;
+                acc = acc + sp3(lds[3 * j], lds[3 * j + 1], lds[3 * j + 2]);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid < npix) film_out(P, pixBase + tid, acc);
+    if (STATS) {
+        atomicAdd(&P.stats[0], (unsigned long long)cnt.rays);
+        atomicAdd(&P.stats[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&P.stats[2], (unsigned long long)cnt.prims);
+        atomicAdd(&P.stats[3], (unsigned long long)cnt.shading);
+    }
+}
+
+// ---------------------------------------------------------------- introspection kernels
+__global__ void k_sampler_values(DeviceSampler smp, HaltonParams hp, int n, const int32_t* q, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t idx = halton_pixel_offset(hp, q[4 * i], q[4 * i + 1]) + (uint32_t)q[4 * i + 2] * (uint32_t)hp.stride;
+    out[i] = sample_dimension(smp, idx, q[4 * i + 3]);
+}
+__global__ void k_camera_rays(DeviceCamera cam, int n, const float* pf, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r = camera_ray(cam, pf[2 * i], pf[2 * i + 1], 0.5f, 0.5f);
+    out[6 * i] = r.o.x; out[6 * i + 1] = r.o.y; out[6 * i + 2] = r.o.z;
+    out[6 * i + 3] = r.d.x; out[6 * i + 4] = r.d.y; out[6 * i + 5] = r.d.z;
+}
+__global__ void k_intersect(DeviceScene S, const int32_t* primIds, int n, const float* rays, float* out, int any) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* rr = rays + 7 * i;
+    Ray r = mkray(mk(rr[0], rr[1], rr[2]), mk(rr[3], rr[4], rr[5]), rr[6], -1);
+    HitRec h;
+    Counters c;
+    float* o = out + 5 * i;
+    if (any) {
+        o[0] = traverse<true, false>(S, r, &h, &c) ? 1.f : 0.f;
+        o[1] = o[2] = o[3] = o[4] = 0.f;
+    } else {
+        bool hit = traverse<false, false>(S, r, &h, &c);
+        o[0] = hit ? 1.f : 0.f;
+        o[1] = hit ? r.tMax : 0.f;
+        o[2] = hit ? (float)primIds[h.slot] : -1.f;
+        o[3] = hit ? h.b1 : 0.f;
+        o[4] = hit ? h.b2 : 0.f;
+    }
+}
+
+}  // namespace
+
+// ======================================================================== C-ABI
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    template <class T> hipError_t upload(const std::vector<T>& v, hipStream_t s) {
+        hipError_t e = ensure(v.size() * sizeof(T));
+        if (e != hipSuccess || v.empty()) return e;
+        return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+    }
+};
+
+struct pbr_hip_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    bool haveScene = false;
+    HostScene host;
+    HaltonTables halton;
+    DevBuf dNodes, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
+    DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
+    DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
+    int curStrategy = PBR_LIGHTS_UNIFORM;
+    float funcInt = 0;
+};
+
+namespace {
+
+int set_err(pbr_hip_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return set_err(ctx, PBR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+DeviceScene device_scene(pbr_hip_ctx* ctx) {
+    const HostScene& h = ctx->host;
+    DeviceScene S;
+    std::memset(&S, 0, sizeof(S));
+    S.nodes = (const float4*)ctx->dNodes.p;
+    S.triVerts = (const float4*)ctx->dTri.p;
+    S.primInfo = (const int4*)ctx->dInfo.p;
+    S.triUV = h.triUV.empty() ? nullptr : (const float2*)ctx->dUV.p;
+    S.spheres = (const SphereRec*)ctx->dSph.p;
+    S.materials = (const MatTemplate*)ctx->dMat.p;
+    S.lights = (const DLight*)ctx->dLights.p;
+    S.env = h.env.empty() ? nullptr : (const float4*)ctx->dEnv.p;
+    S.nNodes = (int)h.nodes.size();
+    S.nPrims = (int)h.primIds.size();
+    S.nLights = (int)h.lights.size();
+    S.nMaterials = (int)h.materials.size() / 2;
+    S.envLight = h.envLight;
+    S.nInfinite = (int)h.infinite.size();
+    for (int i = 0; i < S.nInfinite && i < 4; ++i) S.infinite[i] = h.infinite[i];
+    S.lightCdf = (const float*)ctx->dCdf.p;
+    S.lightFunc = (const float*)ctx->dFunc.p;
+    S.lightFuncInt = ctx->funcInt;
+    S.media = (const float*)ctx->dMedia.p;
+    S.nMedia = (int)h.media.size() / 10;
+    return S;
+}
+
+DeviceSampler device_sampler(pbr_hip_ctx* ctx, int type, int spp, int w, int h) {
+    DeviceSampler s;
+    std::memset(&s, 0, sizeof(s));
+    s.type = type;
+    s.spp = spp;
+    halton_params(w, h, &s);
+    s.primes = (const uint32_t*)ctx->dPrimes.p;
+    s.recips = (const uint32_t*)ctx->dRecips.p;
+    s.primeSums = (const uint32_t*)ctx->dPrimeSums.p;
+    s.perms = (const uint16_t*)ctx->dPerms.p;
+    return s;
+}
+
+int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
+    std::vector<float> cdf, func;
+    float fi = 0;
+    light_distribution(ctx->host, strategy, &cdf, &func, &fi);
+    if (func.empty()) func.push_back(0.f);
+    HIP_TRY(ctx->dCdf.upload(cdf, ctx->stream));
+    HIP_TRY(ctx->dFunc.upload(func, ctx->stream));
+    ctx->funcInt = fi;
+    ctx->curStrategy = strategy;
+    return PBR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbr_hip_abi_version(void) { return PBR_HIP_ABI_VERSION; }
+const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 megakernel r1"; }
+
+int pbr_hip_create(int device, pbr_hip_ctx** out) {
+    if (!out) return PBR_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return PBR_E_NODEVICE;
+    if (device < 0 || device >= n) return PBR_E_INVALID;
+    std::unique_ptr<pbr_hip_ctx> ctx(new pbr_hip_ctx);
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess) return PBR_E_HIP;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return PBR_E_HIP;
+    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return PBR_E_HIP;
+    build_halton_tables(1000, &ctx->halton);
+    pbr_hip_ctx* c = ctx.get();
+    {
+        pbr_hip_ctx* ctx = c;   // for HIP_TRY
+        HIP_TRY(ctx->dPrimes.upload(ctx->halton.primes, ctx->stream));
+        HIP_TRY(ctx->dRecips.upload(ctx->halton.recips, ctx->stream));
+        HIP_TRY(ctx->dPrimeSums.upload(ctx->halton.primeSums, ctx->stream));
+        HIP_TRY(ctx->dPerms.upload(ctx->halton.perms, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    *out = ctx.release();
+    return PBR_OK;
+}
+
+int pbr_hip_destroy(pbr_hip_ctx* ctx) {
+    if (!ctx) return PBR_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    hipStream_t s = ctx->stream;
+    delete ctx;
+    if (s) (void)hipStreamDestroy(s);
+    return PBR_OK;
+}
+
+const char* pbr_hip_last_error(const pbr_hip_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
+    if (!ctx) return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    try {
+        build_host_scene(desc, &ctx->host);
+    } catch (const std::exception& e) {
+        ctx->haveScene = false;
+        return set_err(ctx, PBR_E_INVALID, e.what());
+    }
+    const HostScene& h = ctx->host;
+    HIP_TRY(ctx->dNodes.upload(h.nodes, ctx->stream));
+    HIP_TRY(ctx->dTri.upload(h.triVerts, ctx->stream));
+    HIP_TRY(ctx->dInfo.upload(h.primInfo, ctx->stream));
+    HIP_TRY(ctx->dUV.upload(h.triUV, ctx->stream));
+    HIP_TRY(ctx->dSph.upload(h.spheres, ctx->stream));
+    HIP_TRY(ctx->dMat.upload(h.materials, ctx->stream));
+    HIP_TRY(ctx->dLights.upload(h.lights, ctx->stream));
+    HIP_TRY(ctx->dEnv.upload(h.env, ctx->stream));
+    HIP_TRY(ctx->dMedia.upload(h.media, ctx->stream));
+    HIP_TRY(ctx->dPrimIds.upload(h.primIds, ctx->stream));
+    int rc = upload_light_distribution(ctx, PBR_LIGHTS_UNIFORM);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->haveScene = true;
+    return PBR_OK;
+}
+
+int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, uint8_t* rgba_out, pbr_render_stats* stats) {
+    if (!ctx) return PBR_E_INVALID;
+    if (!d) return set_err(ctx, PBR_E_INVALID, "null render desc");
+    if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    if (d->spp <= 0) return set_err(ctx, PBR_E_INVALID, "spp must be positive");
+    if (d->max_depth < 0) return set_err(ctx, PBR_E_INVALID, "max_depth must be >= 0");
+    if (d->integrator < PBR_INTEGRATOR_WHITTED || d->integrator > PBR_INTEGRATOR_VOLPATH)
+        return set_err(ctx, PBR_E_INVALID, "unknown integrator");
+    if (d->sampler != PBR_SAMPLER_HALTON) return set_err(ctx, PBR_E_UNSUPPORTED, "only the Halton sampler is available in this build");
+    if ((long long)d->spp * (long long)31104 >= (1ll << 32)) return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
+    auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = d->stream ? (hipStream_t)d->stream : ctx->stream;
+
+    KParams P;
+    std::memset(&P, 0, sizeof(P));
+    try {
+        build_camera(&d->camera, &P.cam);
+    } catch (const std::exception& e) {
+        return set_err(ctx, PBR_E_INVALID, e.what());
+    }
+    if (d->light_strategy != ctx->curStrategy) {
+        int rc = upload_light_distribution(ctx, d->light_strategy);
+        if (rc) return rc;
+    }
+    P.S = device_scene(ctx);
+    P.smp = device_sampler(ctx, d->sampler, d->spp, d->camera.width, d->camera.height);
+    P.integrator = d->integrator;
+    P.maxDepth = d->max_depth;
+    P.rrThreshold = d->rr_threshold;
+    P.spp = d->spp;
+    P.ppb = d->spp >= 256 ? 1 : 256 / d->spp;
+    // tiles
+    std::vector<int32_t> tiles;
+    std::vector<long long> starts;
+    long long npx = 0;
+    if (d->n_tiles > 0) {
+        if (!d->tiles) return set_err(ctx, PBR_E_INVALID, "tiles == NULL");
+        for (int i = 0; i < d->n_tiles; ++i) {
+            const pbr_tile& t = d->tiles[i];
+            if (t.x0 < 0 || t.y0 < 0 || t.x1 > d->camera.width || t.y1 > d->camera.height || t.x1 <= t.x0 || t.y1 <= t.y0)
+                return set_err(ctx, PBR_E_INVALID, "tile outside the raster");
+            tiles.insert(tiles.end(), {t.x0, t.y0, t.x1, t.y1});
+            starts.push_back(npx);
+            npx += (long long)(t.x1 - t.x0) * (t.y1 - t.y0);
+        }
+    } else {
+        tiles = {0, 0, d->camera.width, d->camera.height};
+        starts.push_back(0);
+        npx = (long long)d->camera.width * d->camera.height;
+    }
+    HIP_TRY(ctx->dTiles.upload(tiles, s));
+    HIP_TRY(ctx->dTileStart.upload(starts, s));
+    P.tiles = (const int4*)ctx->dTiles.p;
+    P.tileStart = (const long long*)ctx->dTileStart.p;
+    P.nTiles = (int)starts.size();
+    P.nPixels = npx;
+    // outputs
+    if (d->outputs_on_device) {
+        P.rgbOut = rgb_out;
+        P.rgbaOut = rgba_out;
+    } else {
+        if (rgb_out) { HIP_TRY(ctx->dRgb.ensure((size_t)npx * 12)); P.rgbOut = (float*)ctx->dRgb.p; }
+        if (rgba_out) { HIP_TRY(ctx->dRgba.ensure((size_t)npx * 4)); P.rgbaOut = (uint8_t*)ctx->dRgba.p; }
+    }
+    if (d->collect_stats) {
+        HIP_TRY(ctx->dStats.ensure(4 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(ctx->dStats.p, 0, 4 * sizeof(unsigned long long), s));
+        P.stats = (unsigned long long*)ctx->dStats.p;
+    }
+    long long blocks = (npx + P.ppb - 1) / P.ppb;
+    if (blocks > 0x7fffffffLL) return set_err(ctx, PBR_E_UNSUPPORTED, "frame too large");
+    dim3 grid((unsigned)blocks), block(256);
+    HIP_TRY(hipEventRecord(ctx->ev0, s));
+    if (blocks > 0) {
+        bool st = d->collect_stats != 0;
+        switch (d->integrator) {
+        case PBR_INTEGRATOR_WHITTED:
+            if (st) hipLaunchKernelGGL((k_render<PBR_INTEGRATOR_WHITTED, true>), grid, block, 0, s, P);
+            else hipLaunchKernelGGL((k_render<PBR_INTEGRATOR_WHITTED, false>), grid, block, 0, s, P);
+            break;
+        case PBR_INTEGRATOR_PATH:
+            if (st) hipLaunchKernelGGL((k_render<PBR_INTEGRATOR_PATH, true>), grid, block, 0, s, P);
+            else hipLaunchKernelGGL((k_render<PBR_INTEGRATOR_PATH, false>), grid, block, 0, s, P);
+            break;
+        default:
+            if (st) hipLaunchKernelGGL((k_render<PBR_INTEGRATOR_VOLPATH, true>), grid, block, 0, s, P);
+            else hipLaunchKernelGGL((k_render<PBR_INTEGRATOR_VOLPATH, false>), grid, block, 0, s, P);
+            break;
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(ctx->ev1, s));
+    if (!d->outputs_on_device) {
+        if (rgb_out) HIP_TRY(hipMemcpyAsync(rgb_out, P.rgbOut, (size_t)npx * 12, hipMemcpyDeviceToHost, s));
+        if (rgba_out) HIP_TRY(hipMemcpyAsync(rgba_out, P.rgbaOut, (size_t)npx * 4, hipMemcpyDeviceToHost, s));
+    }
+    unsigned long long hs[4] = {0, 0, 0, 0};
+    if (d->collect_stats) HIP_TRY(hipMemcpyAsync(hs, ctx->dStats.p, sizeof(hs), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    auto t1 = std::chrono::steady_clock::now();
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+        stats->kernel_ms = ms;
+        stats->film_ms = 0;
+        stats->seconds = std::chrono::duration<double>(t1 - t0).count();
+        stats->samples = (uint64_t)npx * (uint64_t)d->spp;
+        stats->rays = hs[0];
+        stats->node_visits = hs[1];
+        stats->prim_tests = hs[2];
+        stats->shading_events = hs[3];
+        stats->n_launches = blocks > 0 ? 1 : 0;
+    }
+    return PBR_OK;
+}
+
+int pbr_hip_get_bvh(pbr_hip_ctx* ctx, void* nodes_out, int* n_nodes, int32_t* prim_ids_out, int* n_prims) {
+    if (!ctx) return PBR_E_INVALID;
+    if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    const HostScene& h = ctx->host;
+    if (n_nodes) *n_nodes = (int)h.nodes.size();
+    if (n_prims) *n_prims = (int)h.primIds.size();
+    if (nodes_out) {   // read back what the device traverses
+        HIP_TRY(hipMemcpy(nodes_out, ctx->dNodes.p, h.nodes.size() * sizeof(LinearBVHNode), hipMemcpyDeviceToHost));
+    }
+    if (prim_ids_out) std::memcpy(prim_ids_out, h.primIds.data(), h.primIds.size() * sizeof(int32_t));
+    return PBR_OK;
+}
+
+int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height, int spp, int n, const int32_t* q, float* out) {
+    if (!ctx || !q || !out || n < 0 || width <= 0 || height <= 0) return PBR_E_INVALID;
+    if (sampler != PBR_SAMPLER_HALTON) return set_err(ctx, PBR_E_UNSUPPORTED, "only Halton");
+    HIP_TRY(hipSetDevice(ctx->device));
+    DeviceSampler s = device_sampler(ctx, sampler, spp, width, height);
+    HaltonParams hp = hparams(s);
+    HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 16));
+    HIP_TRY(ctx->dScratchOut.ensure((size_t)n * 4));
+    HIP_TRY(hipMemcpyAsync(ctx->dScratchIn.p, q, (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (n > 0) hipLaunchKernelGGL(k_sampler_values, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, s, hp, n,
+                                  (const int32_t*)ctx->dScratchIn.p, (float*)ctx->dScratchOut.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->dScratchOut.p, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PBR_OK;
+}
+
+int pbr_hip_camera_rays(pbr_hip_ctx* ctx, const pbr_camera_desc* cam, int n, const float* pf, float* out) {
+    if (!ctx || !cam || !pf || !out || n < 0) return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    DeviceCamera dc;
+    try {
+        build_camera(cam, &dc);
+    } catch (const std::exception& e) {
+        return set_err(ctx, PBR_E_INVALID, e.what());
+    }
+    HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 8));
+    HIP_TRY(ctx->dScratchOut.ensure((size_t)n * 24));
+    HIP_TRY(hipMemcpyAsync(ctx->dScratchIn.p, pf, (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (n > 0) hipLaunchKernelGGL(k_camera_rays, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dc, n,
+                                  (const float*)ctx->dScratchIn.p, (float*)ctx->dScratchOut.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->dScratchOut.p, (size_t)n * 24, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PBR_OK;
+}
+
+int pbr_hip_intersect(pbr_hip_ctx* ctx, int n, const float* rays, float* out, int any_hit) {
+    if (!ctx || !rays || !out || n < 0) return PBR_E_INVALID;
+    if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 28));
+    HIP_TRY(ctx->dScratchOut.ensure((size_t)n * 20));
+    HIP_TRY(hipMemcpyAsync(ctx->dScratchIn.p, rays, (size_t)n * 28, hipMemcpyHostToDevice, ctx->stream));
+    DeviceScene S = device_scene(ctx);
+    if (n > 0) hipLaunchKernelGGL(k_intersect, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, S,
+                                  (const int32_t*)ctx->dPrimIds.p, n, (const float*)ctx->dScratchIn.p,
+                                  (float*)ctx->dScratchOut.p, any_hit);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->dScratchOut.p, (size_t)n * 20, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PBR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,686 @@
+// pbr_scene.cpp — host half of pbr_hip_upload_scene: turns the reference-shaped scene descriptor
+// into the flattened HBM layout (pbr_layout.h).
+//
+// The BVH must come out node-for-node identical to BVHAccel (Accelerator/BVHAccel.cpp:57-283):
+// the F8 tie rule (later primitive wins on t == tMax) makes the traversal order — and so the
+// topology — observable in the image.  The builder below is iterative and writes nodes directly
+// in depth-first preorder (the reference's flatten order), but performs the same bucket SAH,
+// the same std::partition / std::nth_element calls on the same element order, so the layout is
+// identical.
+#include "pbr_scene.h"
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+
+namespace pbr {
+
+namespace {
+
+struct Box {
+    f3 lo, hi;
+    Box() {
+        float big = std::numeric_limits<float>::max(), low = std::numeric_limits<float>::lowest();
+        lo = mk(big, big, big);
+        hi = mk(low, low, low);
+    }
+    void add(f3 p) { lo = vmin(lo, p); hi = vmax(hi, p); }
+    void add(const Box& b) { lo = vmin(lo, b.lo); hi = vmax(hi, b.hi); }
+    float area() const { f3 d = hi - lo; return 2 * (d.x * d.y + d.x * d.z + d.y * d.z); }
+    int longest() const {
+        f3 d = hi - lo;
+        if (d.x > d.y && d.x > d.z) return 0;
+        if (d.y > d.z) return 1;
+        return 2;
+    }
+    float rel(f3 p, int axis) const {   // Bounds3::Offset(p)[axis]
+        float o = get(p, axis) - get(lo, axis);
+        float ext_hi = get(hi, axis), ext_lo = get(lo, axis);
+        if (ext_hi > ext_lo) o /= ext_hi - ext_lo;
+        return o;
+    }
+};
+
+struct Item {                 // BVHPrimitiveInfo
+    size_t id;
+    Box box;
+    f3 c;
+};
+
+// Row-major 4x4 helpers for the camera/transform math (Core/Transform.*).
+struct Mat { float a[4][4]; };
+Mat identity() { Mat m; for (int i = 0; i < 4; ++i) for (int j = 0; j < 4; ++j) m.a[i][j] = i == j ? 1.f : 0.f; return m; }
+Mat from_rows(const float* r) { Mat m; std::memcpy(m.a, r, 64); return m; }
+Mat mul(const Mat& x, const Mat& y) {
+    Mat r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            r.a[i][j] = x.a[i][0] * y.a[0][j] + x.a[i][1] * y.a[1][j] + x.a[i][2] * y.a[2][j] + x.a[i][3] * y.a[3][j];
+    return r;
+}
+// Gauss-Jordan elimination with full pivoting, float arithmetic (Transform.cpp:59-130)
+Mat invert(const Mat& in) {
+    int colOf[4], rowOf[4], used[4] = {0, 0, 0, 0};
+    float w[4][4];
+    std::memcpy(w, in.a, 64);
+    for (int step = 0; step < 4; ++step) {
+        int prow = 0, pcol = 0;
+        float best = 0.f;
+        for (int r = 0; r < 4; ++r) {
+            if (used[r] == 1) continue;
+            for (int c = 0; c < 4; ++c)
+                if (used[c] == 0 && std::fabs(w[r][c]) >= best) { best = std::fabs(w[r][c]); prow = r; pcol = c; }
+        }
+        ++used[pcol];
+        if (prow != pcol) for (int c = 0; c < 4; ++c) std::swap(w[prow][c], w[pcol][c]);
+        rowOf[step] = prow;
+        colOf[step] = pcol;
+        float inv = 1. / w[pcol][pcol];
+        w[pcol][pcol] = 1.;
+        for (int c = 0; c < 4; ++c) w[pcol][c] *= inv;
+        for (int r = 0; r < 4; ++r) {
+            if (r == pcol) continue;
+            float f = w[r][pcol];
+            w[r][pcol] = 0;
+            for (int c = 0; c < 4; ++c) w[r][c] -= w[pcol][c] * f;
+        }
+    }
+    for (int k = 3; k >= 0; --k)
+        if (rowOf[k] != colOf[k])
+            for (int r = 0; r < 4; ++r) std::swap(w[r][rowOf[k]], w[r][colOf[k]]);
+    Mat m;
+    std::memcpy(m.a, w, 64);
+    return m;
+}
+struct Xf { Mat m, mi; };
+Xf compose(const Xf& x, const Xf& y) { return Xf{mul(x.m, y.m), mul(y.mi, x.mi)}; }   // Transform::operator*
+Xf inverse(const Xf& x) { return Xf{x.mi, x.m}; }
+Xf scale(float x, float y, float z) {
+    Xf t{identity(), identity()};
+    t.m.a[0][0] = x; t.m.a[1][1] = y; t.m.a[2][2] = z;
+    t.mi.a[0][0] = 1 / x; t.mi.a[1][1] = 1 / y; t.mi.a[2][2] = 1 / z;
+    return t;
+}
+Xf translate(f3 d) {
+    Xf t{identity(), identity()};
+    t.m.a[0][3] = d.x; t.m.a[1][3] = d.y; t.m.a[2][3] = d.z;
+    t.mi.a[0][3] = -d.x; t.mi.a[1][3] = -d.y; t.mi.a[2][3] = -d.z;
+    return t;
+}
+Xf perspective(float fovDeg, float n, float f) {   // Transform.cpp:257-264
+    Mat p = identity();
+    p.a[2][2] = f / (f - n);
+    p.a[2][3] = -f * n / (f - n);
+    p.a[3][2] = 1;
+    p.a[3][3] = 0;
+    float half = ((kPi / 180) * fovDeg) / 2;
+    float invTanAng = 1 / (float)tan((double)half);
+    return compose(scale(invTanAng, invTanAng, 1), Xf{p, invert(p)});
+}
+Xf look_at(f3 pos, f3 look, f3 up) {   // Transform.cpp:208-239 (world → camera)
+    Mat c = identity();
+    c.a[0][3] = pos.x; c.a[1][3] = pos.y; c.a[2][3] = pos.z; c.a[3][3] = 1;
+    f3 dir = normalize(look - pos);
+    if (len(cross(normalize(up), dir)) == 0) return Xf{identity(), identity()};
+    f3 right = normalize(cross(normalize(up), dir));
+    f3 newUp = cross(dir, right);
+    c.a[0][0] = right.x; c.a[1][0] = right.y; c.a[2][0] = right.z; c.a[3][0] = 0.;
+    c.a[0][1] = newUp.x; c.a[1][1] = newUp.y; c.a[2][1] = newUp.z; c.a[3][1] = 0.;
+    c.a[0][2] = dir.x; c.a[1][2] = dir.y; c.a[2][2] = dir.z; c.a[3][2] = 0.;
+    return Xf{invert(c), c};
+}
+bool swaps_handedness(const Mat& m) {   // Transform.cpp:144-150
+    float det = m.a[0][0] * (m.a[1][1] * m.a[2][2] - m.a[1][2] * m.a[2][1]) -
+                m.a[0][1] * (m.a[1][0] * m.a[2][2] - m.a[1][2] * m.a[2][0]) +
+                m.a[0][2] * (m.a[1][0] * m.a[2][1] - m.a[1][1] * m.a[2][0]);
+    return det < 0;
+}
+
+struct PrimRef { int shape, tri; };
+
+void fail(const std::string& why) { throw std::invalid_argument(why); }
+
+// Bucketed SAH builder writing LinearBVHNodes in depth-first preorder.
+class SahBuilder {
+  public:
+    SahBuilder(std::vector<Item>& items, int maxPrims, std::vector<LinearBVHNode>* nodes, std::vector<int32_t>* order)
+        : it_(items), maxPrims_(std::min(255, maxPrims)), nodes_(nodes), order_(order) {}
+
+    void run() {
+        nodes_->clear();
+        order_->clear();
+        if (it_.empty()) return;
+        // explicit DFS: each task is (start, end, parentIndexToPatch or -1)
+        struct Task { int start, end, patch; };
+        std::vector<Task> todo;
+        todo.push_back({0, (int)it_.size(), -1});
+        while (!todo.empty()) {
+            Task t = todo.back();
+            todo.pop_back();
+            int me = (int)nodes_->size();
+            nodes_->push_back(LinearBVHNode());
+            if (t.patch >= 0) (*nodes_)[t.patch].offset = me;   // secondChildOffset
+            int mid, axis;
+            Box box;
+            if (!split(t.start, t.end, &mid, &axis, &box)) {
+                emit_leaf(me, t.start, t.end, box);
+                continue;
+            }
+            LinearBVHNode& n = (*nodes_)[me];
+            put_box(n, box);
+            n.axis = (uint8_t)axis;
+            n.nPrimitives = 0;
+            // right child is visited after the whole left subtree: push it first
+            todo.push_back({mid, t.end, me});
+            todo.push_back({t.start, mid, -1});
+        }
+    }
+
+  private:
+    static void put_box(LinearBVHNode& n, const Box& b) {
+        n.pMin[0] = b.lo.x; n.pMin[1] = b.lo.y; n.pMin[2] = b.lo.z;
+        n.pMax[0] = b.hi.x; n.pMax[1] = b.hi.y; n.pMax[2] = b.hi.z;
+    }
+    void emit_leaf(int me, int s, int e, const Box& box) {
+        LinearBVHNode& n = (*nodes_)[me];
+        put_box(n, box);
+        n.offset = (int32_t)order_->size();
+        n.nPrimitives = (uint16_t)(e - s);
+        for (int i = s; i < e; ++i) order_->push_back((int32_t)it_[i].id);
+    }
+    // Decide leaf vs interior for [s,e); on interior, partitions it_ and returns the split.
+    bool split(int s, int e, int* mid, int* axis, Box* box) {
+        Box b;
+        for (int i = s; i < e; ++i) b.add(it_[i].box);
+        *box = b;
+        int n = e - s;
+        if (n == 1) return false;
+        Box cb;
+        for (int i = s; i < e; ++i) cb.add(it_[i].c);
+        int dim = cb.longest();
+        *axis = dim;
+        if (get(cb.hi, dim) == get(cb.lo, dim)) return false;
+        Item* first = it_.data() + s;
+        Item* last = it_.data() + e;
+        if (n <= 2) {
+            *mid = (s + e) / 2;
+            std::nth_element(first, it_.data() + *mid, last,
+                             [dim](const Item& a, const Item& c) { return get(a.c, dim) < get(c.c, dim); });
+            return true;
+        }
+        const int NB = 12;
+        int cnt[NB] = {0};
+        Box bb[NB];
+        for (int i = s; i < e; ++i) {
+            int k = NB * cb.rel(it_[i].c, dim);
+            if (k == NB) k = NB - 1;
+            cnt[k]++;
+            bb[k].add(it_[i].box);
+        }
+        float cost[NB - 1];
+        for (int i = 0; i < NB - 1; ++i) {
+            Box b0, b1;
+            int c0 = 0, c1 = 0;
+            for (int j = 0; j <= i; ++j) { b0.add(bb[j]); c0 += cnt[j]; }
+            for (int j = i + 1; j < NB; ++j) { b1.add(bb[j]); c1 += cnt[j]; }
+            cost[i] = 1 + (c0 * b0.area() + c1 * b1.area()) / b.area();
+        }
+        float best = cost[0];
+        int bestK = 0;
+        for (int i = 1; i < NB - 1; ++i)
+            if (cost[i] < best) { best = cost[i]; bestK = i; }
+        float leafCost = n;
+        if (!(n > maxPrims_ || best < leafCost)) return false;
+        Item* pm = std::partition(first, last, [=](const Item& p) {
+            int k = NB * cb.rel(p.c, dim);
+            if (k == NB) k = NB - 1;
+            return k <= bestK;
+        });
+        *mid = (int)(pm - it_.data());
+        return true;
+    }
+
+    std::vector<Item>& it_;
+    int maxPrims_;
+    std::vector<LinearBVHNode>* nodes_;
+    std::vector<int32_t>* order_;
+};
+
+float roughness_to_alpha(float roughness) {   // Microfacet.h:78-83
+    roughness = mx(roughness, (float)1e-3);
+    float x = t_log(roughness);
+    return 1.62142f + 0.819955f * x + 0.1734f * x * x + 0.0171201f * x * x * x + 0.000640711f * x * x * x * x;
+}
+void put3(float* d, const float* s) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
+bool is_black3(const float* v) { return v[0] == 0.f && v[1] == 0.f && v[2] == 0.f; }
+void clamp3(float* d, const float* s) { for (int i = 0; i < 3; ++i) d[i] = clampf(s[i], 0, PBR_INF); }
+
+Lobe lobe0() { Lobe l; std::memset(&l, 0, sizeof(l)); return l; }
+void set_tr(Lobe& l, float ax, float ay) { l.ax = mx(float(0.001), ax); l.ay = mx(float(0.001), ay); }
+
+// Material::ComputeScatteringFunctions with constant textures folded (Material/*.cpp)
+MatTemplate material_template(const pbr_material_desc& m, bool multi) {
+    MatTemplate t;
+    std::memset(&t, 0, sizeof(t));
+    if (m.type == PBR_MAT_NONE) return t;
+    t.valid = 1;
+    t.eta = 1;
+    auto add = [&](const Lobe& l) { t.lobes[t.nLobes++] = l; };
+    switch (m.type) {
+    case PBR_MAT_MATTE: {
+        float r[3];
+        clamp3(r, m.Kd);
+        float sig = clampf(m.sigma, 0, 90);
+        if (!is_black3(r)) {
+            Lobe l = lobe0();
+            put3(l.R, r);
+            l.type = BSDF_REFLECTION | BSDF_DIFFUSE;
+            if (sig == 0) l.kind = L_LAMBERT;
+            else {
+                l.kind = L_OREN;
+                float s = (kPi / 180) * sig;
+                float s2 = s * s;
+                l.A = 1.f - (s2 / (2.f * (s2 + 0.33f)));
+                l.B = 0.45f * s2 / (s2 + 0.09f);
+            }
+            add(l);
+        }
+        break;
+    }
+    case PBR_MAT_MIRROR: {
+        float r[3];
+        clamp3(r, m.Kr);
+        if (!is_black3(r)) {
+            Lobe l = lobe0();
+            l.kind = L_SPEC_R; l.type = BSDF_REFLECTION | BSDF_SPECULAR; l.fresnel = FR_NOOP;
+            put3(l.R, r);
+            add(l);
+        }
+        break;
+    }
+    case PBR_MAT_GLASS: {
+        t.eta = m.eta;
+        float R[3], T[3];
+        clamp3(R, m.Kr);
+        clamp3(T, m.Kt);
+        float ur = m.uroughness, vr = m.vroughness;
+        if (is_black3(R) && is_black3(T)) break;
+        bool spec = ur == 0 && vr == 0;
+        if (spec && multi) {
+            Lobe l = lobe0();
+            l.kind = L_FRESNEL_SPEC; l.type = BSDF_REFLECTION | BSDF_TRANSMISSION | BSDF_SPECULAR;
+            put3(l.R, R); put3(l.T, T); l.etaA = 1.f; l.etaB = m.eta;
+            add(l);
+            break;
+        }
+        if (m.remap_roughness) { ur = roughness_to_alpha(ur); vr = roughness_to_alpha(vr); }
+        if (!is_black3(R)) {
+            Lobe l = lobe0();
+            put3(l.R, R); l.fresnel = FR_DIEL; l.fEtaI = 1.f; l.fEtaT = m.eta;
+            if (spec) { l.kind = L_SPEC_R; l.type = BSDF_REFLECTION | BSDF_SPECULAR; }
+            else { l.kind = L_MF_R; l.type = BSDF_REFLECTION | BSDF_GLOSSY; set_tr(l, ur, vr); }
+            add(l);
+        }
+        if (!is_black3(T)) {
+            Lobe l = lobe0();
+            put3(l.T, T); l.etaA = 1.f; l.etaB = m.eta;
+            if (spec) { l.kind = L_SPEC_T; l.type = BSDF_TRANSMISSION | BSDF_SPECULAR; }
+            else { l.kind = L_MF_T; l.type = BSDF_TRANSMISSION | BSDF_GLOSSY; set_tr(l, ur, vr); }
+            add(l);
+        }
+        break;
+    }
+    case PBR_MAT_METAL: {
+        float ur = m.has_uv_roughness ? m.uroughness : m.roughness;
+        float vr = m.has_uv_roughness ? m.vroughness : m.roughness;
+        if (m.remap_roughness) { ur = roughness_to_alpha(ur); vr = roughness_to_alpha(vr); }
+        Lobe l = lobe0();
+        l.kind = L_MF_R; l.type = BSDF_REFLECTION | BSDF_GLOSSY;
+        l.R[0] = l.R[1] = l.R[2] = 1.f;
+        l.fresnel = FR_COND;
+        l.cEtaI[0] = l.cEtaI[1] = l.cEtaI[2] = 1.f;
+        put3(l.cEtaT, m.metal_eta);
+        put3(l.cK, m.metal_k);
+        set_tr(l, ur, vr);
+        add(l);
+        break;
+    }
+    case PBR_MAT_PLASTIC: {
+        float kd[3], ks[3];
+        clamp3(kd, m.Kd);
+        if (!is_black3(kd)) {
+            Lobe l = lobe0();
+            l.kind = L_LAMBERT; l.type = BSDF_REFLECTION | BSDF_DIFFUSE;
+            put3(l.R, kd);
+            add(l);
+        }
+        clamp3(ks, m.Ks);
+        if (!is_black3(ks)) {
+            float r = m.roughness;
+            if (m.remap_roughness) r = roughness_to_alpha(r);
+            Lobe l = lobe0();
+            l.kind = L_MF_R; l.type = BSDF_REFLECTION | BSDF_GLOSSY;
+            put3(l.R, ks);
+            l.fresnel = FR_DIEL; l.fEtaI = 1.5f; l.fEtaT = 1.f;
+            set_tr(l, r, r);
+            add(l);
+        }
+        break;
+    }
+    default:
+        fail("unknown material type");
+    }
+    return t;
+}
+
+// Distribution1D construction (Sampling.h:77-90)
+void distribution1d(const std::vector<float>& f, std::vector<float>* cdf, float* funcInt) {
+    int n = (int)f.size();
+    cdf->assign(n + 1, 0.f);
+    (*cdf)[0] = 0;
+    for (int i = 1; i < n + 1; ++i) (*cdf)[i] = (*cdf)[i - 1] + f[i - 1] / n;
+    *funcInt = (*cdf)[n];
+    if (*funcInt == 0) for (int i = 1; i < n + 1; ++i) (*cdf)[i] = float(i) / float(n);
+    else for (int i = 1; i < n + 1; ++i) (*cdf)[i] /= *funcInt;
+}
+
+}  // namespace
+
+void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
+    if (!d) fail("null scene");
+    if (d->abi_version != PBR_HIP_ABI_VERSION) fail("abi_version mismatch");
+    if (d->n_shapes < 0 || (d->n_shapes > 0 && !d->shapes)) fail("bad shapes");
+    *S = HostScene();
+    const int ns = d->n_shapes;
+    // 1. world-space vertex bake (TriangleMesh ctor, Triangle.cpp:12-44) + primitive list
+    std::vector<std::vector<f3>> world(ns);
+    std::vector<PrimRef> prims;
+    std::vector<int> firstPrim(ns, 0);
+    std::vector<int> flip(ns, 0);
+    S->spheres.clear();
+    std::vector<int> sphereIndex(ns, -1);
+    for (int i = 0; i < ns; ++i) {
+        const pbr_shape_desc& sd = d->shapes[i];
+        Mat o2w = from_rows(sd.object_to_world.m);
+        flip[i] = (sd.reverse_orientation != 0) ^ swaps_handedness(o2w);
+        firstPrim[i] = (int)prims.size();
+        if (sd.material >= d->n_materials) fail("material index out of range");
+        if (sd.type == PBR_SHAPE_TRIANGLE_MESH) {
+            if (sd.N) fail("per-vertex normals are not supported");
+            if (sd.n_triangles < 0 || sd.n_vertices < 0 || (sd.n_triangles && (!sd.indices || !sd.P))) fail("bad mesh");
+            world[i].resize(sd.n_vertices);
+            for (int v = 0; v < sd.n_vertices; ++v)
+                world[i][v] = xf_point(&o2w.a[0][0], mk(sd.P[3 * v], sd.P[3 * v + 1], sd.P[3 * v + 2]));
+            for (int t = 0; t < sd.n_triangles; ++t) {
+                for (int k = 0; k < 3; ++k) {
+                    int vi = sd.indices[3 * t + k];
+                    if (vi < 0 || vi >= sd.n_vertices) fail("vertex index out of range");
+                }
+                prims.push_back({i, t});
+            }
+        } else if (sd.type == PBR_SHAPE_SPHERE) {
+            if (sd.area_light_first >= 0) fail("sphere area lights are not supported");
+            SphereRec r;
+            std::memset(&r, 0, sizeof(r));
+            std::memcpy(r.o2w, sd.object_to_world.m, 64);
+            std::memcpy(r.w2o, sd.object_to_world.m_inv, 64);
+            r.radius = sd.radius;
+            r.flip = flip[i];
+            sphereIndex[i] = (int)S->spheres.size();
+            S->spheres.push_back(r);
+            prims.push_back({i, -1});
+        } else {
+            fail("unknown shape type");
+        }
+    }
+    const int np = (int)prims.size();
+    auto vert = [&](const PrimRef& p, int k) {
+        const pbr_shape_desc& sd = d->shapes[p.shape];
+        return world[p.shape][sd.indices[3 * p.tri + k]];
+    };
+    // 2. SAH BVH over primitive world bounds
+    std::vector<Item> items(np);
+    for (int i = 0; i < np; ++i) {
+        Box b;
+        if (prims[i].tri >= 0) {   // Triangle::WorldBound (Triangle.cpp:55-62)
+            f3 p0 = vert(prims[i], 0), p1 = vert(prims[i], 1), p2 = vert(prims[i], 2);
+            b.lo = vmin(p0, p1); b.hi = vmax(p0, p1);
+            b.add(p2);
+        } else {                   // Shape::WorldBound → Transform(Bounds3f)
+            const SphereRec& r = S->spheres[sphereIndex[prims[i].shape]];
+            float rad = r.radius;
+            f3 lo = mk(-rad, -rad, -rad), hi = mk(rad, rad, rad);
+            f3 corners[8] = {mk(lo.x, lo.y, lo.z), mk(hi.x, lo.y, lo.z), mk(lo.x, hi.y, lo.z), mk(lo.x, lo.y, hi.z),
+                             mk(lo.x, hi.y, hi.z), mk(hi.x, hi.y, lo.z), mk(hi.x, lo.y, hi.z), mk(hi.x, hi.y, hi.z)};
+            f3 c0 = xf_point(r.o2w, corners[0]);
+            b.lo = c0; b.hi = c0;
+            for (int k = 1; k < 8; ++k) b.add(xf_point(r.o2w, corners[k]));
+        }
+        items[i].id = (size_t)i;
+        items[i].box = b;
+        items[i].c = .5f * b.lo + .5f * b.hi;
+    }
+    SahBuilder(items, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1, &S->nodes, &S->primIds).run();
+    // 3. primitive payloads in BVH order
+    std::vector<int> slotOf(np, -1);
+    bool anyUV = false;
+    for (int i = 0; i < ns; ++i) if (d->shapes[i].type == PBR_SHAPE_TRIANGLE_MESH && d->shapes[i].UV) anyUV = true;
+    S->triVerts.assign((size_t)np * 12, 0.f);
+    S->primInfo.assign((size_t)np * 4, 0);
+    if (anyUV) S->triUV.assign((size_t)np * 6, 0.f);
+    for (int slot = 0; slot < np; ++slot) {
+        const PrimRef& p = prims[S->primIds[slot]];
+        slotOf[S->primIds[slot]] = slot;
+        const pbr_shape_desc& sd = d->shapes[p.shape];
+        int flags = flip[p.shape] ? PRIM_FLIP : 0;
+        float* tv = &S->triVerts[(size_t)slot * 12];
+        if (p.tri >= 0) {
+            for (int k = 0; k < 3; ++k) {
+                f3 v = vert(p, k);
+                tv[4 * k] = v.x; tv[4 * k + 1] = v.y; tv[4 * k + 2] = v.z; tv[4 * k + 3] = 0.f;
+            }
+            if (sd.UV) {
+                flags |= PRIM_HAS_UV;
+                for (int k = 0; k < 3; ++k) {
+                    int vi = sd.indices[3 * p.tri + k];
+                    S->triUV[(size_t)slot * 6 + 2 * k] = sd.UV[2 * vi];
+                    S->triUV[(size_t)slot * 6 + 2 * k + 1] = sd.UV[2 * vi + 1];
+                }
+            }
+        } else {
+            flags |= PRIM_SPHERE;
+            tv[0] = bitsf((uint32_t)sphereIndex[p.shape]);
+        }
+        int32_t* pi = &S->primInfo[(size_t)slot * 4];
+        pi[0] = flags;
+        pi[1] = sd.material;
+        pi[2] = (p.tri >= 0 && sd.area_light_first >= 0) ? sd.area_light_first + p.tri : -1;
+        if (sd.medium_inside >= d->n_media || sd.medium_outside >= d->n_media) fail("medium index out of range");
+        pi[3] = (int32_t)(((uint32_t)(sd.medium_inside & 0xffff)) | ((uint32_t)(sd.medium_outside & 0xffff) << 16));
+    }
+    // 4. materials → lobe templates for allowMultipleLobes = false / true
+    S->materials.clear();
+    for (int m = 0; m < d->n_materials; ++m) {
+        S->materials.push_back(material_template(d->materials[m], false));
+        S->materials.push_back(material_template(d->materials[m], true));
+    }
+    // 5. media (HomogeneousMedium.h: sigma_t = sigma_s + sigma_a)
+    for (int m = 0; m < d->n_media; ++m) {
+        const pbr_medium_desc& md = d->media[m];
+        for (int k = 0; k < 3; ++k) S->media.push_back(md.sigma_a[k]);
+        for (int k = 0; k < 3; ++k) S->media.push_back(md.sigma_s[k]);
+        for (int k = 0; k < 3; ++k) S->media.push_back(md.sigma_s[k] + md.sigma_a[k]);
+        S->media.push_back(md.g);
+    }
+    // 6. lights
+    for (int li = 0; li < d->n_lights; ++li) {
+        const pbr_light_desc& ld = d->lights[li];
+        DLight L;
+        std::memset(&L, 0, sizeof(L));
+        L.type = ld.type;
+        L.medIn = ld.medium_inside;
+        L.medOut = ld.medium_outside;
+        L.primSlot = -1;
+        if (ld.type == PBR_LIGHT_POINT) {
+            f3 p = xf_point(ld.light_to_world.m, mk(0, 0, 0));
+            L.p[0] = p.x; L.p[1] = p.y; L.p[2] = p.z;
+            put3(L.L, ld.I);
+            float P[3];
+            for (int k = 0; k < 3; ++k) P[k] = (4 * kPi) * ld.I[k];   // PointLight::Power
+            S->lightPower.push_back(0.212671f * P[0] + 0.715160f * P[1] + 0.072169f * P[2]);
+        } else if (ld.type == PBR_LIGHT_DIFFUSE_AREA) {
+            if (ld.shape < 0 || ld.shape >= ns || d->shapes[ld.shape].type != PBR_SHAPE_TRIANGLE_MESH ||
+                ld.triangle < 0 || ld.triangle >= d->shapes[ld.shape].n_triangles)
+                fail("area light shape out of range");
+            int orig = firstPrim[ld.shape] + ld.triangle;
+            L.primSlot = slotOf[orig];
+            L.twoSided = ld.two_sided;
+            put3(L.L, ld.Le);
+            f3 p0 = vert(prims[orig], 0), p1 = vert(prims[orig], 1), p2 = vert(prims[orig], 2);
+            L.area = (float)(0.5 * (double)len(cross(p1 - p0, p2 - p0)));   // Triangle::Area
+            float P[3];
+            for (int k = 0; k < 3; ++k) P[k] = (float)(ld.two_sided ? 2 : 1) * ld.Le[k] * L.area * kPi;
+            S->lightPower.push_back(0.212671f * P[0] + 0.715160f * P[1] + 0.072169f * P[2]);
+        } else if (ld.type == PBR_LIGHT_SKYBOX) {
+            if (S->envLight >= 0) fail("only one SkyBoxLight is supported");
+            L.worldRadius = ld.world_radius;
+            if (ld.env_data && ld.env_width > 0 && ld.env_height > 0) {
+                if (ld.env_components < 3) fail("SkyBox env needs >= 3 components");
+                L.envW = ld.env_width;
+                L.envH = ld.env_height;
+                // HDRtoLDR(texel, 0.3) once per texel (Spectrum.h:219-226, SkyBoxLight.cpp:37)
+                float invExposure = (float)(1.0 / (1.0 - (double)0.3f));
+                size_t nt = (size_t)L.envW * L.envH;
+                S->env.resize(nt * 4);
+                for (size_t t = 0; t < nt; ++t) {
+                    for (int k = 0; k < 3; ++k) {
+                        float c = ld.env_data[t * ld.env_components + k];
+                        S->env[4 * t + k] = (float)(1.0 - (double)t_exp(-c * invExposure));
+                    }
+                    S->env[4 * t + 3] = 0.f;
+                }
+            }
+            S->envLight = li;
+            S->infinite.push_back(li);
+            S->lightPower.push_back(0.f);
+        } else {
+            fail("unknown light type");
+        }
+        S->lights.push_back(L);
+    }
+    for (size_t slot = 0; slot < (size_t)np; ++slot) {
+        int al = S->primInfo[slot * 4 + 2];
+        if (al >= d->n_lights) fail("area light index out of range");
+    }
+    if (S->infinite.size() > 4) fail("at most 4 infinite lights");
+    light_distribution(*S, PBR_LIGHTS_UNIFORM, &S->lightCdf, &S->lightFunc, &S->lightFuncInt);
+}
+
+void light_distribution(const HostScene& s, int strategy, std::vector<float>* cdf, std::vector<float>* func,
+                        float* funcInt) {
+    size_t n = s.lights.size();
+    func->assign(n, 1.f);
+    // CreateLightSampleDistribution: "uniform" or a single light → uniform (LightDistrib.cpp:10-12)
+    if (strategy == PBR_LIGHTS_POWER && n != 1) *func = s.lightPower;
+    if (n == 0) { cdf->assign(1, 0.f); *funcInt = 0; return; }
+    distribution1d(*func, cdf, funcInt);
+}
+
+void build_camera(const pbr_camera_desc* c, DeviceCamera* out) {
+    if (c->width <= 0 || c->height <= 0) fail("bad raster size");
+    Xf camToWorld;
+    if (c->use_look_at) {
+        camToWorld = inverse(look_at(mk(c->eye[0], c->eye[1], c->eye[2]), mk(c->look[0], c->look[1], c->look[2]),
+                                     mk(c->up[0], c->up[1], c->up[2])));
+    } else {
+        camToWorld = Xf{from_rows(c->camera_to_world.m), from_rows(c->camera_to_world.m_inv)};
+    }
+    // CreatePerspectiveCamera screen window (Perspective.cpp:84-104)
+    float frame = (float)c->width / (float)c->height;
+    float x0, x1, y0, y1;
+    if (frame > 1.f) { x0 = -frame; x1 = frame; y0 = -1.f; y1 = 1.f; }
+    else { x0 = -1.f; x1 = 1.f; y0 = -1.f / frame; y1 = 1.f / frame; }
+    // ProjectiveCamera (Camera.h:36-53)
+    Xf camToScreen = perspective(c->fov, 1e-2f, 1000.f);
+    Xf screenToRaster = compose(compose(scale((float)c->width, (float)c->height, 1), scale(1 / (x1 - x0), 1 / (y0 - y1), 1)),
+                                translate(mk(-x0, -y1, 0)));
+    Xf rasterToCamera = compose(inverse(camToScreen), inverse(screenToRaster));
+    std::memcpy(out->rasterToCamera, &rasterToCamera.m.a[0][0], 64);
+    std::memcpy(out->cameraToWorld, &camToWorld.m.a[0][0], 64);
+    out->lensRadius = c->lens_radius;
+    out->focalDistance = c->focal_distance;
+    out->width = c->width;
+    out->height = c->height;
+}
+
+void build_halton_tables(int nPrimes, HaltonTables* t) {
+    t->primes.clear();
+    for (uint32_t c = 2; (int)t->primes.size() < nPrimes; ++c) {
+        bool prime = true;
+        for (uint32_t q : t->primes) { if (q * q > c) break; if (c % q == 0) { prime = false; break; } }
+        if (prime) t->primes.push_back(c);
+    }
+    t->recips.resize(nPrimes);
+    t->primeSums.resize(nPrimes);
+    uint32_t acc = 0;
+    for (int i = 0; i < nPrimes; ++i) {
+        t->recips[i] = (uint32_t)((((uint64_t)1) << 32) / t->primes[i]);
+        t->primeSums[i] = acc;
+        acc += t->primes[i];
+    }
+    // ComputeRadicalInversePermutations (LowDiscrepancy.cpp:2284-2298) with PCG32 defaults
+    t->perms.resize(acc);
+    uint64_t state = 0x853c49e6748fea9bULL;
+    const uint64_t inc = 0xda3e39cb94b95bdbULL;
+    auto next = [&]() -> uint32_t {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    };
+    auto bounded = [&](uint32_t b) -> uint32_t {
+        uint32_t threshold = (~b + 1u) % b;
+        for (;;) { uint32_t r = next(); if (r >= threshold) return r % b; }
+    };
+    uint16_t* p = t->perms.data();
+    for (int i = 0; i < nPrimes; ++i) {
+        uint32_t n = t->primes[i];
+        for (uint32_t j = 0; j < n; ++j) p[j] = (uint16_t)j;
+        for (uint32_t j = 0; j < n; ++j) {           // Shuffle (Sampling.h:47-54)
+            uint32_t other = j + bounded(n - j);
+            std::swap(p[j], p[other]);
+        }
+        p += n;
+    }
+}
+
+void halton_params(int resX, int resY, DeviceSampler* s) {   // HaltonSampler ctor (Halton.cpp:30-58)
+    int res[2] = {resX, resY}, scale[2], expo[2];
+    for (int i = 0; i < 2; ++i) {
+        int base = i == 0 ? 2 : 3, sc = 1, e = 0;
+        while (sc < std::min(res[i], 128)) { sc *= base; ++e; }
+        scale[i] = sc;
+        expo[i] = e;
+    }
+    auto inv_mod = [](int64_t a, int64_t n) -> int64_t {   // multiplicativeInverse via extended GCD
+        int64_t r0 = n, r1 = a % n, s0 = 0, s1 = 1;
+        while (r1 != 0) {
+            int64_t q = r0 / r1, t = r0 - q * r1;
+            r0 = r1; r1 = t;
+            t = s0 - q * s1; s0 = s1; s1 = t;
+        }
+        int64_t x = s0 % n;
+        return x < 0 ? x + n : x;
+    };
+    s->baseExp0 = expo[0];
+    s->baseExp1 = expo[1];
+    s->baseScale1 = scale[1];
+    s->stride = scale[0] * scale[1];
+    s->mult0 = scale[0] > 1 ? (int)inv_mod(scale[1], scale[0]) : 0;
+    s->mult1 = scale[1] > 1 ? (int)inv_mod(scale[0], scale[1]) : 0;
+    s->ratio0 = s->stride / scale[0];
+    s->ratio1 = s->stride / scale[1];
+}
+
+}  // namespace pbr

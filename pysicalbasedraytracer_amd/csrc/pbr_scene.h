@@ -1,0 +1,58 @@
+// pbr_scene.h — host-side flattening of a pbr_scene_desc into the HBM layout of pbr_layout.h.
+#pragma once
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/pbr_hip.h"
+#include "pbr_layout.h"
+#include "pbr_math.h"
+
+namespace pbr {
+
+struct LinearBVHNode {            // BVHAccel.cpp:46-55, 32 bytes
+    float pMin[3], pMax[3];
+    int32_t offset;               // primitivesOffset | secondChildOffset
+    uint16_t nPrimitives;
+    uint8_t axis;
+    uint8_t pad;
+};
+static_assert(sizeof(LinearBVHNode) == 32, "LinearBVHNode is 32 bytes");
+
+struct HostScene {
+    std::vector<LinearBVHNode> nodes;
+    std::vector<int32_t> primIds;           // ordered slot → index in the prims vector
+    std::vector<float> triVerts;            // 12 floats per ordered prim
+    std::vector<int32_t> primInfo;          // 4 ints per ordered prim
+    std::vector<float> triUV;               // 6 floats per ordered prim (if any UVs)
+    std::vector<SphereRec> spheres;
+    std::vector<MatTemplate> materials;     // 2 per material
+    std::vector<DLight> lights;
+    std::vector<float> env;                 // 4 floats per texel
+    int envLight = -1;
+    std::vector<int> infinite;
+    std::vector<float> lightCdf, lightFunc; // uniform distribution (power built per render)
+    float lightFuncInt = 0;
+    std::vector<float> lightPower;          // Power().y() per light (LightDistrib.cpp:36-41)
+    std::vector<float> media;               // 10 floats per medium
+};
+
+// Throws std::invalid_argument on a malformed descriptor.
+void build_host_scene(const pbr_scene_desc* desc, HostScene* out);
+
+// Light sampling distribution (Distribution1D over lights): uniform or power.
+void light_distribution(const HostScene& s, int strategy, std::vector<float>* cdf, std::vector<float>* func,
+                        float* funcInt);
+
+// Camera: RasterToCamera and CameraToWorld matrices exactly as CreatePerspectiveCamera builds them.
+void build_camera(const pbr_camera_desc* cam, DeviceCamera* out);
+
+// Halton: digit permutations for the first n primes (RNG default state), plus per-dim tables.
+struct HaltonTables {
+    std::vector<uint32_t> primes, recips, primeSums;
+    std::vector<uint16_t> perms;
+};
+void build_halton_tables(int nPrimes, HaltonTables* t);
+void halton_params(int resX, int resY, DeviceSampler* s);
+
+}  // namespace pbr
