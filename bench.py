@@ -1,0 +1,167 @@
+"""Headline benchmark: Msamples/s of the MI355X render path on BASELINE config C2
+(1920×1080, 64 spp, WhittedIntegrator, dragon + mirror floor + SkyBox HDR), with the roofline of the
+dominant kernel and the CPU restatement timed beside it.
+
+One step = one full frame.  With --gpus N (launched by torch.distributed.run, one rank per GPU)
+the frame's 64×64 tiles are dealt round-robin over ranks and rank 0 gathers the per-tile float RGB
+spans over RCCL — total work is fixed, so scaling is strong.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from pysicalbasedraytracer_amd import HipRenderer, scenes, tiles_for_rank  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# Algorithmic bytes model: 32 B per LinearBVHNode visit, 48 B per primitive test,
+# 96 B of ray-queue traffic per traced ray, 64 B per shading event.
+B_NODE, B_PRIM, B_RAY, B_SHADE = 32, 48, 96, 64
+
+
+def cpu_baseline(scene, rd, budget_s=12.0):
+    """Oracle (CPU restatement, the reference algorithm) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    W, H, spp = rd.camera.width, rd.camera.height, rd.spp
+    rows_per_chunk = 8
+    done_px = 0
+    secs = 0.0
+    y = H // 2 - 64
+    t_start = time.time()
+    while secs < budget_s and y < H:
+        tiles = [(0, y, W, min(H, y + rows_per_chunk))]
+        rdc = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                                 rd.sampler, tiles=tiles)
+        _, _, sec = oracle_lib.render(scene, rdc, threads=threads)
+        secs += sec
+        done_px += W * (min(H, y + rows_per_chunk) - y)
+        y += rows_per_chunk
+        if time.time() - t_start > 3 * budget_s:
+            break
+    samples = done_px * spp
+    return {"value": samples / secs / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"C2 rows [{H // 2 - 64},{y}) × {W} px × {spp} spp = {samples} samples in {secs:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    scene, rd = scenes.CONFIGS[args.config]()
+    W, H, spp = rd.camera.width, rd.camera.height, rd.spp
+    tiles = tiles_for_rank(W, H, rank, world) if world > 1 else [(0, 0, W, H)]
+    rdr = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                             rd.sampler, tiles=tiles)
+    npx = sum((t[2] - t[0]) * (t[3] - t[1]) for t in tiles)
+
+    r = HipRenderer(local)
+    t0 = time.time()
+    r.upload(scene)
+    upload_s = time.time() - t0
+
+    stream = torch.cuda.current_stream(dev)
+    rgb = torch.empty((npx, 3), dtype=torch.float32, device=dev)
+    rgba = torch.empty((npx, 4), dtype=torch.uint8, device=dev)
+    # gather buffers: every rank pads its packed span to the largest one
+    max_px = npx
+    if world > 1:
+        t = torch.tensor([npx], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        max_px = int(t.item())
+    send = torch.zeros((max_px, 3), dtype=torch.float32, device=dev)
+    gather = [torch.empty_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def step():
+        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+        if world > 1:
+            send[:npx].copy_(rgb)
+            dist.gather(send, gather_list=gather, dst=0)
+
+    # roofline counters: one instrumented, untimed pass on the same workload
+    st = r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, stats=True)
+    torch.cuda.synchronize(dev)
+    samples_rank = npx * spp
+    alg_bytes = B_NODE * st.node_visits + B_PRIM * st.prim_tests + B_RAY * st.rays + B_SHADE * st.shading_events
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ev0.record(stream)
+        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+        ev1.record(stream)
+        if world > 1:
+            send[:npx].copy_(rgb)
+            dist.gather(send, gather_list=gather, dst=0)
+        torch.cuda.synchronize(dev)
+        kernel_ms.append(ev0.elapsed_time(ev1))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        ab = torch.tensor([float(alg_bytes), float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+    ms_per_step = elapsed / args.steps * 1e3
+    total_samples = W * H * spp
+    value = total_samples / (elapsed / args.steps) / 1e6
+
+    if rank == 0:
+        k_ms = float(np.mean(kernel_ms))
+        achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+        out = {
+            "metric": "Msamples/sec (whole node) + wall-clock to 1080p/64spp frame; %HBM roofline",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {W}x{H}, {spp} spp, "
+                                   f"{['Whitted', 'Path', 'VolPath'][rd.integrator]} d{rd.max_depth}",
+                       "scene": scene.info.get("dragon", ""), "triangles": scene.info.get("triangles"),
+                       "parallelism": f"tiles64x64 round-robin over {world} GPU(s), RCCL gather",
+                       "frame_ms": round(ms_per_step, 3), "scene_upload_s": round(upload_s, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_render<Whitted>", "kernel_ms": round(k_ms, 3),
+                         "bytes_per_sample": round(alg_bytes / samples_rank, 1),
+                         "model": "32*node_visits + 48*prim_tests + 96*rays + 64*shading_events per launch"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene, rd)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -220,6 +220,7 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
             } else {
                 int axis = (int)((meta >> 16) & 0xffu);
                 bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+                if (sp >= 64) break;   // BVHAccel's 64-entry stack; the SAH builds here stay < 30 deep
                 if (neg) { stack[sp++] = cur + 1; cur = off; }
                 else { stack[sp++] = off; cur = cur + 1; }
             }

@@ -1,0 +1,50 @@
+"""The C-ABI library loads and exports every symbol include/pbr_hip.h declares (no GPU calls)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from pysicalbasedraytracer_amd import capi
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "pbr_hip.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(pbr_hip_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_ctypes_table_agree():
+    assert declared_symbols() == sorted(capi.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = capi.load_library()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.pbr_hip_abi_version() == capi.ABI_VERSION
+
+
+def test_struct_sizes_match_c():
+    # the ctypes mirror must match the C layout (x86-64 SysV)
+    assert C.sizeof(capi.Transform) == 128
+    assert C.sizeof(capi.Tile) == 16
+    assert C.sizeof(capi.RenderStats) == 8 * 8 + 8
+
+
+def test_no_device_returns_error_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = capi.load_library()
+    ctx = C.c_void_p()
+    assert lib.pbr_hip_create(0, C.byref(ctx)) in (capi.PBR_E_NODEVICE, capi.PBR_E_HIP)
+
+
+def test_null_arguments_are_rejected():
+    lib = capi.load_library()
+    assert lib.pbr_hip_create(0, None) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_upload_scene(None, None) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_render(None, None, None, None, None) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_destroy(None) == capi.PBR_E_INVALID

@@ -1,0 +1,210 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU restatement (oracle/).
+
+Tolerance (north_star): per-pixel L∞ ≤ 1e-3 on linear RGB against the CPU render; sampler values,
+camera rays, BVH layout and intersection records are compared bit for bit.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from pysicalbasedraytracer_amd import HipRenderer, assemble, capi, scenes, tile_grid
+
+pytestmark = pytest.mark.gpu
+LINF = 1e-3
+KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
+
+
+@pytest.fixture(scope="module")
+def hip():
+    r = HipRenderer(0)
+    yield r
+    r.close()
+
+
+def small_dragon(n=48):
+    P, I = scenes.dragon_standin(n=n)
+    return P, I, "standin-small"
+
+
+def compare(gpu_rgb, cpu_rgb, gpu8=None, cpu8=None):
+    d = np.abs(gpu_rgb.astype(np.float64) - cpu_rgb.astype(np.float64))
+    linf = float(np.nanmax(d)) if d.size else 0.0
+    exact = float(np.mean(np.all(gpu_rgb.view(np.uint32) == cpu_rgb.view(np.uint32), axis=1)))
+    assert np.isfinite(gpu_rgb).all()
+    assert linf <= LINF, f"per-pixel L∞ {linf} > {LINF} (bit-exact pixels {exact:.4f})"
+    if gpu8 is not None:
+        diff8 = np.abs(gpu8.astype(int) - cpu8.astype(int)).max()
+        assert diff8 <= 1
+    return linf, exact
+
+
+def test_halton_kats_on_device(hip):
+    k = KATS["halton_1920x1080"]
+    for pixel, bits in k["pixels"].items():
+        x, y = map(int, pixel.split(","))
+        v = hip.sampler_values(1920, 1080, 64, [(x, y, 0, d) for d in k["get2d_x3_dims"]])
+        assert ["%08x" % u for u in v.view(np.uint32)] == bits
+
+
+def test_halton_random_queries_bit_exact(hip):
+    rng = np.random.default_rng(1)
+    for (w, h, spp) in [(1920, 1080, 64), (256, 256, 4), (32, 32, 4), (3840, 2160, 1024), (100, 37, 7)]:
+        q = np.stack([rng.integers(0, w, 4000), rng.integers(0, h, 4000), rng.integers(0, spp, 4000),
+                      rng.integers(0, 200, 4000)], axis=1).astype(np.int32)
+        g = hip.sampler_values(w, h, spp, q)
+        c = O.halton(w, h, spp, q)
+        assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+
+
+def test_camera_rays_bit_exact(hip):
+    rng = np.random.default_rng(2)
+    for (w, h) in [(1920, 1080), (256, 256), (3840, 2160), (100, 300)]:
+        cam = scenes.camera(w, h, (0.3, 0.55, 2.6), (0.0, -0.25, 0.1))
+        pf = np.stack([rng.random(2000) * w, rng.random(2000) * h], axis=1).astype(np.float32)
+        assert np.array_equal(hip.camera_rays(cam, pf).view(np.uint32), O.camera_rays(cam, pf).view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [16, 96])
+def test_bvh_layout_identical_to_restatement(hip, n):
+    s, _ = scenes.config_c2(64, 36, 1, mesh=small_dragon(n), sky=np.ones((8, 16, 3), np.float32))
+    hip.upload(s)
+    gn, gi = hip.get_bvh()
+    cn, ci = O.build_bvh(s)
+    assert np.array_equal(gi, ci)
+    assert np.array_equal(gn, cn)
+
+
+def test_bvh_layout_full_dragon(hip):
+    s, _ = scenes.config_c2(64, 36, 1, sky=np.ones((8, 16, 3), np.float32))
+    hip.upload(s)
+    gn, gi = hip.get_bvh()
+    cn, ci = O.build_bvh(s)
+    assert np.array_equal(gi, ci) and np.array_equal(gn, cn)
+
+
+def test_intersect_records_bit_exact(hip):
+    s, _ = scenes.config_c2(64, 36, 1, mesh=small_dragon(64), sky=np.ones((8, 16, 3), np.float32))
+    hip.upload(s)
+    rng = np.random.default_rng(3)
+    o = rng.normal(size=(5000, 3)) * 2.5
+    t = rng.normal(size=(5000, 3)) * 0.4
+    d = t - o
+    rays = np.concatenate([o, d, np.full((5000, 1), np.inf)], axis=1).astype(np.float32)
+    rays[::7, 6] = 1.0          # some short rays
+    for any_hit in (False, True):
+        g = hip.intersect(rays, any_hit)
+        c = O.intersect(s, rays, any_hit)
+        assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+
+
+def test_li_capture_on_device(hip):
+    k = KATS["li_capture"]
+    s = scenes.Scene()
+    m = s.matte((0.5, 0.5, 0.5))
+    s.mesh(np.array(k["triangle"], np.float32), np.array([[0, 1, 2]], np.int32), m)
+    s.point_light(tuple(k["point_light"]["pos"]), (9.0, 9.0, 9.0))
+    cam = scenes.camera(32, 32, (0, 0, 3), (0, 0, 0))
+    hip.upload(s)
+    rgb, _, _ = hip.render(scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 4, 5))
+    px = rgb.reshape(32, 32, 3)[16, 16]
+    assert np.float32(px[0]).view(np.uint32) == np.float32(k["value"]).view(np.uint32)
+
+
+def test_c1_spheres_point_light(hip):
+    s, rd = scenes.config_c1()
+    hip.upload(s)
+    g, g8, st = hip.render(rd)
+    c, c8, _ = O.render(s, rd)
+    compare(g, c, g8, c8)
+    assert st.samples == 256 * 256 * 4
+
+
+def render_pair(hip, s, rd):
+    hip.upload(s)
+    g, g8, _ = hip.render(rd)
+    c, c8, _ = O.render(s, rd)
+    return compare(g, c, g8, c8)
+
+
+def test_c2_whitted_dragon_mirror_skybox(hip):
+    s, rd = scenes.config_c2(192, 108, 4)
+    render_pair(hip, s, rd)
+
+
+def test_c3_path_area_light(hip):
+    s, rd = scenes.config_c3(96, 54, 8, mesh=small_dragon(64))
+    render_pair(hip, s, rd)
+
+
+def test_c4_path_glass_metal_plastic(hip):
+    s, rd = scenes.config_c4(96, 54, 8, mesh=small_dragon(48))
+    render_pair(hip, s, rd)
+
+
+def test_c5_volpath_medium(hip):
+    s, rd = scenes.config_c5(64, 36, 8, mesh=small_dragon(40))
+    render_pair(hip, s, rd)
+
+
+def test_power_light_strategy_and_specular_glass(hip):
+    s = scenes.Scene()
+    white = s.matte((0.7, 0.7, 0.7))
+    g = s.glass(urough=0.0, vrough=0.0)
+    s.sphere((0.0, 0.0, 0.0), 0.8, g)
+    Pf, If = scenes.quad(-0.8, 5.0)
+    s.mesh(Pf, If, white)
+    Pl, Il = scenes.quad(2.0, 0.7, flip=True)
+    s.area_light_mesh(Pl, Il, (6.0, 6.0, 6.0), white)
+    s.point_light((1.5, 1.5, 1.5), (3.0, 3.0, 3.0))
+    cam = scenes.camera(48, 48, (0.0, 0.5, 3.0), (0.0, 0.0, 0.0))
+    for integ, depth in ((capi.INTEGRATOR_PATH, 6), (capi.INTEGRATOR_WHITTED, 5), (capi.INTEGRATOR_VOLPATH, 6)):
+        rd = scenes.render_desc(cam, integ, 8, depth, rr_threshold=0.8, light_strategy=capi.LIGHTS_POWER)
+        render_pair(hip, s, rd)
+
+
+def test_tiles_and_determinism(hip):
+    s, rd = scenes.config_c2(128, 72, 2, mesh=small_dragon(48))
+    hip.upload(s)
+    full, full8, _ = hip.render(rd)
+    again, _, _ = hip.render(rd)
+    assert np.array_equal(full.view(np.uint32), again.view(np.uint32))
+    tiles = tile_grid(128, 72, 32)
+    mine = [t for i, t in enumerate(tiles) if i % 3 == 1]
+    rd2 = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, tiles=mine)
+    part, part8, _ = hip.render(rd2)
+    frame = assemble(128, 72, mine, part, 3)
+    ref = full.reshape(72, 128, 3)
+    for (x0, y0, x1, y1) in mine:
+        assert np.array_equal(frame[y0:y1, x0:x1].view(np.uint32), ref[y0:y1, x0:x1].view(np.uint32))
+
+
+def test_full_size_c2_properties(hip):
+    """BASELINE size (1080p/64spp) checked through size-independent properties: finite, bounded,
+    and the 8-bit image equals the float image's output transform (done on the device)."""
+    s, rd = scenes.config_c2()
+    hip.upload(s)
+    g, g8, st = hip.render(rd, stats=True)
+    assert g.shape == (1920 * 1080, 3) and np.isfinite(g).all() and (g >= 0).all()
+    assert st.samples == 1920 * 1080 * 64 and st.rays > st.samples
+    # spot-check 64 pixels against the oracle's per-pixel render
+    rng = np.random.default_rng(5)
+    picks = rng.integers(0, 1920 * 1080, 64)
+    tiles = [(int(p % 1920), int(p // 1920), int(p % 1920) + 1, int(p // 1920) + 1) for p in picks]
+    rd2 = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, tiles=tiles)
+    c, c8, _ = O.render(s, rd2)
+    compare(g[picks], c, g8[picks], c8)
+
+
+def test_errors_fail_loudly(hip):
+    fresh = HipRenderer(0)
+    s, rd = scenes.config_c1(8, 8, 1)
+    with pytest.raises(RuntimeError):
+        fresh.render(rd)
+    fresh.upload(s)
+    bad = scenes.render_desc(rd.camera, rd.integrator, 1, 5, tiles=[(0, 0, 9, 9)])
+    with pytest.raises(RuntimeError):
+        fresh.render(bad)
+    fresh.close()

@@ -1,0 +1,125 @@
+"""The oracle (CPU restatement, oracle/) against the reference's own recorded outputs and
+analytic known answers. CPU only."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from pysicalbasedraytracer_amd import capi, scenes
+
+KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
+
+
+def test_linear_bvh_node_is_32_bytes():
+    assert O.load().oracle_sizeof_linear_bvh_node() == KATS["sizeof"]["LinearBVHNode"]
+
+
+@pytest.mark.parametrize("pixel", ["0,0", "1,0", "1919,1079"])
+def test_halton_kats_bit_exact(pixel):
+    k = KATS["halton_1920x1080"]
+    x, y = map(int, pixel.split(","))
+    v = O.halton(1920, 1080, 64, [(x, y, 0, d) for d in k["get2d_x3_dims"]])
+    assert ["%08x" % u for u in v.view(np.uint32)] == k["pixels"][pixel]
+
+
+def test_halton_second_sample():
+    v = O.halton(1920, 1080, 64, [(0, 0, 1, 0), (0, 0, 1, 1)])
+    assert np.allclose(v, KATS["halton_1920x1080"]["pixel_0_0_sample_1_dims_0_1"], rtol=0, atol=6e-8)  # printed to 7 significant digits
+
+
+def test_halton_permutations_are_permutations():
+    perms = O.halton_perms(64)
+    pos = 0
+    p = 2
+    primes = []
+    while len(primes) < 64:
+        if all(p % q for q in primes):
+            primes.append(p)
+        p += 1
+    for b in primes:
+        assert sorted(perms[pos:pos + b].tolist()) == list(range(b))
+        pos += b
+
+
+def li_capture_scene():
+    k = KATS["li_capture"]
+    s = scenes.Scene()
+    m = s.matte((0.5, 0.5, 0.5))
+    s.mesh(np.array(k["triangle"], np.float32), np.array([[0, 1, 2]], np.int32), m)
+    s.point_light(tuple(k["point_light"]["pos"]), (k["point_light"]["I"],) * 3)
+    cam = scenes.camera(k["width"], k["height"], tuple(k["camera"]["eye"]), tuple(k["camera"]["look"]))
+    return s, scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, k["spp"], k["max_depth"])
+
+
+def test_li_capture_bit_exact():
+    """The reference's float Li capture, reproduced bit for bit."""
+    k = KATS["li_capture"]
+    s, rd = li_capture_scene()
+    rgb, rgba, _ = O.render(s, rd)
+    px = rgb.reshape(k["height"], k["width"], 3)[k["pixel"][1], k["pixel"][0]]
+    assert np.float32(px[0]).view(np.uint32) == np.float32(k["value"]).view(np.uint32)
+    assert px[0] == px[1] == px[2]
+    # analytic centre value 0.5/π · 9/3²
+    assert abs(px[0] - k["analytic_centre"]) < 1e-3
+
+
+def test_point_light_background_is_grey_08():
+    """F4: Whitted sums Light::Le = 0.8 over all lights on a miss → 8-bit 231."""
+    s, rd = scenes.config_c1(32, 32, 1)
+    rgb, rgba, _ = O.render(s, rd)
+    assert np.allclose(rgb[0], 0.8)
+    assert tuple(rgba[0]) == (231, 231, 231, 255)
+
+
+def test_sphere_lambert_analytic():
+    """F2 unpinned by the reference: a Lambertian sphere under a point light gives the analytic
+    value at the point nearest the light (Kd/π · I/d²)."""
+    s = scenes.Scene()
+    m = s.matte((0.5, 0.5, 0.5))
+    s.sphere((0.0, 0.0, 0.0), 1.0, m)
+    s.point_light((0.0, 0.0, 4.0), (9.0, 9.0, 9.0))
+    cam = scenes.camera(33, 33, (0.0, 0.0, 4.0), (0.0, 0.0, 0.0))
+    rgb, _, _ = O.render(s, scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 16, 5))
+    c = rgb.reshape(33, 33, 3)[16, 16, 0]
+    assert abs(c - 0.5 / math.pi * 9.0 / 9.0) < 2e-3
+
+
+def test_render_tiles_equal_full_frame():
+    """Per-pixel sample indices do not depend on tile ownership (Halton.cpp:61-81)."""
+    s, rd = scenes.config_c1(48, 40, 2)
+    full, full8, _ = O.render(s, rd)
+    from pysicalbasedraytracer_amd import tile_grid, assemble
+    tiles = tile_grid(48, 40, 16)
+    rd2 = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, tiles=tiles)
+    part, part8, _ = O.render(s, rd2)
+    frame = assemble(48, 40, tiles, part, 3)
+    assert np.array_equal(frame.reshape(-1, 3), full)
+
+
+def test_bvh_structure_invariants():
+    P, I = scenes.dragon_standin(n=24)
+    s = scenes.Scene()
+    m = s.matte((0.5, 0.5, 0.5))
+    s.mesh(P, I, m)
+    nodes, ids = O.build_bvh(s)
+    assert sorted(ids.tolist()) == list(range(I.shape[0]))
+    rec = nodes.view(np.uint8).reshape(-1, 32)
+    nprims = rec[:, 28:30].copy().view(np.uint16).ravel()
+    assert int(nprims.sum()) == I.shape[0]
+    assert rec.shape[0] == 2 * I.shape[0] - 1        # maxPrimsInNode = 1, distinct centroids
+
+
+def test_watertight_triangle_edge_tie_later_wins():
+    """F8: t == tMax accepted → on a shared edge the later-tested primitive wins; our
+    intersect reports it."""
+    tri = np.array([0, 0, 0, 1, 0, 0, 0, 1, 0], np.float32)
+    hit = O.triangle_test(tri, np.array([0.25, 0.25, 1, 0, 0, -1, np.inf], np.float32))
+    assert hit[0] == 1 and hit[1] == np.float32(1.0)
+    miss = O.triangle_test(tri, np.array([0.75, 0.75, 1, 0, 0, -1, np.inf], np.float32))
+    assert miss[0] == 0
+    # tMax equal to the hit distance is still a hit
+    tie = O.triangle_test(tri, np.array([0.25, 0.25, 1, 0, 0, -1, 1.0], np.float32))
+    assert tie[0] == 1
