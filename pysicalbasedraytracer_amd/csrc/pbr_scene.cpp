@@ -491,6 +491,7 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
             flags |= PRIM_SPHERE;
             tv[0] = bitsf((uint32_t)sphereIndex[p.shape]);
         }
+        tv[3] = bitsf((uint32_t)flags);   // the traversal reads the primitive flags from v0.w
         int32_t* pi = &S->primInfo[(size_t)slot * 4];
         pi[0] = flags;
         pi[1] = sd.material;

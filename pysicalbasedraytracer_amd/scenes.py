@@ -69,9 +69,10 @@ def _xf(t):
 
 # ----------------------------------------------------------------------------- geometry
 def dragon_standin(n=224, center=(0.0, 0.0, 0.0), radius=1.0):
-    """Deterministic displaced UV sphere, 2·n·(n−1) triangles (100,352 at n=224), SURVEY §8(d):
-    r = 1 + 0.08·sin7θ·cos9φ + 0.03·sin(31θ+17φ)."""
-    th = np.linspace(0.0, math.pi, n, dtype=np.float64)
+    """Deterministic displaced UV sphere, (n+1) latitude rows × n longitudes → 2·n·n triangles
+    (100,352 at n=224), SURVEY §8(d): r = 1 + 0.08·sin7θ·cos9φ + 0.03·sin(31θ+17φ)."""
+    rows = n + 1
+    th = np.linspace(0.0, math.pi, rows, dtype=np.float64)
     ph = np.linspace(0.0, 2 * math.pi, n + 1, dtype=np.float64)[:-1]
     T, Pp = np.meshgrid(th, ph, indexing="ij")
     r = radius * (1.0 + 0.08 * np.sin(7 * T) * np.cos(9 * Pp) + 0.03 * np.sin(31 * T + 17 * Pp))
@@ -80,7 +81,7 @@ def dragon_standin(n=224, center=(0.0, 0.0, 0.0), radius=1.0):
     z = r * np.sin(T) * np.sin(Pp)
     P = np.stack([x + center[0], y + center[1], z + center[2]], axis=-1).reshape(-1, 3).astype(f32)
     idx = []
-    for i in range(n - 1):
+    for i in range(rows - 1):
         a = i * n + np.arange(n)
         b = i * n + (np.arange(n) + 1) % n
         c = (i + 1) * n + np.arange(n)
@@ -89,7 +90,7 @@ def dragon_standin(n=224, center=(0.0, 0.0, 0.0), radius=1.0):
         idx.append(np.stack([b, c, d], axis=1))
     I = np.concatenate(idx, axis=0).astype(np.int32)
     # interleave to keep neighbouring triangles adjacent in prims order
-    I = I.reshape(2, n - 1, n, 3).transpose(1, 2, 0, 3).reshape(-1, 3)
+    I = I.reshape(rows - 1, 2, n, 3).transpose(0, 2, 1, 3).reshape(-1, 3)
     return P, np.ascontiguousarray(I)
 
 

@@ -109,7 +109,10 @@ def test_bvh_structure_invariants():
     rec = nodes.view(np.uint8).reshape(-1, 32)
     nprims = rec[:, 28:30].copy().view(np.uint16).ravel()
     assert int(nprims.sum()) == I.shape[0]
-    assert rec.shape[0] == 2 * I.shape[0] - 1        # maxPrimsInNode = 1, distinct centroids
+    leaves = int((nprims > 0).sum())
+    assert rec.shape[0] == 2 * leaves - 1            # full binary tree
+    # maxPrimsInNode = 1: only coincident-centroid sets (the degenerate pole triangles) share a leaf
+    assert leaves >= I.shape[0] - 2 * 24
 
 
 def test_watertight_triangle_edge_tie_later_wins():
