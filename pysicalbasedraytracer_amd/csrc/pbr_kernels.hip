@@ -9,6 +9,7 @@
 // transform runs in the same kernel (no second pass over HBM).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -483,6 +484,8 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
     }
 }
 
+#include "pbr_wavefront.h"
+
 // ---------------------------------------------------------------- introspection kernels
 __global__ void k_sampler_values(DeviceSampler smp, HaltonParams hp, int n, const int32_t* q, float* out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -550,6 +553,8 @@ struct pbr_hip_ctx {
     DevBuf dNodes, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
+    // wavefront queues and per-sample records (pbr_wavefront.h)
+    DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wCnt;
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
 };
@@ -615,6 +620,67 @@ int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
     HIP_TRY(ctx->dFunc.upload(func, ctx->stream));
     ctx->funcInt = fi;
     ctx->curStrategy = strategy;
+    return PBR_OK;
+}
+
+
+// Wavefront Whitted: chunks of ~2^23 samples, per level shade → shadow → extend (pbr_wavefront.h).
+int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
+    const int spp = P.spp;
+    long long chunkPix = std::max(1LL, (1LL << 23) / spp);
+    if (chunkPix > P.nPixels) chunkPix = P.nPixels;
+    const size_t cap = (size_t)chunkPix * spp;
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(ctx->wqO[k].ensure(cap * 16)); HIP_TRY(ctx->wqD[k].ensure(cap * 16));
+        HIP_TRY(ctx->wqId[k].ensure(cap * 4)); HIP_TRY(ctx->wqHit[k].ensure(cap * 16));
+    }
+    HIP_TRY(ctx->wsO.ensure(cap * 16)); HIP_TRY(ctx->wsD.ensure(cap * 16));
+    HIP_TRY(ctx->wsC.ensure(cap * 16)); HIP_TRY(ctx->wsId.ensure(cap * 4));
+    const int levels = P.maxDepth < 1 ? 1 : P.maxDepth;
+    HIP_TRY(ctx->wRecA.ensure(cap * 16 * levels)); HIP_TRY(ctx->wRecF.ensure(cap * 16 * levels));
+    HIP_TRY(ctx->wRecP.ensure(cap * 4 * levels)); HIP_TRY(ctx->wDepth.ensure(cap * 4));
+    HIP_TRY(ctx->wCnt.ensure(16));
+    int* cnt = (int*)ctx->wCnt.p;
+    WfParams W;
+    std::memset(&W, 0, sizeof(W));
+    W.P = P;
+    W.so = (float4*)ctx->wsO.p; W.sd = (float4*)ctx->wsD.p; W.sc = (float4*)ctx->wsC.p; W.sid = (int*)ctx->wsId.p;
+    W.shadowCount = cnt + 2;
+    W.recA = (float4*)ctx->wRecA.p; W.recF = (float4*)ctx->wRecF.p; W.recP = (float*)ctx->wRecP.p;
+    W.depthOf = (int*)ctx->wDepth.p;
+    W.cap = (int)cap;
+    auto queue = [&](int k) {
+        WfQueue q;
+        q.o = (float4*)ctx->wqO[k].p; q.d = (float4*)ctx->wqD[k].p; q.id = (int*)ctx->wqId[k].p; q.hit = (float4*)ctx->wqHit[k].p;
+        return q;
+    };
+    const dim3 blk(256), gstride(2048);
+    for (long long p0 = 0; p0 < P.nPixels; p0 += chunkPix) {
+        W.chunkPix0 = p0;
+        W.chunkPix = (int)std::min<long long>(chunkPix, P.nPixels - p0);
+        W.nSamples = W.chunkPix * spp;
+        int cur = 0;
+        W.cur = queue(0);
+        hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
+        const int maxLevels = levels + 2;   // + pass-through hits on material-less primitives
+        for (int level = 0; level < maxLevels; ++level) {
+            W.cur = queue(cur);
+            W.next = queue(cur ^ 1);
+            W.curCount = cnt + cur;
+            W.nextCount = cnt + (cur ^ 1);
+            HIP_TRY(hipMemsetAsync(W.nextCount, 0, 4, s));
+            HIP_TRY(hipMemsetAsync(W.shadowCount, 0, 4, s));
+            hipLaunchKernelGGL(k_wf_shade<0>, gstride, blk, 0, s, W, level == 0 ? 1 : 0);
+            hipLaunchKernelGGL(k_wf_shadow<0>, gstride, blk, 0, s, W);
+            if (level + 1 == maxLevels) break;
+            cur ^= 1;
+            W.cur = queue(cur);
+            W.curCount = cnt + cur;
+            hipLaunchKernelGGL(k_wf_extend<0>, gstride, blk, 0, s, W);
+        }
+        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + 255) / 256), blk, 0, s, W);
+    }
+    HIP_TRY(hipGetLastError());
     return PBR_OK;
 }
 
@@ -767,6 +833,9 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     HIP_TRY(hipEventRecord(ctx->ev0, s));
     if (blocks > 0) {
         bool st = d->collect_stats != 0;
+        const char* wfEnv = getenv("PBR_WAVEFRONT");
+        bool wavefront = d->integrator == PBR_INTEGRATOR_WHITTED && !st && ctx->host.lights.size() == 1 &&
+                         d->max_depth <= kWfMaxDepth && !(wfEnv && wfEnv[0] == '0');
         // waves per SIMD the megakernel is compiled for: trades VGPRs for scratch (PBR_OCC=1|2|4)
         int occ = 2;   // measured: 2 waves/SIMD beats 1 by 1.78x on C2 and ties 4
         if (const char* e = getenv("PBR_OCC")) occ = atoi(e);
@@ -775,7 +844,10 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     else if (occ >= 4) hipLaunchKernelGGL((k_render<I, false, 4>), grid, block, 0, s, P);            \
     else if (occ >= 2) hipLaunchKernelGGL((k_render<I, false, 2>), grid, block, 0, s, P);            \
     else hipLaunchKernelGGL((k_render<I, false, 1>), grid, block, 0, s, P);
-        switch (d->integrator) {
+        if (wavefront) {
+            int rc = render_wavefront(ctx, P, s);
+            if (rc) return rc;
+        } else switch (d->integrator) {
         case PBR_INTEGRATOR_WHITTED: PBR_LAUNCH(PBR_INTEGRATOR_WHITTED) break;
         case PBR_INTEGRATOR_PATH: PBR_LAUNCH(PBR_INTEGRATOR_PATH) break;
         default: PBR_LAUNCH(PBR_INTEGRATOR_VOLPATH) break;

@@ -1,0 +1,249 @@
+// pbr_wavefront.h — wavefront schedule for WhittedIntegrator::Li (WhittedIntegrator.cpp:11-65).
+// Included by pbr_kernels.hip inside its anonymous namespace (uses KParams, the sampler, film_out).
+//
+// The megakernel keeps a whole recursion's state live while it traverses the BVH, which caps it at
+// 2 waves/SIMD.  Here each stage is its own small kernel, so the latency-bound traversals run at
+// high occupancy:
+//
+//   k_wf_camera_extend   sampler dims 0-4 → camera ray → closest hit          (level 0, 1 lane/sample)
+//   k_wf_shade           SI + BSDF; light sample → shadow queue; SpecularReflect → next ray queue
+//   k_wf_shadow          any-hit; visible → rec[depth].A += contribution   (one light → no ordering issue)
+//   k_wf_extend          closest hit for the continuation queue
+//   k_wf_finish          fold L_k = A_k + ((F_k·L_{k+1})·c_k)/pdf_k deepest-first, per-pixel in-order sum, film
+//
+// Queues are SoA in HBM and compacted with one atomic per wave (ballot + popcount).  Records are
+// indexed by sample so the fold reproduces the recursive evaluation bit for bit.
+#pragma once
+
+constexpr int kWfMaxDepth = 8;
+
+struct WfQueue {
+    float4* o;      // origin.xyz, tMax
+    float4* d;      // dir.xyz, packed (dim | depth << 16) as int bits
+    int* id;        // sample index within the chunk
+    float4* hit;    // slot (int bits, -1 = miss), b0, b1, b2
+};
+struct WfParams {
+    KParams P;
+    long long chunkPix0;   // first packed pixel of the chunk
+    int chunkPix;          // pixels in the chunk
+    int nSamples;          // chunkPix * spp
+    WfQueue cur, next;
+    int* curCount;
+    int* nextCount;
+    // shadow queue
+    float4* so; float4* sd; float4* sc; int* sid; int* shadowCount;
+    // per-sample records, [depth * cap + sample]
+    float4* recA;          // A.rgb, flags (bit0: add +0 at the end)
+    float4* recF;          // F.rgb, cos term
+    float* recP;           // pdf
+    int* depthOf;          // deepest level of each sample
+    int cap;               // record stride (>= nSamples)
+};
+
+__device__ __forceinline__ int wave_push(int* counter, bool pred) {
+    unsigned long long m = __ballot(pred);
+    int lane = (int)__lane_id();
+    int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (m != 0ull && lane == leader) base = atomicAdd(counter, (int)__popcll(m));
+    base = __shfl(base, leader < 0 ? 0 : leader);
+    return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+__device__ __forceinline__ int pack_dd(int dim, int depth) { return (dim & 0xffff) | (depth << 16); }
+
+template <int DUMMY>
+__global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
+    const KParams& P = W.P;
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= W.nSamples) return;
+    int lp = q / P.spp, s = q - lp * P.spp;
+    int x, y;
+    pixel_xy(P, W.chunkPix0 + lp, &x, &y);
+    SState st;
+    st.index = halton_pixel_offset(hparams(P.smp), x, y) + (uint32_t)s * (uint32_t)P.smp.stride;
+    st.dim = 0;
+    float u0, u1, l0, l1;
+    get2d(P.smp, st, &u0, &u1);
+    get1d(P.smp, st);
+    get2d(P.smp, st, &l0, &l1);
+    Ray r = camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
+    HitRec h;
+    Counters c;
+    bool hit = traverse<false, false>(P.S, r, &h, &c);
+    W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
+    W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(st.dim, 0)));
+    W.cur.id[q] = q;
+    W.depthOf[q] = 0;                          // a sample dropped by the level cap reads black
+    W.recA[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
+}
+
+template <int DUMMY>
+__global__ __launch_bounds__(256) void k_wf_extend(WfParams W) {
+    int n = *W.curCount;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        float4 o = W.cur.o[q], d = W.cur.d[q];
+        Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+        HitRec h;
+        Counters c;
+        bool hit = traverse<false, false>(W.P.S, r, &h, &c);
+        W.cur.o[q].w = r.tMax;
+        W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
+    }
+}
+
+// One level of WhittedIntegrator::Li for every queued ray (single-light scenes).
+template <int DUMMY>
+__global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
+    const KParams& P = W.P;
+    const DeviceScene& S = P.S;
+    int n = level0 ? W.nSamples : *W.curCount;
+    int stride = gridDim.x * blockDim.x;
+    int nIter = (n + stride - 1) / stride;
+    for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
+        int q = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        bool active = q < n;
+        bool pushShadow = false, pushNext = false;
+        int id = 0, depth = 0, dim = 0, emitDepth = 0;
+        Ray ray, shadow, cont;
+        rgb contrib = sp(0.f);
+        if (active) {
+            float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
+            id = W.cur.id[q];
+            int dd = __float_as_int(d.w);
+            dim = dd & 0xffff;
+            depth = dd >> 16;
+            emitDepth = depth;
+            ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+            int slot = __float_as_int(hr.x);
+            size_t ri = (size_t)depth * W.cap + id;
+            if (slot < 0) {   // miss: Σ over all lights of Le (F4)
+                rgb L = sp(0.f);
+                for (int i = 0; i < S.nLights; ++i) L = L + light_Le(S, S.lights[i], ray);
+                W.recA[ri] = make_float4(L.r, L.g, L.b, 0.f);
+                W.depthOf[id] = depth;
+            } else {
+                Isect isect;
+                int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
+                if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
+                else triangle_si(S, slot, ray, hr.y, hr.z, hr.w, flags, &isect);
+                isect.slot = slot;
+                isect.medIn = isect.medOut = -1;
+                BSDF bsdf;
+                if (!make_bsdf(S, isect, false, &bsdf)) {
+                    cont = spawn_ray(isect, ray.d);        // Li(isect.SpawnRay(ray.d), depth)
+                    pushNext = true;
+                } else {
+                    f3 n = isect.sn, wo = isect.wo;
+                    rgb L = sp(0.f);
+                    L = L + si_Le(S, isect, wo);
+                    SState st;
+                    st.index = 0;
+                    st.dim = dim;
+                    // the sample index is recomputed from the sample id
+                    int lp = id / P.spp, s = id - lp * P.spp;
+                    int x, y;
+                    pixel_xy(P, W.chunkPix0 + lp, &x, &y);
+                    st.index = halton_pixel_offset(hparams(P.smp), x, y) + (uint32_t)s * (uint32_t)P.smp.stride;
+                    {   // the single light (WhittedIntegrator.cpp:39-54)
+                        f3 wi;
+                        float pdf;
+                        VisPt vis;
+                        float a, b;
+                        get2d(P.smp, st, &a, &b);
+                        rgb Li = sample_li(S, S.lights[0], isect, a, b, &wi, &pdf, &vis);
+                        if (!(black(Li) || pdf == 0)) {
+                            rgb f = bsdf_f(bsdf, wo, wi, BSDF_ALL);
+                            if (!black(f)) {
+                                contrib = f * Li * absdot(wi, n) / pdf;
+                                shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
+                                pushShadow = true;
+                            }
+                        }
+                    }
+                    float flagsA = 0.f;
+                    bool final_ = true;
+                    if (depth + 1 < P.maxDepth) {   // SpecularReflect (Integrator.cpp:179-222)
+                        f3 wi = mk(0, 0, 0);
+                        float pdf = 0;
+                        int stype = 0;
+                        float a, b;
+                        get2d(P.smp, st, &a, &b);
+                        rgb f = bsdf_sample(bsdf, wo, &wi, a, b, &pdf, BSDF_REFLECTION | BSDF_SPECULAR, &stype);
+                        if (!black(f) && pdf > 0.f && absdot(wi, isect.sn) != 0.f && depth + 1 < kWfMaxDepth) {
+                            W.recF[ri] = make_float4(f.r, f.g, f.b, absdot(wi, isect.sn));
+                            W.recP[ri] = pdf;
+                            cont = spawn_ray(isect, wi);
+                            pushNext = true;
+                            final_ = false;
+                            depth += 1;
+                        } else {
+                            flagsA = 1.f;   // L += Spectrum(0) from a failed SpecularReflect
+                        }
+                    }
+                    W.recA[ri] = make_float4(L.r, L.g, L.b, flagsA);
+                    if (final_) W.depthOf[id] = depth;
+                    dim = st.dim;
+                }
+            }
+        }
+        int si = wave_push(W.shadowCount, pushShadow);
+        if (pushShadow) {   // the visibility result lands in the level that emitted the ray
+            W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
+            W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(emitDepth));
+            W.sc[si] = make_float4(contrib.r, contrib.g, contrib.b, 0.f);
+            W.sid[si] = id;
+        }
+        int ni = wave_push(W.nextCount, pushNext);
+        if (pushNext) {
+            W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
+            W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_dd(dim, depth)));
+            W.next.id[ni] = id;
+        }
+    }
+}
+
+// any-hit for the shadow queue; a visible light adds its contribution to the emitting level
+template <int DUMMY>
+__global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
+    int n = *W.shadowCount;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        float4 o = W.so[q], d = W.sd[q];
+        Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+        HitRec h;
+        Counters c;
+        if (!traverse<true, false>(W.P.S, r, &h, &c)) {
+            int id = W.sid[q];
+            float4 cc = W.sc[q];
+            size_t ri = (size_t)__float_as_int(d.w) * W.cap + id;
+            float4 A = W.recA[ri];
+            A.x = A.x + cc.x; A.y = A.y + cc.y; A.z = A.z + cc.z;
+            W.recA[ri] = A;
+        }
+    }
+}
+
+// fold the recursion and run the film for every pixel of the chunk
+template <int DUMMY>
+__global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
+    const KParams& P = W.P;
+    int lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= W.chunkPix) return;
+    rgb acc = sp(0.0f);
+    for (int s = 0; s < P.spp; ++s) {
+        int id = lp * P.spp + s;
+        int dpt = W.depthOf[id];
+        float4 a = W.recA[(size_t)dpt * W.cap + id];
+        rgb L = sp3(a.x, a.y, a.z);
+        if (a.w != 0.f) L = L + sp(0.f);
+        for (int k = dpt - 1; k >= 0; --k) {
+            size_t ri = (size_t)k * W.cap + id;
+            float4 A = W.recA[ri], F = W.recF[ri];
+            float pdf = W.recP[ri];
+            L = sp3(A.x, A.y, A.z) + sp3(F.x, F.y, F.z) * L * F.w / pdf;
+        }
+        acc = acc + L;
+    }
+    film_out(P, W.chunkPix0 + lp, acc);
+}

@@ -208,3 +208,15 @@ def test_errors_fail_loudly(hip):
     with pytest.raises(RuntimeError):
         fresh.render(bad)
     fresh.close()
+
+
+def test_wavefront_equals_megakernel(hip, monkeypatch):
+    """The wavefront Whitted schedule and the megakernel produce identical bits."""
+    s, rd = scenes.config_c2(160, 90, 8, mesh=small_dragon(64))
+    hip.upload(s)
+    monkeypatch.setenv("PBR_WAVEFRONT", "1")
+    wf, wf8, _ = hip.render(rd)
+    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    mk, mk8, _ = hip.render(rd)
+    assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32))
+    assert np.array_equal(wf8, mk8)
