@@ -179,10 +179,9 @@ __device__ void sphere_si(const SphereRec& s, const Ray& r, float t, Isect* si) 
 
 __device__ __forceinline__ bool prim_hit(const DeviceScene& S, int slot, const Ray& r, float* t, float* b0, float* b1, float* b2) {
     const float4* tv = S.triVerts + 3 * (size_t)slot;
-    float4 v0 = tv[0];
+    float4 v0 = tv[0], v1 = tv[1], v2 = tv[2];   // one 48-B record; issue all loads before the branch
     int flags = __float_as_int(v0.w);
     if (flags & PRIM_SPHERE) return sphere_test(S.spheres[__float_as_int(v0.x)], r, t);
-    float4 v1 = tv[1], v2 = tv[2];
     return tri_test(mk(v0.x, v0.y, v0.z), mk(v1.x, v1.y, v1.z), mk(v2.x, v2.y, v2.z), r, t, b0, b1, b2);
 }
 

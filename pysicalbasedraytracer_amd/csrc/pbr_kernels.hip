@@ -661,24 +661,25 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
         W.cur = queue(0);
+        W.nextCount = cnt + 1;
         hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
-        const int maxLevels = levels + 2;   // + pass-through hits on material-less primitives
+        // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
+        const int maxLevels = levels + (ctx->host.anyNoMaterial ? 2 : 0);
         for (int level = 0; level < maxLevels; ++level) {
             W.cur = queue(cur);
             W.next = queue(cur ^ 1);
             W.curCount = cnt + cur;
             W.nextCount = cnt + (cur ^ 1);
-            HIP_TRY(hipMemsetAsync(W.nextCount, 0, 4, s));
-            HIP_TRY(hipMemsetAsync(W.shadowCount, 0, 4, s));
             hipLaunchKernelGGL(k_wf_shade<0>, gstride, blk, 0, s, W, level == 0 ? 1 : 0);
             hipLaunchKernelGGL(k_wf_shadow<0>, gstride, blk, 0, s, W);
             if (level + 1 == maxLevels) break;
             cur ^= 1;
             W.cur = queue(cur);
             W.curCount = cnt + cur;
+            W.nextCount = cnt + (cur ^ 1);   // reset by the extend kernel for the next shade
             hipLaunchKernelGGL(k_wf_extend<0>, gstride, blk, 0, s, W);
         }
-        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + 255) / 256), blk, 0, s, W);
+        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + 3) / 4), blk, 0, s, W);
     }
     HIP_TRY(hipGetLastError());
     return PBR_OK;

@@ -499,6 +499,10 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
         if (sd.medium_inside >= d->n_media || sd.medium_outside >= d->n_media) fail("medium index out of range");
         pi[3] = (int32_t)(((uint32_t)(sd.medium_inside & 0xffff)) | ((uint32_t)(sd.medium_outside & 0xffff) << 16));
     }
+    for (int slot = 0; slot < np; ++slot) {
+        int m = S->primInfo[(size_t)slot * 4 + 1];
+        if (m < 0 || d->materials[m].type == PBR_MAT_NONE) S->anyNoMaterial = true;
+    }
     // 4. materials → lobe templates for allowMultipleLobes = false / true
     S->materials.clear();
     for (int m = 0; m < d->n_materials; ++m) {

@@ -35,6 +35,7 @@ struct HostScene {
     float lightFuncInt = 0;
     std::vector<float> lightPower;          // Power().y() per light (LightDistrib.cpp:36-41)
     std::vector<float> media;               // 10 floats per medium
+    bool anyNoMaterial = false;             // some primitive has material == nullptr
 };
 
 // Throws std::invalid_argument on a malformed descriptor.

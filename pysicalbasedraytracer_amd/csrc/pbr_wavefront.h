@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(st.dim, 0)));
     W.cur.id[q] = q;
+    if (q == 0) { *W.nextCount = 0; *W.shadowCount = 0; }   // queue counters of the level-0 shade
     W.depthOf[q] = 0;                          // a sample dropped by the level cap reads black
     W.recA[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
@@ -82,6 +83,7 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
 template <int DUMMY>
 __global__ __launch_bounds__(256) void k_wf_extend(WfParams W) {
     int n = *W.curCount;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { *W.nextCount = 0; *W.shadowCount = 0; }   // for the next shade
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
         float4 o = W.cur.o[q], d = W.cur.d[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -147,18 +149,43 @@ __global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
                     pixel_xy(P, W.chunkPix0 + lp, &x, &y);
                     st.index = halton_pixel_offset(hparams(P.smp), x, y) + (uint32_t)s * (uint32_t)P.smp.stride;
                     {   // the single light (WhittedIntegrator.cpp:39-54)
-                        f3 wi;
-                        float pdf;
-                        VisPt vis;
                         float a, b;
                         get2d(P.smp, st, &a, &b);
-                        rgb Li = sample_li(S, S.lights[0], isect, a, b, &wi, &pdf, &vis);
-                        if (!(black(Li) || pdf == 0)) {
-                            rgb f = bsdf_f(bsdf, wo, wi, BSDF_ALL);
-                            if (!black(f)) {
-                                contrib = f * Li * absdot(wi, n) / pdf;
-                                shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
-                                pushShadow = true;
+                        // Reordered but equivalent: f(wo, wi) does not depend on Li, and nothing is
+                        // added when f is black — so the light's radiance (for the SkyBox: atan2,
+                        // asin and an env gather) is only evaluated when f is not black, and a
+                        // purely specular BSDF (f ≡ 0) skips the light sample altogether.
+                        if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0) {
+                            f3 wi;
+                            float pdf;
+                            VisPt vis;
+                            const DLight& light = S.lights[0];
+                            rgb Li;
+                            if (light.type == LT_SKY) {
+                                wi = uniform_sphere(a, b);
+                                pdf = 1.f / (4 * kPi);
+                                vis.p = isect.p + wi * (2 * light.worldRadius); vis.pError = mk(0, 0, 0); vis.n = mk(0, 0, 0);
+                                rgb f = bsdf_f(bsdf, wo, wi, BSDF_ALL);
+                                if (!black(f)) {
+                                    float ul, vl;
+                                    sphere_uv(normalize(wi), &ul, &vl);
+                                    Li = light.envW > 0 ? sky_value(S, light, ul, vl) : sp(0.f);
+                                    if (!black(Li)) {
+                                        contrib = f * Li * absdot(wi, n) / pdf;
+                                        shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
+                                        pushShadow = true;
+                                    }
+                                }
+                            } else {
+                                Li = sample_li(S, light, isect, a, b, &wi, &pdf, &vis);
+                                if (!(black(Li) || pdf == 0)) {
+                                    rgb f = bsdf_f(bsdf, wo, wi, BSDF_ALL);
+                                    if (!black(f)) {
+                                        contrib = f * Li * absdot(wi, n) / pdf;
+                                        shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
+                                        pushShadow = true;
+                                    }
+                                }
                             }
                         }
                     }
@@ -224,26 +251,41 @@ __global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
     }
 }
 
-// fold the recursion and run the film for every pixel of the chunk
+// Fold the recursion and run the film: one wave per pixel, lane = sample (coalesced record reads),
+// then lane 0 adds the 64 folded values in sample order (the reference's colObj += Li order).
 template <int DUMMY>
 __global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
+    __shared__ float lds[4][64 * 3];
     const KParams& P = W.P;
-    int lp = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lp >= W.chunkPix) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lp = blockIdx.x * 4 + wave;
+    if (lp >= W.chunkPix) return;          // wave-uniform
     rgb acc = sp(0.0f);
-    for (int s = 0; s < P.spp; ++s) {
-        int id = lp * P.spp + s;
-        int dpt = W.depthOf[id];
-        float4 a = W.recA[(size_t)dpt * W.cap + id];
-        rgb L = sp3(a.x, a.y, a.z);
-        if (a.w != 0.f) L = L + sp(0.f);
-        for (int k = dpt - 1; k >= 0; --k) {
-            size_t ri = (size_t)k * W.cap + id;
-            float4 A = W.recA[ri], F = W.recF[ri];
-            float pdf = W.recP[ri];
-            L = sp3(A.x, A.y, A.z) + sp3(F.x, F.y, F.z) * L * F.w / pdf;
+    for (int base = 0; base < P.spp; base += 64) {
+        int s = base + lane;
+        rgb L = sp(0.f);
+        if (s < P.spp) {
+            int id = lp * P.spp + s;
+            int dpt = W.depthOf[id];
+            float4 a = W.recA[(size_t)dpt * W.cap + id];
+            L = sp3(a.x, a.y, a.z);
+            if (a.w != 0.f) L = L + sp(0.f);
+            for (int k = dpt - 1; k >= 0; --k) {
+                size_t ri = (size_t)k * W.cap + id;
+                float4 A = W.recA[ri], F = W.recF[ri];
+                float pdf = W.recP[ri];
+                L = sp3(A.x, A.y, A.z) + sp3(F.x, F.y, F.z) * L * F.w / pdf;
+            }
         }
-        acc = acc + L;
+        lds[wave][3 * lane] = L.r; lds[wave][3 * lane + 1] = L.g; lds[wave][3 * lane + 2] = L.b;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane == 0) {
+            int cnt = P.spp - base < 64 ? P.spp - base : 64;
+            for (int k = 0; k < cnt; ++k) acc = acc + sp3(lds[wave][3 * k], lds[wave][3 * k + 1], lds[wave][3 * k + 2]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    film_out(P, W.chunkPix0 + lp, acc);
+    if (lane == 0) film_out(P, W.chunkPix0 + lp, acc);
 }
