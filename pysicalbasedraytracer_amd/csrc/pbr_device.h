@@ -187,13 +187,24 @@ __device__ __forceinline__ bool prim_hit(const DeviceScene& S, int slot, const R
 
 // BVHAccel::Intersect / IntersectP (BVHAccel.cpp:285-366): the same near-first order (dirIsNeg of
 // the node's split axis) so ties between primitives resolve exactly as on the CPU (F8).
-template <bool ANY, bool STATS>
+// Short traversal stack in LDS for the 256-lane wavefront kernels: entries [0, SHORT) live in LDS
+// ([entry][lane], conflict-free), deeper ones in the private (scratch) array.  Only where entries
+// are kept changes; the visit order does not.
+constexpr int kShortStack = 16;
+__shared__ int s_trav_stack[kShortStack * 256];
+
+template <bool ANY, bool STATS, int SHORT = 0>
 __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
+    static_assert(SHORT == 0 || SHORT == kShortStack, "short stack is kShortStack deep");
     if (STATS) c->rays++;
     if (S.nNodes == 0) return false;
     f3 inv = ANY ? mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z) : mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
     bool n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
-    int stack[64];
+    int stack[64 - SHORT];
+    int* lstack = nullptr;
+    if constexpr (SHORT > 0) lstack = s_trav_stack + threadIdx.x;
+    auto push = [&](int sp_, int v) { if (SHORT && sp_ < SHORT) lstack[sp_ * 256] = v; else stack[sp_ - SHORT] = v; };
+    auto pop = [&](int sp_) { return (SHORT && sp_ < SHORT) ? lstack[sp_ * 256] : stack[sp_ - SHORT]; };
     int sp = 0, cur = 0;
     bool found = false;
     while (true) {
@@ -215,17 +226,17 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
                     }
                 }
                 if (sp == 0) break;
-                cur = stack[--sp];
+                cur = pop(--sp);
             } else {
                 int axis = (int)((meta >> 16) & 0xffu);
                 bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
                 if (sp >= 64) break;   // BVHAccel's 64-entry stack; the SAH builds here stay < 30 deep
-                if (neg) { stack[sp++] = cur + 1; cur = off; }
-                else { stack[sp++] = off; cur = cur + 1; }
+                if (neg) { push(sp++, cur + 1); cur = off; }
+                else { push(sp++, off); cur = cur + 1; }
             }
         } else {
             if (sp == 0) break;
-            cur = stack[--sp];
+            cur = pop(--sp);
         }
     }
     return found;
@@ -366,10 +377,15 @@ PBR_HD f3 tr_sample_wh(const Lobe& l, f3 wo, float u0, float u1) {
 }
 PBR_HD float tr_pdf(const Lobe& l, f3 wo, f3 wh) { return tr_D(l, wh) * tr_G1(l, wo) * absdot(wo, wh) / abscos_t(wo); }
 
+// K: bit mask of the LobeKinds the caller can meet (the scene's materials, or what a type filter
+// admits); kinds outside it compile out, which keeps the microfacet code out of simple kernels.
+constexpr int kAllLobes = 0x7f;
+#define PBR_HAS(K, kind) (((K) >> (kind)) & 1)
+template <int K = kAllLobes>
 PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
     switch (l.kind) {
-    case L_LAMBERT: return ld3(l.R) * kInvPi;
-    case L_OREN: {
+    case L_LAMBERT: if constexpr (PBR_HAS(K, L_LAMBERT)) return ld3(l.R) * kInvPi; break;
+    case L_OREN: if constexpr (PBR_HAS(K, L_OREN)) {
         float sI = sin_t(wi), sO = sin_t(wo);
         float maxCos = 0;
         if ((double)sI > 1e-4 && (double)sO > 1e-4) {
@@ -380,8 +396,8 @@ PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
         if (abscos_t(wi) > abscos_t(wo)) { sinAlpha = sO; tanBeta = sI / abscos_t(wi); }
         else { sinAlpha = sI; tanBeta = sO / abscos_t(wo); }
         return ld3(l.R) * kInvPi * (l.A + l.B * maxCos * sinAlpha * tanBeta);
-    }
-    case L_MF_R: {
+    } break;
+    case L_MF_R: if constexpr (PBR_HAS(K, L_MF_R)) {
         float cO = abscos_t(wo), cI = abscos_t(wi);
         f3 wh = wi + wo;
         if (cI == 0 || cO == 0) return sp(0.f);
@@ -389,8 +405,8 @@ PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
         wh = normalize(wh);
         rgb F = fresnel_eval(l, dot(wi, faceforward(wh, mk(0, 0, 1))));
         return ld3(l.R) * tr_D(l, wh) * tr_G(l, wo, wi) * F / (4 * cI * cO);
-    }
-    case L_MF_T: {
+    } break;
+    case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
         if (same_hemi(wo, wi)) return sp(0.f);
         float cO = cos_t(wo), cI = cos_t(wi);
         if (cI == 0 || cO == 0) return sp(0.f);
@@ -404,19 +420,23 @@ PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
         return (sp(1.f) - F) * ld3(l.T) *
                fabsf(tr_D(l, wh) * tr_G(l, wo, wi) * eta * eta * absdot(wi, wh) * absdot(wo, wh) * factor * factor /
                      (cI * cO * sqrtDenom * sqrtDenom));
+    } break;
+    default: break;
     }
-    default: return sp(0.f);
-    }
+    return sp(0.f);
 }
+template <int K = kAllLobes>
 PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
     switch (l.kind) {
-    case L_LAMBERT: case L_OREN: return same_hemi(wo, wi) ? abscos_t(wi) * kInvPi : 0;
-    case L_MF_R: {
+    case L_LAMBERT: case L_OREN:
+        if constexpr (PBR_HAS(K, L_LAMBERT) || PBR_HAS(K, L_OREN)) return same_hemi(wo, wi) ? abscos_t(wi) * kInvPi : 0;
+        break;
+    case L_MF_R: if constexpr (PBR_HAS(K, L_MF_R)) {
         if (!same_hemi(wo, wi)) return 0;
         f3 wh = normalize(wo + wi);
         return tr_pdf(l, wo, wh) / (4 * dot(wo, wh));
-    }
-    case L_MF_T: {
+    } break;
+    case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
         if (same_hemi(wo, wi)) return 0;
         float eta = cos_t(wo) > 0 ? (l.etaB / l.etaA) : (l.etaA / l.etaB);
         f3 wh = normalize(wo + wi * eta);
@@ -424,9 +444,10 @@ PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
         float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
         float dwh = fabsf((eta * eta * dot(wi, wh)) / (sqrtDenom * sqrtDenom));
         return tr_pdf(l, wo, wh) * dwh;
+    } break;
+    default: break;
     }
-    default: return 0;
-    }
+    return 0;
 }
 // Sampling.cpp:74-92, Sampling.h:57-61
 PBR_HD void concentric_disk(float u0, float u1, float* dx, float* dy) {
@@ -444,20 +465,21 @@ PBR_HD f3 cosine_hemisphere(float u0, float u1) {
     float z = sqrtf(mx((float)0, 1 - dx * dx - dy * dy));
     return mk(dx, dy, z);
 }
+template <int K = kAllLobes>
 PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* pdf, int* st) {
     switch (l.kind) {
-    case L_LAMBERT: case L_OREN: {
+    case L_LAMBERT: case L_OREN: if constexpr (PBR_HAS(K, L_LAMBERT) || PBR_HAS(K, L_OREN)) {
         *wi = cosine_hemisphere(u0, u1);
         if (wo.z < 0) wi->z *= -1;
-        *pdf = lobe_pdf(l, wo, *wi);
-        return lobe_f(l, wo, *wi);
-    }
-    case L_SPEC_R: {
+        *pdf = lobe_pdf<K>(l, wo, *wi);
+        return lobe_f<K>(l, wo, *wi);
+    } break;
+    case L_SPEC_R: if constexpr (PBR_HAS(K, L_SPEC_R)) {
         *wi = mk(-wo.x, -wo.y, wo.z);
         *pdf = 1;
         return fresnel_eval(l, cos_t(*wi)) * ld3(l.R) / abscos_t(*wi);
-    }
-    case L_SPEC_T: {
+    } break;
+    case L_SPEC_T: if constexpr (PBR_HAS(K, L_SPEC_T)) {
         bool entering = cos_t(wo) > 0;
         float etaI = entering ? l.etaA : l.etaB, etaT = entering ? l.etaB : l.etaA;
         if (!refract_(wo, faceforward(mk(0, 0, 1), wo), etaI / etaT, wi)) return sp(0.f);
@@ -465,8 +487,8 @@ PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* 
         rgb ft = ld3(l.T) * (sp(1.f) - sp(fr_dielectric(cos_t(*wi), l.etaA, l.etaB)));
         ft = ft * ((etaI * etaI) / (etaT * etaT));
         return ft / abscos_t(*wi);
-    }
-    case L_FRESNEL_SPEC: {
+    } break;
+    case L_FRESNEL_SPEC: if constexpr (PBR_HAS(K, L_FRESNEL_SPEC)) {
         float F = fr_dielectric(cos_t(wo), l.etaA, l.etaB);
         if (u0 < F) {
             *wi = mk(-wo.x, -wo.y, wo.z);
@@ -482,25 +504,26 @@ PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* 
         *st = BSDF_SPECULAR | BSDF_TRANSMISSION;
         *pdf = 1 - F;
         return ft / abscos_t(*wi);
-    }
-    case L_MF_R: {
+    } break;
+    case L_MF_R: if constexpr (PBR_HAS(K, L_MF_R)) {
         if (wo.z == 0) return sp(0.f);
         f3 wh = tr_sample_wh(l, wo, u0, u1);
         if (dot(wo, wh) < 0) return sp(0.f);
         *wi = reflect_(wo, wh);
         if (!same_hemi(wo, *wi)) return sp(0.f);
         *pdf = tr_pdf(l, wo, wh) / (4 * dot(wo, wh));
-        return lobe_f(l, wo, *wi);
-    }
-    case L_MF_T: {
+        return lobe_f<K>(l, wo, *wi);
+    } break;
+    case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
         if (wo.z == 0) return sp(0.f);
         f3 wh = tr_sample_wh(l, wo, u0, u1);
         if (dot(wo, wh) < 0) return sp(0.f);
         float eta = cos_t(wo) > 0 ? (l.etaA / l.etaB) : (l.etaB / l.etaA);
         if (!refract_(wo, wh, eta, wi)) return sp(0.f);
-        *pdf = lobe_pdf(l, wo, *wi);
-        return lobe_f(l, wo, *wi);
-    }
+        *pdf = lobe_pdf<K>(l, wo, *wi);
+        return lobe_f<K>(l, wo, *wi);
+    } break;
+    default: break;
     }
     return sp(0.f);
 }
@@ -519,6 +542,7 @@ PBR_HD int num_components(const BSDF& b, int flags) {
     for (int i = 0; i < b.mt->nLobes; ++i) if (matches(b.mt->lobes[i], flags)) ++k;
     return k;
 }
+template <int K = kAllLobes>
 PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:56-71
     f3 wi = b.to_local(wiW), wo = b.to_local(woW);
     if (wo.z == 0) return sp(0.f);
@@ -527,10 +551,11 @@ PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cp
     for (int i = 0; i < b.mt->nLobes; ++i) {
         const Lobe& l = b.mt->lobes[i];
         if (matches(l, flags) && ((reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION))))
-            f = f + lobe_f(l, wo, wi);
+            f = f + lobe_f<K>(l, wo, wi);
     }
     return f;
 }
+template <int K = kAllLobes>
 PBR_HD float bsdf_pdf(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:92-106
     if (b.mt->nLobes == 0) return 0.f;
     f3 wo = b.to_local(woW), wi = b.to_local(wiW);
@@ -538,10 +563,11 @@ PBR_HD float bsdf_pdf(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflectio
     float pdf = 0.f;
     int m = 0;
     for (int i = 0; i < b.mt->nLobes; ++i)
-        if (matches(b.mt->lobes[i], flags)) { ++m; pdf += lobe_pdf(b.mt->lobes[i], wo, wi); }
+        if (matches(b.mt->lobes[i], flags)) { ++m; pdf += lobe_pdf<K>(b.mt->lobes[i], wo, wi); }
     return m > 0 ? pdf / m : 0.f;
 }
 // Reflection.cpp:108-164. On the wo.z == 0 early-out *pdf and *sampledType are left as they were.
+template <int K = kAllLobes>
 PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float* pdf, int type, int* sampledType) {
     int m = num_components(b, type);
     if (m == 0) { *pdf = 0; *sampledType = 0; return sp(0.f); }
@@ -556,13 +582,13 @@ PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float
     if (wo.z == 0) return sp(0.f);
     *pdf = 0;
     int st = bx.type;
-    rgb f = lobe_sample(bx, wo, &wi, ur0, u1, pdf, &st);
+    rgb f = lobe_sample<K>(bx, wo, &wi, ur0, u1, pdf, &st);
     *sampledType = st;
     if (*pdf == 0) { *sampledType = 0; return sp(0.f); }
     *wiW = b.to_world(wi);
     if (!(bx.type & BSDF_SPECULAR) && m > 1)
         for (int i = 0; i < b.mt->nLobes; ++i)
-            if (i != chosen && matches(b.mt->lobes[i], type)) *pdf += lobe_pdf(b.mt->lobes[i], wo, wi);
+            if (i != chosen && matches(b.mt->lobes[i], type)) *pdf += lobe_pdf<K>(b.mt->lobes[i], wo, wi);
     if (m > 1) *pdf /= m;
     if (!(bx.type & BSDF_SPECULAR)) {
         bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
@@ -570,16 +596,17 @@ PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float
         for (int i = 0; i < b.mt->nLobes; ++i) {
             const Lobe& l = b.mt->lobes[i];
             if (matches(l, type) && ((reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION))))
-                f = f + lobe_f(l, wo, wi);
+                f = f + lobe_f<K>(l, wo, wi);
         }
     }
     return f;
 }
 // SurfaceInteraction::ComputeScatteringFunctions → BSDF(si, eta) frame (Reflection.h:105-110)
-__device__ __forceinline__ bool make_bsdf(const DeviceScene& S, const Isect& si, bool multiLobe, BSDF* b) {
+// mats: S.materials, or a kernel's LDS copy of it
+__device__ __forceinline__ bool make_bsdf(const DeviceScene& S, const MatTemplate* mats, const Isect& si, bool multiLobe, BSDF* b) {
     int mat = S.primInfo[si.slot].y;
     if (mat < 0) return false;
-    const MatTemplate* mt = S.materials + 2 * mat + (multiLobe ? 1 : 0);
+    const MatTemplate* mt = mats + 2 * mat + (multiLobe ? 1 : 0);
     if (!mt->valid) return false;
     b->mt = mt;
     b->ns = si.sn;

@@ -36,20 +36,46 @@ __host__ __device__ __forceinline__ HaltonParams hparams(const DeviceSampler& s)
     return h;
 }
 
+// The low Halton dimensions a bounce loop samples over and over, staged in LDS by the kernels that
+// ask for it (LDS = true): one scrambled radical inverse is a chain of dependent digit-permutation
+// lookups, and ds_read latency is a fraction of an L1/L2 round trip.
+constexpr int kLdsDims = 64;
+constexpr int kLdsPermEntries = 8893;              // Σ of the first 64 primes
+__shared__ uint16_t s_halton_perm[kLdsPermEntries];
+__shared__ uint4 s_halton_tab[kLdsDims];           // prime, floor(2^32/prime), primeSums
+
+// Whole workgroup; call before the first LDS sample and follow with __syncthreads().
+__device__ void stage_halton_lds(const DeviceSampler& s) {
+    const int nd = s.ldsDims;
+    for (int i = threadIdx.x; i < nd; i += blockDim.x)
+        s_halton_tab[i] = make_uint4(s.primes[i], s.recips[i], s.primeSums[i], 0u);
+    const int n = nd > 0 ? (int)(s.primeSums[nd - 1] + s.primes[nd - 1]) : 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s_halton_perm[i] = s.perms[i];
+}
+
+template <bool LDS = false>
 __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int dim) {
     // HaltonSampler::SampleDimension (Halton.cpp:83-92)
     if (dim == 0) return radical_inverse_2(index >> s.baseExp0);
     if (dim == 1) return radical_inverse_b(3u, 0x55555555u, div_prime(index, (uint32_t)s.baseScale1, 0xffffffffu / (uint32_t)s.baseScale1));
     if (dim >= 1000) return 0.f;
+    if constexpr (LDS) {
+        if (dim < s.ldsDims) {
+            uint4 t = s_halton_tab[dim];
+            return scrambled_radical_inverse(t.x, t.y, s_halton_perm + t.z, index);
+        }
+    }
     return scrambled_radical_inverse(s.primes[dim], s.recips[dim], s.perms + s.primeSums[dim], index);
 }
 // GlobalSampler::Get1D/Get2D (Sampler.cpp:131-143): with no requested sample arrays
 // arrayStartDim == arrayEndDim == 5, so only a Get2D that would straddle dimension 5 is moved.
-__device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) { return sample_dimension(s, st.index, st.dim++); }
+template <bool LDS = false>
+__device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) { return sample_dimension<LDS>(s, st.index, st.dim++); }
+template <bool LDS = false>
 __device__ __forceinline__ void get2d(const DeviceSampler& s, SState& st, float* a, float* b) {
     if (st.dim == 4) st.dim = 5;
-    *a = sample_dimension(s, st.index, st.dim);
-    *b = sample_dimension(s, st.index, st.dim + 1);
+    *a = sample_dimension<LDS>(s, st.index, st.dim);
+    *b = sample_dimension<LDS>(s, st.index, st.dim + 1);
     st.dim += 2;
 }
 
@@ -228,7 +254,7 @@ __device__ rgb whitted_li(const KParams& P, Ray ray, SState& st, Counters* c) {
         if (STATS) c->shading++;
         f3 n = isect.sn, wo = isect.wo;
         BSDF bsdf;
-        if (!make_bsdf(S, isect, false, &bsdf)) {
+        if (!make_bsdf(S, S.materials, isect, false, &bsdf)) {
             if (guard > 1024) { Llast = sp(0.f); break; }
             ray = spawn_ray(isect, ray.d);     // Li(isect.SpawnRay(ray.d), depth)
             continue;
@@ -284,7 +310,7 @@ __device__ rgb path_li(const KParams& P, Ray ray, SState& st, Counters* c) {
         if (!found || bounces >= P.maxDepth) break;
         if (STATS) c->shading++;
         BSDF bsdf;
-        if (!make_bsdf(S, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
+        if (!make_bsdf(S, S.materials, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
         if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0) {
             rgb Ld = beta * uniform_sample_one_light<STATS>(P, isect, &bsdf, 0.f, st, false, c);
             L = L + Ld;
@@ -366,7 +392,7 @@ __device__ rgb volpath_li(const KParams& P, Ray ray, SState& st, Counters* c) {
             if (!found || bounces >= P.maxDepth) break;
             if (STATS) c->shading++;
             BSDF bsdf;
-            if (!make_bsdf(S, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
+            if (!make_bsdf(S, S.materials, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
             L = L + beta * uniform_sample_one_light<STATS>(P, isect, &bsdf, 0.f, st, true, c);
             f3 wo = -ray.d, wi = mk(0, 0, 0);
             float pdf = 0;
@@ -554,7 +580,7 @@ struct pbr_hip_ctx {
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
     // wavefront queues and per-sample records (pbr_wavefront.h)
-    DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wCnt;
+    DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
 };
@@ -629,18 +655,19 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const int spp = P.spp;
     long long chunkPix = std::max(1LL, (1LL << 23) / spp);
     if (chunkPix > P.nPixels) chunkPix = P.nPixels;
-    const size_t cap = (size_t)chunkPix * spp;
+    const size_t cap = (size_t)chunkPix * spp, qcap = cap;
     for (int k = 0; k < 2; ++k) {
-        HIP_TRY(ctx->wqO[k].ensure(cap * 16)); HIP_TRY(ctx->wqD[k].ensure(cap * 16));
-        HIP_TRY(ctx->wqId[k].ensure(cap * 4)); HIP_TRY(ctx->wqHit[k].ensure(cap * 16));
+        HIP_TRY(ctx->wqO[k].ensure(qcap * 16)); HIP_TRY(ctx->wqD[k].ensure(qcap * 16));
+        HIP_TRY(ctx->wqId[k].ensure(qcap * 4)); HIP_TRY(ctx->wqHit[k].ensure(qcap * 16));
     }
-    HIP_TRY(ctx->wsO.ensure(cap * 16)); HIP_TRY(ctx->wsD.ensure(cap * 16));
-    HIP_TRY(ctx->wsC.ensure(cap * 16)); HIP_TRY(ctx->wsId.ensure(cap * 4));
+    HIP_TRY(ctx->wsO.ensure(qcap * 16)); HIP_TRY(ctx->wsD.ensure(qcap * 16));
+    HIP_TRY(ctx->wsC.ensure(qcap * 16)); HIP_TRY(ctx->wsId.ensure(qcap * 4));
     const int levels = P.maxDepth < 1 ? 1 : P.maxDepth;
     HIP_TRY(ctx->wRecA.ensure(cap * 16 * levels)); HIP_TRY(ctx->wRecF.ensure(cap * 16 * levels));
     HIP_TRY(ctx->wRecP.ensure(cap * 4 * levels)); HIP_TRY(ctx->wDepth.ensure(cap * 4));
+    HIP_TRY(ctx->wIndex.ensure(cap * 4));
     HIP_TRY(ctx->wCnt.ensure(16));
-    int* cnt = (int*)ctx->wCnt.p;
+    int* cnt = (int*)ctx->wCnt.p;   // queue 0, queue 1, shadow queue
     WfParams W;
     std::memset(&W, 0, sizeof(W));
     W.P = P;
@@ -648,13 +675,25 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     W.shadowCount = cnt + 2;
     W.recA = (float4*)ctx->wRecA.p; W.recF = (float4*)ctx->wRecF.p; W.recP = (float*)ctx->wRecP.p;
     W.depthOf = (int*)ctx->wDepth.p;
+    W.sampleIndex = (uint32_t*)ctx->wIndex.p;
+    // Halton dims one sample reaches: 5 camera + 4 per level (light 2D, SpecularReflect 2D)
+    W.P.smp.ldsDims = std::min(kLdsDims, 5 + 4 * levels + 2);
+    int lobes = 0;
+    for (const MatTemplate& m : ctx->host.materials)
+        for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
+    const bool simple = (lobes & ~kSimpleLobes) == 0;
+    // tuning switches (results are bit-identical either way): LDS short stack, shade occupancy
+    const char* eStack = getenv("PBR_SHORT_STACK");
+    const bool shortStack = !(eStack && eStack[0] == '0');
+    const char* eMats = getenv("PBR_MATS_LDS");
+    const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
     W.cap = (int)cap;
     auto queue = [&](int k) {
         WfQueue q;
         q.o = (float4*)ctx->wqO[k].p; q.d = (float4*)ctx->wqD[k].p; q.id = (int*)ctx->wqId[k].p; q.hit = (float4*)ctx->wqHit[k].p;
         return q;
     };
-    const dim3 blk(256), gstride(2048);
+    const dim3 blk(256), gstride(kWfBlocks);
     for (long long p0 = 0; p0 < P.nPixels; p0 += chunkPix) {
         W.chunkPix0 = p0;
         W.chunkPix = (int)std::min<long long>(chunkPix, P.nPixels - p0);
@@ -662,7 +701,8 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         int cur = 0;
         W.cur = queue(0);
         W.nextCount = cnt + 1;
-        hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
+        if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
+        else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
         // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
         const int maxLevels = levels + (ctx->host.anyNoMaterial ? 2 : 0);
         for (int level = 0; level < maxLevels; ++level) {
@@ -670,14 +710,20 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             W.next = queue(cur ^ 1);
             W.curCount = cnt + cur;
             W.nextCount = cnt + (cur ^ 1);
-            hipLaunchKernelGGL(k_wf_shade<0>, gstride, blk, 0, s, W, level == 0 ? 1 : 0);
-            hipLaunchKernelGGL(k_wf_shadow<0>, gstride, blk, 0, s, W);
+            const int l0 = level == 0 ? 1 : 0;
+            if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, s, W, l0);
+            else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, s, W, l0);
+            else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, s, W, l0);
+            else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, s, W, l0);
+            if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gstride, blk, 0, s, W);
+            else hipLaunchKernelGGL(k_wf_shadow<0>, gstride, blk, 0, s, W);
             if (level + 1 == maxLevels) break;
             cur ^= 1;
             W.cur = queue(cur);
             W.curCount = cnt + cur;
             W.nextCount = cnt + (cur ^ 1);   // reset by the extend kernel for the next shade
-            hipLaunchKernelGGL(k_wf_extend<0>, gstride, blk, 0, s, W);
+            if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gstride, blk, 0, s, W);
+            else hipLaunchKernelGGL(k_wf_extend<0>, gstride, blk, 0, s, W);
         }
         hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + 3) / 4), blk, 0, s, W);
     }

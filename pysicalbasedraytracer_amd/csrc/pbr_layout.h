@@ -89,6 +89,7 @@ struct DeviceSampler {
     int nSobolDims;
     int sobolLog2Res;              // log2 of the power-of-two resolution
     int sobolRes;
+    int ldsDims;                   // Halton dimensions a kernel may stage in LDS (<= 64)
 };
 
 struct DeviceCamera {

@@ -36,13 +36,18 @@ constexpr float gamma_n(int n) {
     return (float)((n * (1.1920928955078125e-07 * 0.5)) / (1 - n * (1.1920928955078125e-07 * 0.5)));
 }
 
-PBR_HD float t_sin(float x) { return (float)sin((double)x); }
-PBR_HD float t_cos(float x) { return (float)cos((double)x); }
-PBR_HD float t_exp(float x) { return (float)exp((double)x); }
-PBR_HD float t_log(float x) { return (float)log((double)x); }
-PBR_HD float t_pow(float x, float y) { return (float)pow((double)x, (double)y); }
-PBR_HD float t_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-PBR_HD float t_asin(float x) { return (float)asin((double)x); }
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PBR_TRANS __host__ __device__ __attribute__((noinline))
+#else
+#define PBR_TRANS PBR_HD
+#endif
+PBR_TRANS float t_sin(float x) { return (float)sin((double)x); }
+PBR_TRANS float t_cos(float x) { return (float)cos((double)x); }
+PBR_TRANS float t_exp(float x) { return (float)exp((double)x); }
+PBR_TRANS float t_log(float x) { return (float)log((double)x); }
+PBR_TRANS float t_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+PBR_TRANS float t_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+PBR_TRANS float t_asin(float x) { return (float)asin((double)x); }
 
 // std::min/std::max/Clamp with the reference's NaN behaviour
 PBR_HD float mn(float a, float b) { return (b < a) ? b : a; }

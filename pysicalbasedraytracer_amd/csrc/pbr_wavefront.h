@@ -11,11 +11,15 @@
 //   k_wf_extend          closest hit for the continuation queue
 //   k_wf_finish          fold L_k = A_k + ((F_k·L_{k+1})·c_k)/pdf_k deepest-first, per-pixel in-order sum, film
 //
-// Queues are SoA in HBM and compacted with one atomic per wave (ballot + popcount).  Records are
-// indexed by sample so the fold reproduces the recursive evaluation bit for bit.
+// Queues are SoA in HBM and compacted with one atomic per wave (ballot + popcount); the consumers
+// read them densely with grid-stride loops.  (Per-workgroup queue segments without global atomics
+// were measured 16% slower on C2: segment occupancy follows the image, so the traversal kernels
+// load-imbalance.)  Records are indexed by sample, so the fold reproduces the recursive
+// evaluation bit for bit whatever order the queues end up in.
 #pragma once
 
 constexpr int kWfMaxDepth = 8;
+constexpr int kWfBlocks = 2048;   // workgroups of the grid-stride queue kernels
 
 struct WfQueue {
     float4* o;      // origin.xyz, tMax
@@ -38,9 +42,11 @@ struct WfParams {
     float4* recF;          // F.rgb, cos term
     float* recP;           // pdf
     int* depthOf;          // deepest level of each sample
+    uint32_t* sampleIndex; // Halton global index of each sample (GlobalSampler::SetSampleNumber)
     int cap;               // record stride (>= nSamples)
 };
 
+// the wave's lanes must be converged
 __device__ __forceinline__ int wave_push(int* counter, bool pred) {
     unsigned long long m = __ballot(pred);
     int lane = (int)__lane_id();
@@ -52,7 +58,7 @@ __device__ __forceinline__ int wave_push(int* counter, bool pred) {
 }
 __device__ __forceinline__ int pack_dd(int dim, int depth) { return (dim & 0xffff) | (depth << 16); }
 
-template <int DUMMY>
+template <int SHORT>
 __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
     const KParams& P = W.P;
     int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -70,17 +76,18 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
     Ray r = camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
     HitRec h;
     Counters c;
-    bool hit = traverse<false, false>(P.S, r, &h, &c);
+    bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(st.dim, 0)));
     W.cur.id[q] = q;
     if (q == 0) { *W.nextCount = 0; *W.shadowCount = 0; }   // queue counters of the level-0 shade
+    W.sampleIndex[q] = st.index;
     W.depthOf[q] = 0;                          // a sample dropped by the level cap reads black
     W.recA[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
 }
 
-template <int DUMMY>
+template <int SHORT>
 __global__ __launch_bounds__(256) void k_wf_extend(WfParams W) {
     int n = *W.curCount;
     if (blockIdx.x == 0 && threadIdx.x == 0) { *W.nextCount = 0; *W.shadowCount = 0; }   // for the next shade
@@ -89,17 +96,35 @@ __global__ __launch_bounds__(256) void k_wf_extend(WfParams W) {
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
         Counters c;
-        bool hit = traverse<false, false>(W.P.S, r, &h, &c);
+        bool hit = traverse<false, false, SHORT>(W.P.S, r, &h, &c);
         W.cur.o[q].w = r.tMax;
         W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
     }
 }
 
-// One level of WhittedIntegrator::Li for every queued ray (single-light scenes).
-template <int DUMMY>
-__global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
+// One level of WhittedIntegrator::Li for every queued ray (single-light scenes).  LOBES: the lobe
+// kinds present in the scene (kSimpleLobes drops the microfacet code and its registers).
+constexpr int kSimpleLobes = (1 << L_LAMBERT) | (1 << L_OREN) | (1 << L_SPEC_R) | (1 << L_SPEC_T) | (1 << L_FRESNEL_SPEC);
+// MATS_LDS: the material templates fit kLdsMats and are read from an LDS copy (the BSDF code walks
+// them with dependent loads).
+constexpr int kLdsMats = 32;
+__shared__ MatTemplate s_mats[kLdsMats];
+
+template <int LOBES, bool MATS_LDS, int OCC = (LOBES & ~kSimpleLobes) ? 2 : 4>
+__global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     const KParams& P = W.P;
     const DeviceScene& S = P.S;
+    stage_halton_lds(P.smp);
+    const MatTemplate* mats = S.materials;
+    if constexpr (MATS_LDS) {
+        constexpr int words = (int)(sizeof(MatTemplate) / 4);
+        const int n = 2 * S.nMaterials * words;
+        const uint32_t* src = (const uint32_t*)S.materials;
+        uint32_t* dst = (uint32_t*)s_mats;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+        mats = s_mats;
+    }
+    __syncthreads();
     int n = level0 ? W.nSamples : *W.curCount;
     int stride = gridDim.x * blockDim.x;
     int nIter = (n + stride - 1) / stride;
@@ -133,7 +158,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
                 isect.slot = slot;
                 isect.medIn = isect.medOut = -1;
                 BSDF bsdf;
-                if (!make_bsdf(S, isect, false, &bsdf)) {
+                if (!make_bsdf(S, mats, isect, false, &bsdf)) {
                     cont = spawn_ray(isect, ray.d);        // Li(isect.SpawnRay(ray.d), depth)
                     pushNext = true;
                 } else {
@@ -141,16 +166,11 @@ __global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
                     rgb L = sp(0.f);
                     L = L + si_Le(S, isect, wo);
                     SState st;
-                    st.index = 0;
+                    st.index = W.sampleIndex[id];
                     st.dim = dim;
-                    // the sample index is recomputed from the sample id
-                    int lp = id / P.spp, s = id - lp * P.spp;
-                    int x, y;
-                    pixel_xy(P, W.chunkPix0 + lp, &x, &y);
-                    st.index = halton_pixel_offset(hparams(P.smp), x, y) + (uint32_t)s * (uint32_t)P.smp.stride;
                     {   // the single light (WhittedIntegrator.cpp:39-54)
                         float a, b;
-                        get2d(P.smp, st, &a, &b);
+                        get2d<true>(P.smp, st, &a, &b);
                         // Reordered but equivalent: f(wo, wi) does not depend on Li, and nothing is
                         // added when f is black — so the light's radiance (for the SkyBox: atan2,
                         // asin and an env gather) is only evaluated when f is not black, and a
@@ -165,7 +185,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
                                 wi = uniform_sphere(a, b);
                                 pdf = 1.f / (4 * kPi);
                                 vis.p = isect.p + wi * (2 * light.worldRadius); vis.pError = mk(0, 0, 0); vis.n = mk(0, 0, 0);
-                                rgb f = bsdf_f(bsdf, wo, wi, BSDF_ALL);
+                                rgb f = bsdf_f<LOBES>(bsdf, wo, wi, BSDF_ALL);
                                 if (!black(f)) {
                                     float ul, vl;
                                     sphere_uv(normalize(wi), &ul, &vl);
@@ -179,7 +199,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
                             } else {
                                 Li = sample_li(S, light, isect, a, b, &wi, &pdf, &vis);
                                 if (!(black(Li) || pdf == 0)) {
-                                    rgb f = bsdf_f(bsdf, wo, wi, BSDF_ALL);
+                                    rgb f = bsdf_f<LOBES>(bsdf, wo, wi, BSDF_ALL);
                                     if (!black(f)) {
                                         contrib = f * Li * absdot(wi, n) / pdf;
                                         shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
@@ -196,8 +216,9 @@ __global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
                         float pdf = 0;
                         int stype = 0;
                         float a, b;
-                        get2d(P.smp, st, &a, &b);
-                        rgb f = bsdf_sample(bsdf, wo, &wi, a, b, &pdf, BSDF_REFLECTION | BSDF_SPECULAR, &stype);
+                        get2d<true>(P.smp, st, &a, &b);
+                        // only L_SPEC_R lobes match BSDF_REFLECTION | BSDF_SPECULAR
+                        rgb f = bsdf_sample<(1 << L_SPEC_R)>(bsdf, wo, &wi, a, b, &pdf, BSDF_REFLECTION | BSDF_SPECULAR, &stype);
                         if (!black(f) && pdf > 0.f && absdot(wi, isect.sn) != 0.f && depth + 1 < kWfMaxDepth) {
                             W.recF[ri] = make_float4(f.r, f.g, f.b, absdot(wi, isect.sn));
                             W.recP[ri] = pdf;
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(WfParams W, int level0) {
 }
 
 // any-hit for the shadow queue; a visible light adds its contribution to the emitting level
-template <int DUMMY>
+template <int SHORT>
 __global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
     int n = *W.shadowCount;
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
@@ -240,7 +261,7 @@ __global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
         Counters c;
-        if (!traverse<true, false>(W.P.S, r, &h, &c)) {
+        if (!traverse<true, false, SHORT>(W.P.S, r, &h, &c)) {
             int id = W.sid[q];
             float4 cc = W.sc[q];
             size_t ri = (size_t)__float_as_int(d.w) * W.cap + id;
@@ -252,7 +273,8 @@ __global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
 }
 
 // Fold the recursion and run the film: one wave per pixel, lane = sample (coalesced record reads),
-// then lane 0 adds the 64 folded values in sample order (the reference's colObj += Li order).
+// then lanes 0-2 each add one channel of the 64 folded values in sample order (the reference's
+// colObj += Li order; Spectrum addition is per channel).
 template <int DUMMY>
 __global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
     __shared__ float lds[4][64 * 3];
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lp = blockIdx.x * 4 + wave;
     if (lp >= W.chunkPix) return;          // wave-uniform
-    rgb acc = sp(0.0f);
+    float accC = 0.0f;   // lane c < 3: channel c of the pixel sum
     for (int base = 0; base < P.spp; base += 64) {
         int s = base + lane;
         rgb L = sp(0.f);
@@ -280,12 +302,13 @@ __global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
         lds[wave][3 * lane] = L.r; lds[wave][3 * lane + 1] = L.g; lds[wave][3 * lane + 2] = L.b;
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (lane == 0) {
+        if (lane < 3) {
             int cnt = P.spp - base < 64 ? P.spp - base : 64;
-            for (int k = 0; k < cnt; ++k) acc = acc + sp3(lds[wave][3 * k], lds[wave][3 * k + 1], lds[wave][3 * k + 2]);
+            for (int k = 0; k < cnt; ++k) accC = accC + lds[wave][3 * k + lane];
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    if (lane == 0) film_out(P, W.chunkPix0 + lp, acc);
+    float r = __shfl(accC, 0), g = __shfl(accC, 1), b = __shfl(accC, 2);
+    if (lane == 0) film_out(P, W.chunkPix0 + lp, sp3(r, g, b));
 }

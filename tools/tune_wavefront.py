@@ -1,0 +1,66 @@
+"""A/B the wavefront tuning switches on one GPU (results must stay bit-identical across them).
+
+    python tools/tune_wavefront.py [--config C2] [--steps 3] VAR=VAL[,VAR=VAL] ...
+
+Each positional argument is one variant: a comma-separated list of environment settings read by
+libpbr_hip at render time (PBR_SHORT_STACK, PBR_SHADE_OCC, PBR_WAVEFRONT, PBR_OCC).
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from pysicalbasedraytracer_amd import HipRenderer, capi, scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="an experimental build of libpbr_hip.so")
+    ap.add_argument("variants", nargs="*", default=[""])
+    a = ap.parse_args()
+    if a.lib:
+        capi._lib = capi.load_library(a.lib)
+    scene, rd = scenes.CONFIGS[a.config]()
+    W, H, spp = rd.camera.width, rd.camera.height, rd.spp
+    r = HipRenderer(0)
+    r.upload(scene)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    rgb = torch.empty((W * H, 3), dtype=torch.float32, device=dev)
+    rgba = torch.empty((W * H, 4), dtype=torch.uint8, device=dev)
+    ref = None
+    for v in a.variants:
+        env = dict(kv.split("=") for kv in v.split(",") if kv)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        ms = []
+        for _ in range(a.steps):
+            t0 = time.perf_counter()
+            r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            ms.append((time.perf_counter() - t0) * 1e3)
+        out = rgb.cpu().numpy()
+        same = "ref" if ref is None else ("identical" if np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+                                          else "DIFFERENT max|d|=%g" % np.abs(out - ref).max())
+        if ref is None:
+            ref = out
+        m = float(np.median(ms))
+        print(f"{a.config} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  {W * H * spp / m / 1e3:8.1f} Msamples/s  {same}", flush=True)
+        for k, old in saved.items():
+            if old is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = old
+
+
+if __name__ == "__main__":
+    main()
