@@ -655,7 +655,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const int spp = P.spp;
     long long chunkPix = std::max(1LL, (1LL << 23) / spp);
     if (chunkPix > P.nPixels) chunkPix = P.nPixels;
-    const size_t cap = (size_t)chunkPix * spp, qcap = cap;
+    const size_t cap = (size_t)chunkPix * spp;
+    // segment capacity: a shade workgroup processes at most ceil(cap / (kWfBlocks·256)) rounds of 256
+    const int segCap = (int)((cap + (size_t)kWfBlocks * 256 - 1) / ((size_t)kWfBlocks * 256) * 256);
+    const size_t qcap = std::max(cap, (size_t)segCap * kWfBlocks);
     for (int k = 0; k < 2; ++k) {
         HIP_TRY(ctx->wqO[k].ensure(qcap * 16)); HIP_TRY(ctx->wqD[k].ensure(qcap * 16));
         HIP_TRY(ctx->wqId[k].ensure(qcap * 4)); HIP_TRY(ctx->wqHit[k].ensure(qcap * 16));
@@ -666,13 +669,14 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     HIP_TRY(ctx->wRecA.ensure(cap * 16 * levels)); HIP_TRY(ctx->wRecF.ensure(cap * 16 * levels));
     HIP_TRY(ctx->wRecP.ensure(cap * 4 * levels)); HIP_TRY(ctx->wDepth.ensure(cap * 4));
     HIP_TRY(ctx->wIndex.ensure(cap * 4));
-    HIP_TRY(ctx->wCnt.ensure(16));
-    int* cnt = (int*)ctx->wCnt.p;   // queue 0, queue 1, shadow queue
+    HIP_TRY(ctx->wCnt.ensure(3 * kWfBlocks * sizeof(int)));
+    int* cnt = (int*)ctx->wCnt.p;   // segment counts: queue 0, queue 1, shadow queue
     WfParams W;
     std::memset(&W, 0, sizeof(W));
     W.P = P;
     W.so = (float4*)ctx->wsO.p; W.sd = (float4*)ctx->wsD.p; W.sc = (float4*)ctx->wsC.p; W.sid = (int*)ctx->wsId.p;
-    W.shadowCount = cnt + 2;
+    W.shadowSeg = cnt + 2 * kWfBlocks;
+    W.segCap = segCap;
     W.recA = (float4*)ctx->wRecA.p; W.recF = (float4*)ctx->wRecF.p; W.recP = (float*)ctx->wRecP.p;
     W.depthOf = (int*)ctx->wDepth.p;
     W.sampleIndex = (uint32_t*)ctx->wIndex.p;
@@ -691,6 +695,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     auto queue = [&](int k) {
         WfQueue q;
         q.o = (float4*)ctx->wqO[k].p; q.d = (float4*)ctx->wqD[k].p; q.id = (int*)ctx->wqId[k].p; q.hit = (float4*)ctx->wqHit[k].p;
+        q.segCount = cnt + k * kWfBlocks;
         return q;
     };
     const dim3 blk(256), gstride(kWfBlocks);
@@ -700,7 +705,6 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
         W.cur = queue(0);
-        W.nextCount = cnt + 1;
         if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
         else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
         // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
@@ -708,8 +712,6 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         for (int level = 0; level < maxLevels; ++level) {
             W.cur = queue(cur);
             W.next = queue(cur ^ 1);
-            W.curCount = cnt + cur;
-            W.nextCount = cnt + (cur ^ 1);
             const int l0 = level == 0 ? 1 : 0;
             if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, s, W, l0);
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, s, W, l0);
@@ -720,8 +722,6 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             if (level + 1 == maxLevels) break;
             cur ^= 1;
             W.cur = queue(cur);
-            W.curCount = cnt + cur;
-            W.nextCount = cnt + (cur ^ 1);   // reset by the extend kernel for the next shade
             if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gstride, blk, 0, s, W);
             else hipLaunchKernelGGL(k_wf_extend<0>, gstride, blk, 0, s, W);
         }

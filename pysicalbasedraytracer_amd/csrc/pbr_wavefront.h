@@ -11,32 +11,35 @@
 //   k_wf_extend          closest hit for the continuation queue
 //   k_wf_finish          fold L_k = A_k + ((F_k·L_{k+1})·c_k)/pdf_k deepest-first, per-pixel in-order sum, film
 //
-// Queues are SoA in HBM and compacted with one atomic per wave (ballot + popcount); the consumers
-// read them densely with grid-stride loops.  (Per-workgroup queue segments without global atomics
-// were measured 16% slower on C2: segment occupancy follows the image, so the traversal kernels
-// load-imbalance.)  Records are indexed by sample, so the fold reproduces the recursive
-// evaluation bit for bit whatever order the queues end up in.
+// Queues are SoA in HBM.  The shade kernel runs kWfBlocks workgroups and workgroup b appends to
+// segment b ([b·segCap, b·segCap + count[b])) of the queues it writes, through an LDS counter
+// (ballot + popcount per wave) — no device-scope atomic: one counter hit by every wave of the grid
+// serialised the level-0 shade (1015 µs → 274 µs per 2^23-sample launch without it).  Consumers
+// read a segmented queue densely: each workgroup scans the kWfBlocks counts into LDS and maps its
+// grid-stride index to (segment, offset) by binary search, so the traversal kernels stay load
+// balanced (reading segment b in workgroup b was measured 16% slower overall).  Records are indexed
+// by sample, so the fold reproduces the recursive evaluation bit for bit in any queue order.
 #pragma once
 
 constexpr int kWfMaxDepth = 8;
-constexpr int kWfBlocks = 2048;   // workgroups of the grid-stride queue kernels
+constexpr int kWfBlocks = 2048;   // workgroups of the queue kernels = segments of a queue
 
 struct WfQueue {
     float4* o;      // origin.xyz, tMax
     float4* d;      // dir.xyz, packed (dim | depth << 16) as int bits
     int* id;        // sample index within the chunk
     float4* hit;    // slot (int bits, -1 = miss), b0, b1, b2
+    int* segCount;  // [kWfBlocks]; null for the dense level-0 queue
 };
 struct WfParams {
     KParams P;
     long long chunkPix0;   // first packed pixel of the chunk
     int chunkPix;          // pixels in the chunk
     int nSamples;          // chunkPix * spp
+    int segCap;            // capacity of one queue segment
     WfQueue cur, next;
-    int* curCount;
-    int* nextCount;
-    // shadow queue
-    float4* so; float4* sd; float4* sc; int* sid; int* shadowCount;
+    // shadow queue (segmented like the ray queues)
+    float4* so; float4* sd; float4* sc; int* sid; int* shadowSeg;
     // per-sample records, [depth * cap + sample]
     float4* recA;          // A.rgb, flags (bit0: add +0 at the end)
     float4* recF;          // F.rgb, cos term
@@ -46,7 +49,7 @@ struct WfParams {
     int cap;               // record stride (>= nSamples)
 };
 
-// the wave's lanes must be converged
+// LDS counter; the wave's lanes must be converged
 __device__ __forceinline__ int wave_push(int* counter, bool pred) {
     unsigned long long m = __ballot(pred);
     int lane = (int)__lane_id();
@@ -57,6 +60,39 @@ __device__ __forceinline__ int wave_push(int* counter, bool pred) {
     return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
 }
 __device__ __forceinline__ int pack_dd(int dim, int depth) { return (dim & 0xffff) | (depth << 16); }
+
+// Exclusive prefix of the kWfBlocks segment counts into s_off[0..kWfBlocks] (whole workgroup of
+// 256); returns the total.
+__shared__ int s_seg_off[kWfBlocks + 1];
+__device__ int seg_scan(const int* counts) {
+    constexpr int per = kWfBlocks / 256;
+    __shared__ int s_wave[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int local[per], sum = 0;
+    for (int i = 0; i < per; ++i) { local[i] = counts[t * per + i]; sum += local[i]; }
+    int incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wave[w] = incl;
+    __syncthreads();
+    int excl = incl - sum;
+    for (int k = 0; k < w; ++k) excl += s_wave[k];
+    for (int i = 0; i < per; ++i) { s_seg_off[t * per + i] = excl; excl += local[i]; }
+    if (t == 255) s_seg_off[kWfBlocks] = excl;
+    __syncthreads();
+    return s_seg_off[kWfBlocks];
+}
+// dense index q < total → queue position: the last segment whose offset is <= q holds it
+__device__ __forceinline__ int seg_pos(int segCap, int q) {
+    int lo = 0, hi = kWfBlocks;
+    while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (s_seg_off[mid] <= q) lo = mid; else hi = mid;
+    }
+    return lo * segCap + (q - s_seg_off[lo]);
+}
 
 template <int SHORT>
 __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
@@ -80,7 +116,6 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(st.dim, 0)));
     W.cur.id[q] = q;
-    if (q == 0) { *W.nextCount = 0; *W.shadowCount = 0; }   // queue counters of the level-0 shade
     W.sampleIndex[q] = st.index;
     W.depthOf[q] = 0;                          // a sample dropped by the level cap reads black
     W.recA[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -89,9 +124,9 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
 
 template <int SHORT>
 __global__ __launch_bounds__(256) void k_wf_extend(WfParams W) {
-    int n = *W.curCount;
-    if (blockIdx.x == 0 && threadIdx.x == 0) { *W.nextCount = 0; *W.shadowCount = 0; }   // for the next shade
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int n = seg_scan(W.cur.segCount);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int q = seg_pos(W.segCap, i);
         float4 o = W.cur.o[q], d = W.cur.d[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
@@ -124,13 +159,17 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
         for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
         mats = s_mats;
     }
+    __shared__ int s_push[2];   // shadow, next
+    if (threadIdx.x < 2) s_push[threadIdx.x] = 0;
     __syncthreads();
-    int n = level0 ? W.nSamples : *W.curCount;
-    int stride = gridDim.x * blockDim.x;
-    int nIter = (n + stride - 1) / stride;
+    const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
+    const int stride = gridDim.x * blockDim.x;
+    const int nIter = (n + stride - 1) / stride;   // <= segCap / 256: a segment holds all pushes
+    const int base = blockIdx.x * W.segCap;
     for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
-        int q = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
-        bool active = q < n;
+        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const bool active = i < n;
+        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
         bool pushShadow = false, pushNext = false;
         int id = 0, depth = 0, dim = 0, emitDepth = 0;
         Ray ray, shadow, cont;
@@ -236,27 +275,30 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                 }
             }
         }
-        int si = wave_push(W.shadowCount, pushShadow);
+        int si = base + wave_push(&s_push[0], pushShadow);
         if (pushShadow) {   // the visibility result lands in the level that emitted the ray
             W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
             W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(emitDepth));
             W.sc[si] = make_float4(contrib.r, contrib.g, contrib.b, 0.f);
             W.sid[si] = id;
         }
-        int ni = wave_push(W.nextCount, pushNext);
+        int ni = base + wave_push(&s_push[1], pushNext);
         if (pushNext) {
             W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
             W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_dd(dim, depth)));
             W.next.id[ni] = id;
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) { W.shadowSeg[blockIdx.x] = s_push[0]; W.next.segCount[blockIdx.x] = s_push[1]; }
 }
 
 // any-hit for the shadow queue; a visible light adds its contribution to the emitting level
 template <int SHORT>
 __global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
-    int n = *W.shadowCount;
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int n = seg_scan(W.shadowSeg);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int q = seg_pos(W.segCap, i);
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;

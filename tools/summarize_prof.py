@@ -1,0 +1,56 @@
+"""Summarise rocprofv3 output (kernel stats + the PMC passes of tools/pmc.sh) into a markdown table.
+
+    python tools/summarize_prof.py gpurun_out/prof gpurun_out/pmc > profiles/rNN_summary.md
+
+FETCH_SIZE is doubled (gfx950 reports half the bytes of a 16-B/lane streaming read,
+MI355X_MICROARCH.md § HBM); WRITE_SIZE is taken as is.  Both are per frame (the PMC runs render
+one warm-up frame and one timed frame, so the per-kernel totals are halved).
+"""
+import collections
+import csv
+import os
+import re
+import sys
+
+
+def short(name):
+    name = re.sub(r"\(anonymous namespace\)::", "", name)
+    name = re.sub(r"^void ", "", name)
+    return re.sub(r"\(.*$", "", name)
+
+
+def main():
+    prof, pmc = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None
+    rows = list(csv.DictReader(open(os.path.join(prof, "run_kernel_stats.csv"))))
+    print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
+    print("| kernel | calls | total ms | avg µs | % |")
+    print("|---|---:|---:|---:|---:|")
+    for r in rows:
+        print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
+              f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
+    if not pmc:
+        return
+    frames = 2.0
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    for sub in ("sq", "fetch", "write"):
+        p = os.path.join(pmc, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            agg[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    print("\n## PMC per frame (separate passes; FETCH_SIZE ×2 gfx950 correction)\n")
+    print("| kernel | HBM read GB | HBM write GB | VALU insts/wave | wave-cycles parked (SQ_WAIT_ANY) | issue-stalled | active |")
+    print("|---|---:|---:|---:|---:|---:|---:|")
+    for k, d in agg.items():
+        if "k_" not in k:
+            continue
+        wc = d.get("SQ_WAVE_CYCLES", 0) or 1
+        waves = d.get("SQ_WAVES", 0) or 1
+        print(f"| `{k}` | {2 * d.get('FETCH_SIZE', 0) * 1024 / 1e9 / frames:.2f} | "
+              f"{d.get('WRITE_SIZE', 0) * 1024 / 1e9 / frames:.2f} | {d.get('SQ_INSTS_VALU', 0) / waves:.0f} | "
+              f"{d.get('SQ_WAIT_ANY', 0) / wc:.2f} | {d.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | "
+              f"{d.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f} |")
+
+
+if __name__ == "__main__":
+    main()
