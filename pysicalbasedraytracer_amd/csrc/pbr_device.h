@@ -187,12 +187,42 @@ __device__ __forceinline__ bool prim_hit(const DeviceScene& S, int slot, const R
 
 // BVHAccel::Intersect / IntersectP (BVHAccel.cpp:285-366): the same near-first order (dirIsNeg of
 // the node's split axis) so ties between primitives resolve exactly as on the CPU (F8).
+// The slab part of node_hit: everything but the final (tMin < ray.tMax), which is the only term
+// that depends on ray.tMax.  Returns false where node_hit would whatever ray.tMax is.
+__device__ __forceinline__ bool node_slab(f3 lo, f3 hi, const Ray& r, f3 inv, bool n0, bool n1, bool n2, float* tEnter) {
+    float tMin = ((n0 ? hi.x : lo.x) - r.o.x) * inv.x;
+    float tMax = ((n0 ? lo.x : hi.x) - r.o.x) * inv.x;
+    float tyMin = ((n1 ? hi.y : lo.y) - r.o.y) * inv.y;
+    float tyMax = ((n1 ? lo.y : hi.y) - r.o.y) * inv.y;
+    if (tMin > tyMax || tyMin > tMax) return false;
+    if (tyMin > tMin) tMin = tyMin;
+    if (tyMax < tMax) tMax = tyMax;
+    float tzMin = ((n2 ? hi.z : lo.z) - r.o.z) * inv.z;
+    float tzMax = ((n2 ? lo.z : hi.z) - r.o.z) * inv.z;
+    if (tMin > tzMax || tzMin > tMax) return false;
+    if (tzMin > tMin) tMin = tzMin;
+    if (tzMax < tMax) tMax = tzMax;
+    *tEnter = tMin;
+    return tMax > 0;
+}
+
 // Short traversal stack in LDS for the 256-lane wavefront kernels: entries [0, SHORT) live in LDS
 // ([entry][lane], conflict-free), deeper ones in the private (scratch) array.  Only where entries
 // are kept changes; the visit order does not.
-constexpr int kShortStack = 16;
-__shared__ int s_trav_stack[kShortStack * 256];
+constexpr int kShortStack = 8;
+__shared__ int s_trav_ref[kShortStack * 256];
+__shared__ float s_trav_t[kShortStack * 256];
 
+// BVHAccel::Intersect / IntersectP (BVHAccel.cpp:285-366) over the wide layout of
+// build_wide_nodes.  The reference pops a node and tests its box against the current ray.tMax;
+// since only the last comparison of that test reads ray.tMax (Geometry.h:1438-1468), the slab part
+// is evaluated once, from the parent, for both children, and the stack keeps (child, tEnter):
+//   * near child (dirIsNeg[axis] order) visited next iff slab && tEnter < tMax — what the
+//     reference's immediate visit of it computes, tMax being unchanged in between;
+//   * far child: the reference pushes it before descending; here it is pushed only if its slab
+//     passes (a failing one is a no-op pop there), and tested against the then-current tMax when
+//     popped; if the near child failed, the reference's next pop is this far child, tested now.
+// Primitive tests therefore run in exactly the reference's order, so ties resolve the same (F8).
 template <bool ANY, bool STATS, int SHORT = 0>
 __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
     static_assert(SHORT == 0 || SHORT == kShortStack, "short stack is kShortStack deep");
@@ -200,44 +230,73 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
     if (S.nNodes == 0) return false;
     f3 inv = ANY ? mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z) : mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
     bool n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
-    int stack[64 - SHORT];
-    int* lstack = nullptr;
-    if constexpr (SHORT > 0) lstack = s_trav_stack + threadIdx.x;
-    auto push = [&](int sp_, int v) { if (SHORT && sp_ < SHORT) lstack[sp_ * 256] = v; else stack[sp_ - SHORT] = v; };
-    auto pop = [&](int sp_) { return (SHORT && sp_ < SHORT) ? lstack[sp_ * 256] : stack[sp_ - SHORT]; };
-    int sp = 0, cur = 0;
+    {   // the root is visited first
+        float4 a = S.nodes[0], b = S.nodes[1];
+        if (STATS) c->nodes++;
+        if (!node_hit(a, b, r, inv, n0, n1, n2)) return false;
+    }
+    int stackRef[64 - SHORT];
+    float stackT[64 - SHORT];
+    int* lref = nullptr;
+    float* lt = nullptr;
+    if constexpr (SHORT > 0) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
+    int cur = S.rootRef, sp = 0;
     bool found = false;
     while (true) {
-        float4 a = S.nodes[2 * cur], b = S.nodes[2 * cur + 1];
-        if (STATS) c->nodes++;
-        if (node_hit(a, b, r, inv, n0, n1, n2)) {
-            int off = __float_as_int(b.z);
-            uint32_t meta = __float_as_uint(b.w);
-            int nprim = (int)(meta & 0xffffu);
-            if (nprim > 0) {
-                for (int i = 0; i < nprim; ++i) {
-                    float t, b0, b1, b2;
-                    if (STATS) c->prims++;
-                    if (prim_hit(S, off + i, r, &t, &b0, &b1, &b2)) {
-                        if (ANY) return true;
-                        r.tMax = t;   // GeometricPrimitive::Intersect (Primitive.cpp:26)
-                        h->slot = off + i; h->b0 = b0; h->b1 = b1; h->b2 = b2;
-                        found = true;
-                    }
+        if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
+            int slot = cur & 0x7fffffff;
+            while (true) {
+                const float4* tv = S.triVerts + 3 * (size_t)slot;
+                float4 v0 = tv[0], v1 = tv[1], v2 = tv[2];
+                int flags = __float_as_int(v0.w);
+                float t, b0 = 0, b1 = 0, b2 = 0;
+                if (STATS) c->prims++;
+                bool hit = (flags & PRIM_SPHERE)
+                               ? sphere_test(S.spheres[__float_as_int(v0.x)], r, &t)
+                               : tri_test(mk(v0.x, v0.y, v0.z), mk(v1.x, v1.y, v1.z), mk(v2.x, v2.y, v2.z), r, &t, &b0, &b1, &b2);
+                if (hit) {
+                    if (ANY) return true;
+                    r.tMax = t;   // GeometricPrimitive::Intersect (Primitive.cpp:26)
+                    h->slot = slot; h->b0 = b0; h->b1 = b1; h->b2 = b2;
+                    found = true;
                 }
-                if (sp == 0) break;
-                cur = pop(--sp);
-            } else {
-                int axis = (int)((meta >> 16) & 0xffu);
-                bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
-                if (sp >= 64) break;   // BVHAccel's 64-entry stack; the SAH builds here stay < 30 deep
-                if (neg) { push(sp++, cur + 1); cur = off; }
-                else { push(sp++, off); cur = cur + 1; }
+                if (flags & PRIM_LEAF_END) break;
+                ++slot;
             }
         } else {
-            if (sp == 0) break;
-            cur = pop(--sp);
+            const float4* w = S.wide + 4 * (size_t)cur;
+            float4 A = w[0], B = w[1], C = w[2], D = w[3];
+            if (STATS) c->nodes += 2;
+            float t0 = 0, t1 = 0;
+            bool ok0 = node_slab(mk(A.x, A.y, A.z), mk(A.w, B.x, B.y), r, inv, n0, n1, n2, &t0);
+            bool ok1 = node_slab(mk(B.z, B.w, C.x), mk(C.y, C.z, C.w), r, inv, n0, n1, n2, &t1);
+            int axis = __float_as_int(D.z);
+            bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+            int nearRef = __float_as_int(neg ? D.y : D.x), farRef = __float_as_int(neg ? D.x : D.y);
+            bool okN = neg ? ok1 : ok0, okF = neg ? ok0 : ok1;
+            float tN = neg ? t1 : t0, tF = neg ? t0 : t1;
+            if (okN && tN < r.tMax) {
+                if (okF) {
+                    if (sp >= 64) break;   // BVHAccel's 64-entry stack; the SAH builds here stay < 30 deep
+                    if (SHORT && sp < SHORT) { lref[sp * 256] = farRef; lt[sp * 256] = tF; }
+                    else { stackRef[sp - SHORT] = farRef; stackT[sp - SHORT] = tF; }
+                    ++sp;
+                }
+                cur = nearRef;
+                continue;
+            }
+            if (okF && tF < r.tMax) { cur = farRef; continue; }
         }
+        bool more = false;   // pop until an entry passes its box test against the current tMax
+        while (sp > 0) {
+            --sp;
+            int rr;
+            float tt;
+            if (SHORT && sp < SHORT) { rr = lref[sp * 256]; tt = lt[sp * 256]; }
+            else { rr = stackRef[sp - SHORT]; tt = stackT[sp - SHORT]; }
+            if (tt < r.tMax) { cur = rr; more = true; break; }
+        }
+        if (!more) break;
     }
     return found;
 }

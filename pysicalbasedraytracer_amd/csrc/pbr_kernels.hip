@@ -576,7 +576,7 @@ struct pbr_hip_ctx {
     bool haveScene = false;
     HostScene host;
     HaltonTables halton;
-    DevBuf dNodes, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
+    DevBuf dNodes, dWide, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
     // wavefront queues and per-sample records (pbr_wavefront.h)
@@ -602,6 +602,8 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     DeviceScene S;
     std::memset(&S, 0, sizeof(S));
     S.nodes = (const float4*)ctx->dNodes.p;
+    S.wide = (const float4*)ctx->dWide.p;
+    S.rootRef = h.rootRef;
     S.triVerts = (const float4*)ctx->dTri.p;
     S.primInfo = (const int4*)ctx->dInfo.p;
     S.triUV = h.triUV.empty() ? nullptr : (const float2*)ctx->dUV.p;
@@ -788,6 +790,7 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     }
     const HostScene& h = ctx->host;
     HIP_TRY(ctx->dNodes.upload(h.nodes, ctx->stream));
+    HIP_TRY(ctx->dWide.upload(h.wide, ctx->stream));
     HIP_TRY(ctx->dTri.upload(h.triVerts, ctx->stream));
     HIP_TRY(ctx->dInfo.upload(h.primInfo, ctx->stream));
     HIP_TRY(ctx->dUV.upload(h.triUV, ctx->stream));

@@ -17,7 +17,8 @@
 
 namespace pbr {
 
-enum PrimFlags { PRIM_SPHERE = 1, PRIM_FLIP = 2, PRIM_HAS_UV = 4 };
+enum PrimFlags { PRIM_SPHERE = 1, PRIM_FLIP = 2, PRIM_HAS_UV = 4, PRIM_LEAF_END = 8 };
+constexpr uint32_t kLeafRef = 0x80000000u;   // traversal child reference: leaf | first slot
 enum LobeKind { L_LAMBERT = 0, L_OREN = 1, L_SPEC_R = 2, L_SPEC_T = 3, L_FRESNEL_SPEC = 4, L_MF_R = 5, L_MF_T = 6 };
 enum FresnelKind { FR_NOOP = 0, FR_DIEL = 1, FR_COND = 2 };
 enum BxDFType { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
@@ -57,6 +58,8 @@ struct SphereRec { float o2w[16]; float w2o[16]; float radius; int flip; int pad
 
 struct DeviceScene {
     const float4* nodes;
+    const float4* wide;            // 4 float4 per interior node: child boxes, child refs, axis
+    int rootRef;
     const float4* triVerts;
     const int4* primInfo;
     const float2* triUV;

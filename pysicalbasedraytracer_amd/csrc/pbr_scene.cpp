@@ -140,6 +140,50 @@ struct PrimRef { int shape, tri; };
 
 void fail(const std::string& why) { throw std::invalid_argument(why); }
 
+// The same tree re-laid out for traversal: each interior node carries both children's boxes (so a
+// child is box-tested from its parent, before its own record is fetched) and child references
+// (interior rank, or kLeafRef | first primitive slot).  The last primitive of every leaf gets
+// PRIM_LEAF_END in its v0.w flags.  Visit order is unchanged (pbr_device.h traverse).
+void build_wide_nodes(HostScene* S) {
+    const std::vector<LinearBVHNode>& L = S->nodes;
+    S->wide.clear();
+    S->rootRef = 0;
+    if (L.empty()) return;
+    std::vector<int> rank(L.size(), -1);
+    int nInterior = 0;
+    for (size_t i = 0; i < L.size(); ++i)
+        if (L[i].nPrimitives == 0) rank[i] = nInterior++;
+    auto ref = [&](int i) -> int32_t {
+        if (L[i].nPrimitives > 0) return (int32_t)(kLeafRef | (uint32_t)L[i].offset);
+        return rank[i];
+    };
+    for (size_t i = 0; i < L.size(); ++i) {
+        if (L[i].nPrimitives == 0) continue;
+        // every leaf ends at its last slot; slots are contiguous per leaf
+        int last = L[i].offset + L[i].nPrimitives - 1;
+        uint32_t f;
+        std::memcpy(&f, &S->triVerts[(size_t)last * 12 + 3], 4);
+        f |= PRIM_LEAF_END;
+        std::memcpy(&S->triVerts[(size_t)last * 12 + 3], &f, 4);
+    }
+    if ((uint32_t)S->primIds.size() >= kLeafRef) fail("too many primitives for the traversal layout");
+    S->wide.assign((size_t)nInterior * 16, 0.f);
+    for (size_t i = 0; i < L.size(); ++i) {
+        if (L[i].nPrimitives > 0) continue;
+        const LinearBVHNode& c0 = L[i + 1];
+        const LinearBVHNode& c1 = L[L[i].offset];
+        float* w = &S->wide[(size_t)rank[i] * 16];
+        w[0] = c0.pMin[0]; w[1] = c0.pMin[1]; w[2] = c0.pMin[2]; w[3] = c0.pMax[0];
+        w[4] = c0.pMax[1]; w[5] = c0.pMax[2]; w[6] = c1.pMin[0]; w[7] = c1.pMin[1];
+        w[8] = c1.pMin[2]; w[9] = c1.pMax[0]; w[10] = c1.pMax[1]; w[11] = c1.pMax[2];
+        int32_t r0 = ref((int)i + 1), r1 = ref(L[i].offset), ax = L[i].axis;
+        std::memcpy(&w[12], &r0, 4);
+        std::memcpy(&w[13], &r1, 4);
+        std::memcpy(&w[14], &ax, 4);
+    }
+    S->rootRef = ref(0);
+}
+
 // Bucketed SAH builder writing LinearBVHNodes in depth-first preorder.
 class SahBuilder {
   public:
@@ -499,6 +543,7 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
         if (sd.medium_inside >= d->n_media || sd.medium_outside >= d->n_media) fail("medium index out of range");
         pi[3] = (int32_t)(((uint32_t)(sd.medium_inside & 0xffff)) | ((uint32_t)(sd.medium_outside & 0xffff) << 16));
     }
+    build_wide_nodes(S);
     for (int slot = 0; slot < np; ++slot) {
         int m = S->primInfo[(size_t)slot * 4 + 1];
         if (m < 0 || d->materials[m].type == PBR_MAT_NONE) S->anyNoMaterial = true;

@@ -36,6 +36,8 @@ struct HostScene {
     std::vector<float> lightPower;          // Power().y() per light (LightDistrib.cpp:36-41)
     std::vector<float> media;               // 10 floats per medium
     bool anyNoMaterial = false;             // some primitive has material == nullptr
+    std::vector<float> wide;                // 16 floats per interior node (build_wide_nodes)
+    int32_t rootRef = 0;
 };
 
 // Throws std::invalid_argument on a malformed descriptor.
