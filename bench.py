@@ -22,9 +22,23 @@ sys.path.insert(0, ROOT)
 from pysicalbasedraytracer_amd import HipRenderer, scenes, tiles_for_rank  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# Algorithmic bytes model: 32 B per LinearBVHNode visit, 48 B per primitive test,
-# 96 B of ray-queue traffic per traced ray, 64 B per shading event.
+# Algorithmic bytes model: 32 B per LinearBVHNode test, 48 B per primitive test,
+# 96 B of ray-queue traffic per traced ray, 64 B per shading event.  The counts come from an
+# instrumented pass that counts tests exactly as BVHAccel performs them (pbr_device.h traverse).
 B_NODE, B_PRIM, B_RAY, B_SHADE = 32, 48, 96, 64
+# rocprofv3 PMC HBM bytes per frame (tools/pmc.sh + tools/summarize_prof.py --json=...); used only
+# when it was measured on the very build that is loaded (source hash from pbr_hip_build_info).
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "c2_traffic.json")
+
+
+def pmc_traffic(build_info):
+    try:
+        t = json.load(open(TRAFFIC_JSON))
+    except (OSError, ValueError):
+        return None, "no PMC summary"
+    if not t.get("build") or not build_info.endswith(t["build"]):
+        return None, f"PMC summary is for build {t.get('build')}, not this one"
+    return t["frame_read_bytes"] + t["frame_write_bytes"], f"{os.path.relpath(TRAFFIC_JSON, ROOT)} ({t['method']})"
 
 
 def cpu_baseline(scene, rd, budget_s=12.0):
@@ -76,6 +90,7 @@ def main():
     npx = sum((t[2] - t[0]) * (t[3] - t[1]) for t in tiles)
 
     r = HipRenderer(local)
+    build_info = r.lib.pbr_hip_build_info().decode()
     t0 = time.time()
     r.upload(scene)
     upload_s = time.time() - t0
@@ -138,6 +153,7 @@ def main():
     if rank == 0:
         k_ms = float(np.mean(kernel_ms))
         achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(build_info) if (world == 1 and args.config == "C2") else (None, "C2, 1 GPU only")
         out = {
             "metric": "Msamples/sec (whole node) + wall-clock to 1080p/64spp frame; %HBM roofline",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -149,10 +165,15 @@ def main():
                        "parallelism": f"tiles64x64 round-robin over {world} GPU(s), RCCL gather",
                        "frame_ms": round(ms_per_step, 3), "scene_upload_s": round(upload_s, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_render<Whitted>", "kernel_ms": round(k_ms, 3),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": ("wavefront frame: k_wf_camera_extend, (k_wf_shade, k_wf_shadow, k_wf_extend) per level, "
+                                    "k_wf_finish, per 2^23-sample chunk" if rd.integrator == 0 else "k_render megakernel"),
+                         "kernel_ms": round(k_ms, 3),
                          "bytes_per_sample": round(alg_bytes / samples_rank, 1),
-                         "model": "32*node_visits + 48*prim_tests + 96*rays + 64*shading_events per launch"},
+                         "model": "per sample: 32*node_tests + 48*prim_tests + 96*rays + 64*shading_events "
+                                  "(SURVEY 8(d)); counts from an instrumented pass over this frame",
+                         "build": build_info},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, rd)

@@ -223,6 +223,8 @@ __shared__ float s_trav_t[kShortStack * 256];
 //     passes (a failing one is a no-op pop there), and tested against the then-current tMax when
 //     popped; if the near child failed, the reference's next pop is this far child, tested now.
 // Primitive tests therefore run in exactly the reference's order, so ties resolve the same (F8).
+// STATS counts node tests as the reference performs them (root, every visited child, every pop):
+// there a far child whose slab fails is still pushed (with a NaN key, so its pop test fails).
 template <bool ANY, bool STATS, int SHORT = 0>
 __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
     static_assert(SHORT == 0 || SHORT == kShortStack, "short stack is kShortStack deep");
@@ -266,7 +268,6 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
         } else {
             const float4* w = S.wide + 4 * (size_t)cur;
             float4 A = w[0], B = w[1], C = w[2], D = w[3];
-            if (STATS) c->nodes += 2;
             float t0 = 0, t1 = 0;
             bool ok0 = node_slab(mk(A.x, A.y, A.z), mk(A.w, B.x, B.y), r, inv, n0, n1, n2, &t0);
             bool ok1 = node_slab(mk(B.z, B.w, C.x), mk(C.y, C.z, C.w), r, inv, n0, n1, n2, &t1);
@@ -275,8 +276,10 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
             int nearRef = __float_as_int(neg ? D.y : D.x), farRef = __float_as_int(neg ? D.x : D.y);
             bool okN = neg ? ok1 : ok0, okF = neg ? ok0 : ok1;
             float tN = neg ? t1 : t0, tF = neg ? t0 : t1;
+            if (STATS) c->nodes++;   // the near child's visit
             if (okN && tN < r.tMax) {
-                if (okF) {
+                if (STATS && !okF) tF = __int_as_float(0x7fc00000);
+                if (okF || STATS) {
                     if (sp >= 64) break;   // BVHAccel's 64-entry stack; the SAH builds here stay < 30 deep
                     if (SHORT && sp < SHORT) { lref[sp * 256] = farRef; lt[sp * 256] = tF; }
                     else { stackRef[sp - SHORT] = farRef; stackT[sp - SHORT] = tF; }
@@ -285,6 +288,7 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
                 cur = nearRef;
                 continue;
             }
+            if (STATS) c->nodes++;   // the far child, popped straight back
             if (okF && tF < r.tMax) { cur = farRef; continue; }
         }
         bool more = false;   // pop until an entry passes its box test against the current tMax
@@ -294,6 +298,7 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
             float tt;
             if (SHORT && sp < SHORT) { rr = lref[sp * 256]; tt = lt[sp * 256]; }
             else { rr = stackRef[sp - SHORT]; tt = stackT[sp - SHORT]; }
+            if (STATS) c->nodes++;
             if (tt < r.tMax) { cur = rr; more = true; break; }
         }
         if (!more) break;

@@ -738,7 +738,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
 extern "C" {
 
 int pbr_hip_abi_version(void) { return PBR_HIP_ABI_VERSION; }
-const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 megakernel r1"; }
+#ifndef PBR_SRC_HASH
+#define PBR_SRC_HASH "unknown"
+#endif
+const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 wavefront+megakernel src " PBR_SRC_HASH; }
 
 int pbr_hip_create(int device, pbr_hip_ctx** out) {
     if (!out) return PBR_E_INVALID;

@@ -20,7 +20,9 @@ def short(name):
 
 
 def main():
-    prof, pmc = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None
+    args = [a for a in sys.argv[1:] if not a.startswith("--json=")]
+    js = [a[7:] for a in sys.argv[1:] if a.startswith("--json=")]
+    prof, pmc = args[0], args[1] if len(args) > 1 else None
     rows = list(csv.DictReader(open(os.path.join(prof, "run_kernel_stats.csv"))))
     print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
     print("| kernel | calls | total ms | avg µs | % |")
@@ -38,6 +40,24 @@ def main():
             continue
         for r in csv.DictReader(open(p)):
             agg[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    build = None
+    for sub in ("sq", "fetch", "write"):
+        p = os.path.join(pmc, sub + ".log")
+        if os.path.exists(p):
+            for line in open(p):
+                if line.startswith("build:"):
+                    build = line.split("src")[-1].strip()
+    rd = sum(2 * d.get("FETCH_SIZE", 0) * 1024 / frames for k, d in agg.items() if "k_" in k)
+    wr = sum(d.get("WRITE_SIZE", 0) * 1024 / frames for k, d in agg.items() if "k_" in k)
+    print(f"\nBuild `{build}`: HBM traffic per frame = {rd / 1e9:.2f} GB read + {wr / 1e9:.2f} GB written "
+          f"= {(rd + wr) / 1e9:.2f} GB\n")
+    if js:
+        import json
+        per = {k: {"read_bytes": 2 * d.get("FETCH_SIZE", 0) * 1024 / frames, "write_bytes": d.get("WRITE_SIZE", 0) * 1024 / frames}
+               for k, d in agg.items() if "k_" in k}
+        json.dump({"build": build, "frame_read_bytes": rd, "frame_write_bytes": wr, "per_kernel": per,
+                   "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in separate passes, "
+                             "2 frames, halved"}, open(js[0], "w"), indent=1)
     print("\n## PMC per frame (separate passes; FETCH_SIZE ×2 gfx950 correction)\n")
     print("| kernel | HBM read GB | HBM write GB | VALU insts/wave | wave-cycles parked (SQ_WAIT_ANY) | issue-stalled | active |")
     print("|---|---:|---:|---:|---:|---:|---:|")

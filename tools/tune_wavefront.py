@@ -27,6 +27,7 @@ def main():
     a = ap.parse_args()
     if a.lib:
         capi._lib = capi.load_library(a.lib)
+    print("build:", capi.load_library().pbr_hip_build_info().decode(), flush=True)
     scene, rd = scenes.CONFIGS[a.config]()
     W, H, spp = rd.camera.width, rd.camera.height, rd.spp
     r = HipRenderer(0)
