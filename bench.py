@@ -19,7 +19,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from pysicalbasedraytracer_amd import HipRenderer, scenes, tiles_for_rank  # noqa: E402
+from pysicalbasedraytracer_amd import FrameGather, HipRenderer, scenes, tiles_for_rank  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Algorithmic bytes model: 32 B per LinearBVHNode test, 48 B per primitive test,
@@ -98,20 +98,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
     rgb = torch.empty((npx, 3), dtype=torch.float32, device=dev)
     rgba = torch.empty((npx, 4), dtype=torch.uint8, device=dev)
-    # gather buffers: every rank pads its packed span to the largest one
-    max_px = npx
-    if world > 1:
-        t = torch.tensor([npx], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        max_px = int(t.item())
-    send = torch.zeros((max_px, 3), dtype=torch.float32, device=dev)
-    gather = [torch.empty_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # multi-GPU: rank 0 gathers the packed tile spans over RCCL and scatters them into the frame
+    exchange = FrameGather(W, H, world, dev) if world > 1 else None
 
     def step():
         r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
-        if world > 1:
-            send[:npx].copy_(rgb)
-            dist.gather(send, gather_list=gather, dst=0)
+        if exchange is not None:
+            exchange(rgb, rank)
 
     # roofline counters: one instrumented, untimed pass on the same workload
     st = r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, stats=True)
@@ -132,9 +125,8 @@ def main():
         ev0.record(stream)
         r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
         ev1.record(stream)
-        if world > 1:
-            send[:npx].copy_(rgb)
-            dist.gather(send, gather_list=gather, dst=0)
+        if exchange is not None:
+            exchange(rgb, rank)
         torch.cuda.synchronize(dev)
         kernel_ms.append(ev0.elapsed_time(ev1))
     if world > 1:
@@ -145,7 +137,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        ab = torch.tensor([float(alg_bytes), float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+        # roofline over the whole job: every rank's algorithmic bytes over the slowest rank's frame
+        ab = torch.tensor([float(alg_bytes)], dtype=torch.float64, device=dev)
+        dist.all_reduce(ab, op=dist.ReduceOp.SUM)
+        km = torch.tensor([float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        alg_bytes, kernel_ms, samples_rank = float(ab.item()), [float(km.item())], W * H * spp
     ms_per_step = elapsed / args.steps * 1e3
     total_samples = W * H * spp
     value = total_samples / (elapsed / args.steps) / 1e6

@@ -1,0 +1,483 @@
+// pbr/pbr.h — C++ host API of the MI355X render path, mirroring the reference's classes.
+//
+// A program written against G0T-cha/PysicalBasedRaytracer's scene API (Main/main.cpp builds a
+// scene from these classes and calls Integrator::Render) compiles against this header with the
+// same class names, constructor arguments and call sequence; Render then runs on the GPU through
+// the C-ABI of include/pbr_hip.h.  Only what the render path consumes is kept: shapes, materials
+// with constant textures, lights, media, the BVH aggregate, the perspective camera, the Halton
+// sampler, the frame buffer and the three sampler integrators.
+//
+// Differences from the reference, all deliberate:
+//  * no CPU ray tracing: Primitive/Scene/BVHAccel hold the scene for flattening; intersection
+//    queries run on the device (pbr_hip_intersect) — BVHAccel is built on upload, node for node
+//    identical to the reference's (Accelerator/BVHAccel.cpp:57-283);
+//  * Render fails loudly (std::runtime_error) instead of silently: no device, bad scene, etc.;
+//  * Render writes the whole W×H frame (the reference's loop renders min(W,H)², finding F1) and
+//    also fills the float buffer (getFCbuffer, F7).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+struct pbr_hip_ctx;
+struct pbr_scene_desc;
+
+// ---------------------------------------------------------------------------- FrameBuffer
+// Core/FrameBuffer.h (global namespace, as in the reference)
+class FrameBuffer {
+  public:
+    FrameBuffer() = default;
+    ~FrameBuffer() = default;
+    FrameBuffer(const FrameBuffer&) = delete;
+    FrameBuffer& operator=(const FrameBuffer&) = delete;
+    void InitBuffer(int width = 800, int height = 600, int channals = 4);
+    void FreeBuffer();
+    bool bufferResize(int width = 800, int height = 600);
+    bool set_uc(int w, int h, int shifting, const unsigned char& dat);
+    bool set_fc(int w, int h, int shifting, const float& dat);
+    unsigned char* getUCbuffer() { return ubuffer.data(); }
+    float* getFCbuffer() { return fbuffer.data(); }   // linear RGB(A) colObj/spp (not in the reference, F7)
+    int width = 0, height = 0, channals = 4;
+
+  private:
+    std::vector<unsigned char> ubuffer;
+    std::vector<float> fbuffer;
+};
+
+namespace PBR {
+
+// ---------------------------------------------------------------------------- Core/Geometry.h
+struct Vector3f {
+    float x = 0, y = 0, z = 0;
+    Vector3f() = default;
+    Vector3f(float x, float y, float z) : x(x), y(y), z(z) {}
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    float& operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+};
+struct Point3f : Vector3f {
+    using Vector3f::Vector3f;
+    Point3f() = default;
+};
+struct Normal3f : Vector3f {
+    using Vector3f::Vector3f;
+    Normal3f() = default;
+};
+struct Point2f {
+    float x = 0, y = 0;
+    Point2f() = default;
+    Point2f(float x, float y) : x(x), y(y) {}
+};
+struct Point2i {
+    int x = 0, y = 0;
+    Point2i() = default;
+    Point2i(int x, int y) : x(x), y(y) {}
+};
+struct Bounds2i {
+    Point2i pMin, pMax;
+    Bounds2i() = default;
+    Bounds2i(const Point2i& a, const Point2i& b) : pMin(a), pMax(b) {}
+};
+struct Bounds2f {
+    Point2f pMin, pMax;
+    Bounds2f() = default;
+    Bounds2f(const Point2f& a, const Point2f& b) : pMin(a), pMax(b) {}
+};
+
+// ---------------------------------------------------------------------------- Core/Spectrum.h
+class Spectrum {   // RGBSpectrum
+  public:
+    explicit Spectrum(float v = 0.f) : c{v, v, v} {}
+    static Spectrum FromRGB(const float rgb[3]) { Spectrum s; s.c[0] = rgb[0]; s.c[1] = rgb[1]; s.c[2] = rgb[2]; return s; }
+    float operator[](int i) const { return c[i]; }
+    float& operator[](int i) { return c[i]; }
+
+  private:
+    float c[3];
+};
+
+// ---------------------------------------------------------------------------- Core/Transform.h
+struct Matrix4x4 {
+    float m[4][4];
+    Matrix4x4();   // identity
+    explicit Matrix4x4(const float mat[4][4]);
+    Matrix4x4(float t00, float t01, float t02, float t03, float t10, float t11, float t12, float t13,
+              float t20, float t21, float t22, float t23, float t30, float t31, float t32, float t33);
+};
+Matrix4x4 Inverse(const Matrix4x4& m);   // Gauss-Jordan with full pivoting, as the reference
+Matrix4x4 Mul(const Matrix4x4& a, const Matrix4x4& b);
+
+class Transform {
+  public:
+    Transform() = default;
+    explicit Transform(const float mat[4][4]);
+    explicit Transform(const Matrix4x4& m);
+    Transform(const Matrix4x4& m, const Matrix4x4& mInv) : m(m), mInv(mInv) {}
+    friend Transform Inverse(const Transform& t) { return Transform(t.mInv, t.m); }
+    Transform operator*(const Transform& t2) const;
+    const Matrix4x4& GetMatrix() const { return m; }
+    const Matrix4x4& GetInverseMatrix() const { return mInv; }
+
+  private:
+    Matrix4x4 m, mInv;
+};
+Transform Translate(const Vector3f& delta);
+Transform Scale(float x, float y, float z);
+Transform RotateX(float theta);   // degrees
+Transform RotateY(float theta);
+Transform RotateZ(float theta);
+Transform LookAt(const Point3f& pos, const Point3f& look, const Vector3f& up);
+
+// ---------------------------------------------------------------------------- Texture/
+template <typename T>
+class Texture {
+  public:
+    virtual ~Texture() = default;
+    // The render path only evaluates constant textures (every material in main.cpp uses them).
+    virtual bool IsConstant() const { return false; }
+    virtual T ConstantValue() const { throw std::invalid_argument("only constant textures reach the GPU path"); }
+};
+template <typename T>
+class ConstantTexture : public Texture<T> {
+  public:
+    explicit ConstantTexture(const T& value) : value(value) {}
+    bool IsConstant() const override { return true; }
+    T ConstantValue() const override { return value; }
+
+  private:
+    T value;
+};
+
+// ---------------------------------------------------------------------------- Media/
+class Medium {
+  public:
+    virtual ~Medium() = default;
+};
+class HomogeneousMedium : public Medium {   // Media/HomogeneousMedium.h
+  public:
+    HomogeneousMedium(const Spectrum& sigma_a, const Spectrum& sigma_s, float g) : sigma_a(sigma_a), sigma_s(sigma_s), g(g) {}
+    const Spectrum sigma_a, sigma_s;
+    const float g;
+};
+struct MediumInterface {   // Media/Medium.h:55-60
+    MediumInterface() : inside(nullptr), outside(nullptr) {}
+    MediumInterface(const Medium* medium) : inside(medium), outside(medium) {}
+    MediumInterface(const Medium* inside, const Medium* outside) : inside(inside), outside(outside) {}
+    bool IsMediumTransition() const { return inside != outside; }
+    const Medium *inside, *outside;
+};
+
+// ---------------------------------------------------------------------------- Shape/
+class Shape {
+  public:
+    Shape(const Transform* ObjectToWorld, const Transform* WorldToObject, bool reverseOrientation)
+        : ObjectToWorld(ObjectToWorld), WorldToObject(WorldToObject), reverseOrientation(reverseOrientation) {}
+    virtual ~Shape() = default;
+    const Transform *ObjectToWorld, *WorldToObject;   // not owned (as in the reference, Shape.h:35)
+    const bool reverseOrientation;
+};
+struct TriangleMesh {   // Shape/Triangle.h:11-24; vertices kept in object space, baked on upload
+    TriangleMesh(const Transform& ObjectToWorld, int nTriangles, const int* vertexIndices, int nVertices, const Point3f* P,
+                 const Vector3f* S, const Normal3f* N, const Point2f* uv, const int* faceIndices);
+    const int nTriangles, nVertices;
+    Transform objectToWorld;
+    std::vector<int> vertexIndices;
+    std::vector<float> p;    // 3 per vertex
+    std::vector<float> n;    // 3 per vertex or empty
+    std::vector<float> uv;   // 2 per vertex or empty
+};
+class Triangle : public Shape {
+  public:
+    Triangle(const Transform* ObjectToWorld, const Transform* WorldToObject, bool reverseOrientation,
+             const std::shared_ptr<TriangleMesh>& mesh, int triNumber)
+        : Shape(ObjectToWorld, WorldToObject, reverseOrientation), mesh(mesh), triNumber(triNumber) {}
+    const std::shared_ptr<TriangleMesh> mesh;
+    const int triNumber;
+};
+std::vector<std::shared_ptr<Shape>> CreateTriangleMesh(const Transform* ObjectToWorld, const Transform* WorldToObject,
+                                                       bool reverseOrientation, int nTriangles, const int* vertexIndices,
+                                                       int nVertices, const Point3f* p, const Vector3f* s,
+                                                       const Normal3f* n, const Point2f* uv, const int* faceIndices = nullptr);
+class Sphere : public Shape {
+  public:
+    Sphere(const Transform* ObjectToWorld, const Transform* WorldToObject, bool reverseOrientation, float radius)
+        : Shape(ObjectToWorld, WorldToObject, reverseOrientation), radius(radius) {}
+    const float radius;
+};
+// Shape/plyRead.h: the reference's ".3d" text format ("vertex N face M", vertices ×20)
+class plyInfo {
+  public:
+    explicit plyInfo(const std::string& filePath);
+    int nVertices = 0, nTriangles = 0;
+    std::vector<Point3f> vertexArray;
+    std::vector<int> vertexIndices;
+};
+// Standard PLY (ascii / binary_little_endian; x y z vertices, triangle or quad faces) for the real
+// Stanford Dragon.  Vertices are not scaled.
+struct PlyMesh {
+    std::vector<Point3f> vertices;
+    std::vector<int> indices;
+};
+PlyMesh LoadPLY(const std::string& path);
+
+// ---------------------------------------------------------------------------- Material/
+class Material {
+  public:
+    virtual ~Material() = default;
+};
+using SpectrumTexture = std::shared_ptr<Texture<Spectrum>>;
+using FloatTexture = std::shared_ptr<Texture<float>>;
+class MatteMaterial : public Material {   // Material/MatteMaterial.h
+  public:
+    MatteMaterial(const SpectrumTexture& Kd, const FloatTexture& sigma, const FloatTexture& bumpMap)
+        : Kd(Kd), sigma(sigma), bumpMap(bumpMap) {}
+    SpectrumTexture Kd;
+    FloatTexture sigma, bumpMap;
+};
+class MirrorMaterial : public Material {   // Material/Mirror.h
+  public:
+    MirrorMaterial(const SpectrumTexture& r, const FloatTexture& bump) : Kr(r), bumpMap(bump) {}
+    SpectrumTexture Kr;
+    FloatTexture bumpMap;
+};
+class GlassMaterial : public Material {   // Material/GlassMaterial.h
+  public:
+    GlassMaterial(const SpectrumTexture& Kr, const SpectrumTexture& Kt, const FloatTexture& uRoughness,
+                  const FloatTexture& vRoughness, const FloatTexture& index, const FloatTexture& bumpMap, bool remapRoughness)
+        : Kr(Kr), Kt(Kt), uRoughness(uRoughness), vRoughness(vRoughness), index(index), bumpMap(bumpMap), remapRoughness(remapRoughness) {}
+    SpectrumTexture Kr, Kt;
+    FloatTexture uRoughness, vRoughness, index, bumpMap;
+    bool remapRoughness;
+};
+class MetalMaterial : public Material {   // Material/MetalMaterial.h
+  public:
+    MetalMaterial(const SpectrumTexture& eta, const SpectrumTexture& k, const FloatTexture& rough, const FloatTexture& urough,
+                  const FloatTexture& vrough, const FloatTexture& bump, bool remapRoughness)
+        : eta(eta), k(k), roughness(rough), uRoughness(urough), vRoughness(vrough), bumpMap(bump), remapRoughness(remapRoughness) {}
+    SpectrumTexture eta, k;
+    FloatTexture roughness, uRoughness, vRoughness, bumpMap;
+    bool remapRoughness;
+};
+class PlasticMaterial : public Material {   // Material/PlasticMaterial.h
+  public:
+    PlasticMaterial(const SpectrumTexture& Kd, const SpectrumTexture& Ks, const FloatTexture& roughness,
+                    const FloatTexture& bumpMap, bool remapRoughness)
+        : Kd(Kd), Ks(Ks), roughness(roughness), bumpMap(bumpMap), remapRoughness(remapRoughness) {}
+    SpectrumTexture Kd, Ks;
+    FloatTexture roughness, bumpMap;
+    bool remapRoughness;
+};
+
+// ---------------------------------------------------------------------------- Light/
+class Light {
+  public:
+    Light(const Transform& LightToWorld, const MediumInterface& mediumInterface, int nSamples = 1)
+        : nSamples(nSamples > 1 ? nSamples : 1), mediumInterface(mediumInterface), LightToWorld(LightToWorld) {}
+    virtual ~Light() = default;
+    virtual bool IsInfinite() const { return false; }
+    const int nSamples;
+    const MediumInterface mediumInterface;
+    const Transform LightToWorld;
+};
+class PointLight : public Light {   // Light/PointLight.h
+  public:
+    PointLight(const Transform& LightToWorld, const MediumInterface& mediumInterface, const Spectrum& I)
+        : Light(LightToWorld, mediumInterface), I(I) {}
+    const Spectrum I;
+};
+class AreaLight : public Light {
+  public:
+    using Light::Light;
+};
+class DiffuseAreaLight : public AreaLight {   // Light/DiffuseLight.h
+  public:
+    DiffuseAreaLight(const Transform& LightToWorld, const MediumInterface& mediumInterface, const Spectrum& Le, int nSamples,
+                     const std::shared_ptr<Shape>& shape, bool twoSided = false)
+        : AreaLight(LightToWorld, mediumInterface, nSamples), Lemit(Le), shape(shape), twoSided(twoSided) {}
+    const Spectrum Lemit;
+    const std::shared_ptr<Shape> shape;
+    const bool twoSided;
+};
+class SkyBoxLight : public Light {   // Light/SkyBoxLight.h
+  public:
+    // Loads a Radiance .hdr the way stbi_loadf does (vertically flipped, 3 components).
+    SkyBoxLight(const Transform& LightToWorld, const Point3f& worldCenter, float worldRadius, const char* file, int nSamples);
+    // In-memory variant: data = width*height*components floats, already in stbi_loadf's row order.
+    SkyBoxLight(const Transform& LightToWorld, const Point3f& worldCenter, float worldRadius, int width, int height,
+                int components, std::vector<float> data, int nSamples);
+    bool IsInfinite() const override { return true; }
+    bool loadImage(const char* imageFile);
+    const Point3f worldCenter;
+    const float worldRadius;
+    int imageWidth = 0, imageHeight = 0, nrComponents = 0;
+    std::vector<float> data;
+};
+
+// ---------------------------------------------------------------------------- Core/Primitive.h
+class Primitive {
+  public:
+    virtual ~Primitive() = default;
+};
+class GeometricPrimitive : public Primitive {
+  public:
+    GeometricPrimitive(const std::shared_ptr<Shape>& shape, const std::shared_ptr<Material>& material,
+                       const std::shared_ptr<AreaLight>& areaLight, const MediumInterface& mediumInterface)
+        : material(material), areaLight(areaLight), shape(shape), mediumInterface(mediumInterface) {}
+    std::shared_ptr<Material> material;
+    std::shared_ptr<AreaLight> areaLight;
+    std::shared_ptr<Shape> shape;
+    MediumInterface mediumInterface;
+};
+class Aggregate : public Primitive {};
+class BVHAccel : public Aggregate {   // Accelerator/BVHAccel.h:16-21; built on the device at upload
+  public:
+    enum class SplitMethod { SAH, HLBVH, Middle, EqualCounts };
+    BVHAccel(std::vector<std::shared_ptr<Primitive>> p, int maxPrimsInNode = 1, SplitMethod splitMethod = SplitMethod::SAH);
+    const std::vector<std::shared_ptr<Primitive>>& Primitives() const { return primitives; }
+    const int maxPrimsInNode;
+    const SplitMethod splitMethod;
+
+  private:
+    std::vector<std::shared_ptr<Primitive>> primitives;
+};
+
+// ---------------------------------------------------------------------------- Core/Scene.h
+class Scene {
+  public:
+    Scene(std::shared_ptr<Primitive> aggregate, const std::vector<std::shared_ptr<Light>>& lights);
+    std::vector<std::shared_ptr<Light>> lights;
+    std::vector<std::shared_ptr<Light>> infiniteLights;
+    const std::shared_ptr<Primitive>& GetAggregate() const { return aggregate; }
+    uint64_t Id() const { return id; }   // identifies the scene for upload caching
+
+  private:
+    std::shared_ptr<Primitive> aggregate;
+    uint64_t id;
+};
+
+// ---------------------------------------------------------------------------- Camera/
+class Camera {
+  public:
+    virtual ~Camera() = default;
+};
+class PerspectiveCamera : public Camera {   // Camera/Perspective.h
+  public:
+    PerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& CameraToWorld, const Bounds2f& screenWindow,
+                      float lensRadius, float focalDistance, float fov, const Medium* medium);
+    const int RasterWidth, RasterHeight;
+    const Transform CameraToWorld;
+    const Bounds2f screenWindow;
+    const float lensRadius, focalDistance, fov;
+    const Medium* medium;
+};
+PerspectiveCamera* CreatePerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& cam2world, Medium* media);
+
+// ---------------------------------------------------------------------------- Sampler/
+class Sampler {
+  public:
+    explicit Sampler(int64_t samplesPerPixel) : samplesPerPixel(samplesPerPixel) {}
+    virtual ~Sampler() = default;
+    const int64_t samplesPerPixel;
+};
+class HaltonSampler : public Sampler {   // Sampler/Halton.h
+  public:
+    HaltonSampler(int nsamp, const Bounds2i& sampleBounds, bool sampleAtCenter = false);
+    const Bounds2i sampleBounds;
+};
+HaltonSampler* CreateHaltonSampler(const Bounds2i& sampleBounds);   // 16 spp, as Halton.cpp:98-104
+
+// ---------------------------------------------------------------------------- Integrator/
+struct RenderStats {   // what the last Render measured (pbr_render_stats)
+    double seconds = 0, kernel_ms = 0;
+    uint64_t samples = 0;
+};
+class Integrator {
+  public:
+    virtual ~Integrator() = default;
+    virtual void Render(const Scene& scene, double& timeConsume) = 0;
+    float IntegratorRenderTime = 0;
+};
+class SamplerIntegrator : public Integrator {
+  public:
+    SamplerIntegrator(std::shared_ptr<const Camera> camera, std::shared_ptr<Sampler> sampler, const Bounds2i& pixelBounds,
+                      FrameBuffer* m_FrameBuffer);
+    ~SamplerIntegrator() override;
+    // SamplerIntegrator::Render (Integrator.cpp:280-356) on the GPU: uploads the scene (once per
+    // Scene), renders every pixel × sample, fills m_FrameBuffer's 8-bit buffer exactly as the
+    // reference (XYZ round trip, gamma, vertical flip) and its float buffer.
+    void Render(const Scene& scene, double& timeConsume) override;
+    // Extensions: device ordinal; restrict to tiles (multi-GPU sharding); last stats.
+    void SetDevice(int device) { this->device = device; }
+    void SetTiles(const std::vector<Bounds2i>& tiles) { this->tiles = tiles; }
+    const RenderStats& LastStats() const { return stats; }
+
+  protected:
+    virtual int IntegratorType() const = 0;
+    virtual int MaxDepth() const = 0;
+    virtual float RRThreshold() const { return 1.f; }
+    virtual int LightStrategy() const { return 0; }
+    std::shared_ptr<const Camera> camera;
+
+  private:
+    std::shared_ptr<Sampler> sampler;
+    const Bounds2i pixelBounds;
+    FrameBuffer* m_FrameBuffer;
+    int device = 0;
+    std::vector<Bounds2i> tiles;
+    RenderStats stats;
+    pbr_hip_ctx* ctx = nullptr;
+    uint64_t uploadedScene = 0;
+};
+class WhittedIntegrator : public SamplerIntegrator {   // Integrator/WhittedIntegrator.h
+  public:
+    WhittedIntegrator(int maxDepth, std::shared_ptr<const Camera> camera, std::shared_ptr<Sampler> sampler,
+                      const Bounds2i& pixelBounds, FrameBuffer* m_FrameBuffer)
+        : SamplerIntegrator(camera, sampler, pixelBounds, m_FrameBuffer), maxDepth(maxDepth) {}
+
+  protected:
+    int IntegratorType() const override;
+    int MaxDepth() const override { return maxDepth; }
+
+  private:
+    const int maxDepth;
+};
+class PathIntegrator : public SamplerIntegrator {   // Integrator/PathIntegrator.h
+  public:
+    PathIntegrator(int maxDepth, std::shared_ptr<const Camera> camera, std::shared_ptr<Sampler> sampler,
+                   const Bounds2i& pixelBounds, float rrThreshold = 1, const std::string& lightSampleStrategy = "spatial",
+                   FrameBuffer* framebuffer = nullptr)
+        : SamplerIntegrator(camera, sampler, pixelBounds, framebuffer), maxDepth(maxDepth), rrThreshold(rrThreshold),
+          lightSampleStrategy(lightSampleStrategy) {}
+
+  protected:
+    int IntegratorType() const override;
+    int MaxDepth() const override { return maxDepth; }
+    float RRThreshold() const override { return rrThreshold; }
+    int LightStrategy() const override;
+
+  private:
+    const int maxDepth;
+    const float rrThreshold;
+    const std::string lightSampleStrategy;
+};
+class VolPathIntegrator : public PathIntegrator {   // Integrator/VolPathIntegrator.h
+  public:
+    using PathIntegrator::PathIntegrator;
+
+  protected:
+    int IntegratorType() const override;
+};
+using HipWhittedIntegrator = WhittedIntegrator;
+using HipPathIntegrator = PathIntegrator;
+using HipVolPathIntegrator = VolPathIntegrator;
+
+// ---------------------------------------------------------------------------- flattening
+// The scene as the C-ABI takes it (pbr_scene_desc + owned arrays); exposed for tests and for
+// callers that drive the C-ABI themselves.
+struct FlatScene;
+std::shared_ptr<FlatScene> FlattenScene(const Scene& scene, const Medium* cameraMedium = nullptr);
+const ::pbr_scene_desc* SceneDesc(const FlatScene& f);
+int MediumIndex(const FlatScene& f, const Medium* m);
+
+}  // namespace PBR

@@ -129,3 +129,47 @@ def assemble(width, height, tiles, packed, channels):
         frame[y0:y1, x0:x1] = packed[pos:pos + n].reshape(y1 - y0, x1 - x0, channels)
         pos += n
     return frame
+
+
+def span_pixels(width, height, rank, world, tile=64):
+    """Pixels in rank's packed span (the sum of its tiles' areas)."""
+    return sum((t[2] - t[0]) * (t[3] - t[1]) for t in tiles_for_rank(width, height, rank, world, tile))
+
+
+class FrameGather:
+    """Multi-GPU exchange.  Every rank holds its tiles' packed float-RGB span (a
+    torch tensor [npx, 3] on its device, or on the CPU under gloo).  One `gather` brings the spans
+    to rank 0 (RCCL over xGMI under the nccl backend), padded to the largest span, and rank 0
+    scatters them into a row-major [height*width, 3] frame on its own device (index_copy_ with
+    per-rank pixel indices computed once)."""
+
+    def __init__(self, width, height, world, device, tile=64):
+        import torch
+        self.world = world
+        self.npx = [span_pixels(width, height, r, world, tile) for r in range(world)]
+        self.max_px = max(self.npx)
+        self.index = []
+        for r in range(world):
+            idx = [y * width + x for (x0, y0, x1, y1) in tiles_for_rank(width, height, r, world, tile)
+                   for y in range(y0, y1) for x in range(x0, x1)]
+            self.index.append(torch.tensor(idx, dtype=torch.long, device=device))
+        self.send = torch.zeros((self.max_px, 3), dtype=torch.float32, device=device)
+        self.recv = [torch.empty_like(self.send) for _ in range(world)]
+        self.frame = torch.zeros((height * width, 3), dtype=torch.float32, device=device)
+
+    def __call__(self, span, rank, group=None):
+        import torch.distributed as dist
+        self.send[:span.shape[0]].copy_(span)
+        dist.gather(self.send, gather_list=self.recv if rank == 0 else None, dst=0, group=group)
+        if rank != 0:
+            return None
+        for r in range(self.world):
+            self.frame.index_copy_(0, self.index[r], self.recv[r][:self.npx[r]])
+        return self.frame
+
+
+def gather_frame(span, width, height, rank, world, group=None, tile=64):
+    """One-shot FrameGather: the assembled [height, width, 3] numpy frame on rank 0, None elsewhere."""
+    g = FrameGather(width, height, world, span.device, tile)
+    f = g(span, rank, group)
+    return None if f is None else f.cpu().numpy().reshape(height, width, 3)

@@ -1,0 +1,710 @@
+// pbr_host.cpp — the C++ host API of include/pbr/pbr.h: the reference's scene classes, flattened
+// into a pbr_scene_desc and rendered through the C-ABI (include/pbr_hip.h).
+#include "../../include/pbr/pbr.h"
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <unordered_map>
+
+#include "../../include/pbr_hip.h"
+#include "../csrc/pbr_xform.h"
+
+// ============================================================================ FrameBuffer
+void FrameBuffer::InitBuffer(int w, int h, int ch) {
+    width = w;
+    height = h;
+    channals = ch;
+    ubuffer.clear();
+    fbuffer.clear();
+    if (ch > 4 || w <= 0 || h <= 0) return;
+    ubuffer.assign((size_t)w * h * ch, 0);
+    fbuffer.assign((size_t)w * h * ch, 0.f);
+}
+void FrameBuffer::FreeBuffer() {
+    ubuffer.clear();
+    fbuffer.clear();
+    width = height = channals = 0;
+}
+bool FrameBuffer::bufferResize(int w, int h) {
+    if (width == 0 || height == 0 || channals == 0) return false;
+    InitBuffer(w, h, channals);
+    return true;
+}
+bool FrameBuffer::set_uc(int w, int h, int shifting, const unsigned char& dat) {
+    if (ubuffer.empty() || w >= width || h >= height || w < 0 || h < 0) return false;
+    ubuffer[((size_t)w + (size_t)h * width) * channals + shifting] = dat;
+    return true;
+}
+bool FrameBuffer::set_fc(int w, int h, int shifting, const float& dat) {
+    if (fbuffer.empty() || w >= width || h >= height || w < 0 || h < 0) return false;
+    fbuffer[((size_t)w + (size_t)h * width) * channals + shifting] = dat;
+    return true;
+}
+
+namespace PBR {
+
+namespace {
+
+pbr::xform::Mat to_mat(const Matrix4x4& m) {
+    pbr::xform::Mat r;
+    std::memcpy(r.a, m.m, 64);
+    return r;
+}
+Matrix4x4 from_mat(const pbr::xform::Mat& m) { return Matrix4x4(m.a); }
+Transform from_xf(const pbr::xform::Xf& x) { return Transform(from_mat(x.m), from_mat(x.mi)); }
+pbr::f3 f3of(const Vector3f& v) { return pbr::mk(v.x, v.y, v.z); }
+
+void fill_transform(const Transform& t, pbr_transform* out) {
+    std::memcpy(out->m, t.GetMatrix().m, 64);
+    std::memcpy(out->m_inv, t.GetInverseMatrix().m, 64);
+}
+
+std::atomic<uint64_t> g_sceneIds{1};
+
+}  // namespace
+
+// ============================================================================ Transform
+Matrix4x4::Matrix4x4() {
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) m[i][j] = i == j ? 1.f : 0.f;
+}
+Matrix4x4::Matrix4x4(const float mat[4][4]) { std::memcpy(m, mat, 64); }
+Matrix4x4::Matrix4x4(float t00, float t01, float t02, float t03, float t10, float t11, float t12, float t13, float t20,
+                     float t21, float t22, float t23, float t30, float t31, float t32, float t33) {
+    const float v[16] = {t00, t01, t02, t03, t10, t11, t12, t13, t20, t21, t22, t23, t30, t31, t32, t33};
+    std::memcpy(m, v, 64);
+}
+Matrix4x4 Inverse(const Matrix4x4& m) { return from_mat(pbr::xform::invert(to_mat(m))); }
+Matrix4x4 Mul(const Matrix4x4& a, const Matrix4x4& b) { return from_mat(pbr::xform::mul(to_mat(a), to_mat(b))); }
+Transform::Transform(const float mat[4][4]) : m(mat), mInv(Inverse(m)) {}
+Transform::Transform(const Matrix4x4& m) : m(m), mInv(Inverse(m)) {}
+Transform Transform::operator*(const Transform& t2) const { return Transform(Mul(m, t2.m), Mul(t2.mInv, mInv)); }
+
+Transform Translate(const Vector3f& d) { return from_xf(pbr::xform::translate(f3of(d))); }
+Transform Scale(float x, float y, float z) { return from_xf(pbr::xform::scale(x, y, z)); }
+namespace {
+Transform rotate_axis(float theta, int axis) {   // Transform.cpp RotateX/Y/Z: m and its transpose
+    float rad = (pbr::kPi / 180) * theta;
+    float s = pbr::t_sin(rad), c = pbr::t_cos(rad);
+    Matrix4x4 m;
+    int a = (axis + 1) % 3, b = (axis + 2) % 3;
+    m.m[a][a] = c;
+    m.m[b][b] = c;
+    // RotateX: m[1][2] = -s, m[2][1] = s; RotateY: m[0][2] = s, m[2][0] = -s; RotateZ: m[0][1] = -s, m[1][0] = s
+    if (axis == 1) { m.m[0][2] = s; m.m[2][0] = -s; }
+    else { m.m[a][b] = -s; m.m[b][a] = s; }
+    Matrix4x4 t;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) t.m[i][j] = m.m[j][i];
+    return Transform(m, t);
+}
+}  // namespace
+Transform RotateX(float theta) { return rotate_axis(theta, 0); }
+Transform RotateY(float theta) { return rotate_axis(theta, 1); }
+Transform RotateZ(float theta) { return rotate_axis(theta, 2); }
+Transform LookAt(const Point3f& pos, const Point3f& look, const Vector3f& up) {
+    return from_xf(pbr::xform::look_at(f3of(pos), f3of(look), f3of(up)));
+}
+
+// ============================================================================ shapes
+TriangleMesh::TriangleMesh(const Transform& ObjectToWorld, int nTriangles, const int* vi, int nVertices, const Point3f* P,
+                           const Vector3f* /*S*/, const Normal3f* N, const Point2f* UV, const int* /*faceIndices*/)
+    : nTriangles(nTriangles), nVertices(nVertices), objectToWorld(ObjectToWorld), vertexIndices(vi, vi + 3 * nTriangles) {
+    p.resize((size_t)3 * nVertices);
+    for (int i = 0; i < nVertices; ++i) { p[3 * i] = P[i].x; p[3 * i + 1] = P[i].y; p[3 * i + 2] = P[i].z; }
+    if (N) {
+        n.resize((size_t)3 * nVertices);
+        for (int i = 0; i < nVertices; ++i) { n[3 * i] = N[i].x; n[3 * i + 1] = N[i].y; n[3 * i + 2] = N[i].z; }
+    }
+    if (UV) {
+        uv.resize((size_t)2 * nVertices);
+        for (int i = 0; i < nVertices; ++i) { uv[2 * i] = UV[i].x; uv[2 * i + 1] = UV[i].y; }
+    }
+}
+
+std::vector<std::shared_ptr<Shape>> CreateTriangleMesh(const Transform* o2w, const Transform* w2o, bool reverseOrientation,
+                                                       int nTriangles, const int* vertexIndices, int nVertices,
+                                                       const Point3f* p, const Vector3f* s, const Normal3f* n,
+                                                       const Point2f* uv, const int* faceIndices) {
+    auto mesh = std::make_shared<TriangleMesh>(*o2w, nTriangles, vertexIndices, nVertices, p, s, n, uv, faceIndices);
+    std::vector<std::shared_ptr<Shape>> tris;
+    tris.reserve(nTriangles);
+    for (int i = 0; i < nTriangles; ++i) tris.push_back(std::make_shared<Triangle>(o2w, w2o, reverseOrientation, mesh, i));
+    return tris;
+}
+
+plyInfo::plyInfo(const std::string& filePath) {   // Shape/plyRead.h:22-47
+    std::ifstream f(filePath);
+    if (!f) throw std::runtime_error("plyInfo: cannot open " + filePath);
+    std::string ed;
+    for (int i = 0; i < 2; i++) {
+        f >> ed;
+        if (ed == "vertex") f >> nVertices;
+        else if (ed == "face") f >> nTriangles;
+    }
+    vertexArray.resize(nVertices);
+    vertexIndices.resize((size_t)3 * nTriangles);
+    for (int i = 0; i < nVertices; i++) {
+        f >> vertexArray[i].x >> vertexArray[i].y >> vertexArray[i].z;
+        vertexArray[i].x *= 20; vertexArray[i].y *= 20; vertexArray[i].z *= 20;
+    }
+    for (int i = 0; i < nTriangles; i++) f >> ed >> vertexIndices[i * 3] >> vertexIndices[i * 3 + 1] >> vertexIndices[i * 3 + 2];
+    if (!f) throw std::runtime_error("plyInfo: truncated " + filePath);
+}
+
+namespace {
+struct PlyProp { std::string name, type, countType; bool list = false; };
+struct PlyElem { std::string name; long count = 0; std::vector<PlyProp> props; };
+size_t ply_size(const std::string& t) {
+    if (t == "char" || t == "uchar" || t == "int8" || t == "uint8") return 1;
+    if (t == "short" || t == "ushort" || t == "int16" || t == "uint16") return 2;
+    if (t == "int" || t == "uint" || t == "float" || t == "int32" || t == "uint32" || t == "float32") return 4;
+    if (t == "double" || t == "float64") return 8;
+    throw std::runtime_error("LoadPLY: unknown property type " + t);
+}
+double ply_read_bin(const unsigned char* b, const std::string& t) {
+    if (t == "char" || t == "int8") return (double)*(const int8_t*)b;
+    if (t == "uchar" || t == "uint8") return (double)*b;
+    int16_t s; uint16_t us; int32_t i; uint32_t u; float fl; double d;
+    if (t == "short" || t == "int16") { std::memcpy(&s, b, 2); return s; }
+    if (t == "ushort" || t == "uint16") { std::memcpy(&us, b, 2); return us; }
+    if (t == "int" || t == "int32") { std::memcpy(&i, b, 4); return i; }
+    if (t == "uint" || t == "uint32") { std::memcpy(&u, b, 4); return u; }
+    if (t == "float" || t == "float32") { std::memcpy(&fl, b, 4); return fl; }
+    std::memcpy(&d, b, 8);
+    return d;
+}
+}  // namespace
+
+PlyMesh LoadPLY(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("LoadPLY: cannot open " + path);
+    std::string line, format;
+    std::vector<PlyElem> elems;
+    std::getline(f, line);
+    if (line.rfind("ply", 0) != 0) throw std::runtime_error("LoadPLY: not a PLY file");
+    while (std::getline(f, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        std::istringstream ls(line);
+        std::string kw;
+        ls >> kw;
+        if (kw == "format") ls >> format;
+        else if (kw == "element") { PlyElem e; ls >> e.name >> e.count; elems.push_back(e); }
+        else if (kw == "property") {
+            PlyProp p;
+            std::string t;
+            ls >> t;
+            if (t == "list") { p.list = true; ls >> p.countType >> p.type >> p.name; }
+            else { p.type = t; ls >> p.name; }
+            if (elems.empty()) throw std::runtime_error("LoadPLY: property before element");
+            elems.back().props.push_back(p);
+        } else if (kw == "end_header") break;
+    }
+    if (format != "ascii" && format != "binary_little_endian") throw std::runtime_error("LoadPLY: unsupported format " + format);
+    const bool ascii = format == "ascii";
+    PlyMesh out;
+    for (const PlyElem& e : elems) {
+        int ix = -1, iy = -1, iz = -1, iface = -1;
+        for (size_t k = 0; k < e.props.size(); ++k) {
+            if (e.props[k].name == "x") ix = (int)k;
+            if (e.props[k].name == "y") iy = (int)k;
+            if (e.props[k].name == "z") iz = (int)k;
+            if (e.props[k].list && (e.props[k].name == "vertex_indices" || e.props[k].name == "vertex_index")) iface = (int)k;
+        }
+        for (long r = 0; r < e.count; ++r) {
+            std::vector<double> scalars(e.props.size(), 0.0);
+            std::vector<long> face;
+            for (size_t k = 0; k < e.props.size(); ++k) {
+                const PlyProp& p = e.props[k];
+                if (p.list) {
+                    long cnt;
+                    if (ascii) f >> cnt;
+                    else { unsigned char b[8]; f.read((char*)b, ply_size(p.countType)); cnt = (long)ply_read_bin(b, p.countType); }
+                    for (long c = 0; c < cnt; ++c) {
+                        double v;
+                        if (ascii) f >> v;
+                        else { unsigned char b[8]; f.read((char*)b, ply_size(p.type)); v = ply_read_bin(b, p.type); }
+                        if ((int)k == iface) face.push_back((long)v);
+                    }
+                } else {
+                    if (ascii) f >> scalars[k];
+                    else { unsigned char b[8]; f.read((char*)b, ply_size(p.type)); scalars[k] = ply_read_bin(b, p.type); }
+                }
+            }
+            if (!f) throw std::runtime_error("LoadPLY: truncated " + path);
+            if (e.name == "vertex" && ix >= 0 && iy >= 0 && iz >= 0)
+                out.vertices.emplace_back((float)scalars[ix], (float)scalars[iy], (float)scalars[iz]);
+            if (e.name == "face" && iface >= 0)
+                for (size_t k = 2; k < face.size(); ++k) {   // fan-triangulate quads / polygons
+                    out.indices.push_back((int)face[0]);
+                    out.indices.push_back((int)face[k - 1]);
+                    out.indices.push_back((int)face[k]);
+                }
+        }
+    }
+    return out;
+}
+
+// ============================================================================ lights
+namespace {
+// Radiance RGBE → float exactly as stbi_loadf (stbi__hdr_load / stbi__hdr_convert), rows flipped
+// as stbi_set_flip_vertically_on_load(true) does (SkyBoxLight.cpp:19-24).
+bool load_hdr(const char* file, int* w, int* h, int* comp, std::vector<float>* data) {
+    std::ifstream f(file, std::ios::binary);
+    if (!f) return false;
+    std::string line;
+    std::getline(f, line);
+    if (line != "#?RADIANCE" && line != "#?RGBE") return false;
+    bool fmt = false;
+    while (std::getline(f, line)) {
+        if (line.empty()) break;
+        if (line == "FORMAT=32-bit_rle_rgbe") fmt = true;
+    }
+    if (!fmt) return false;
+    std::getline(f, line);
+    int H = 0, W = 0;
+    if (std::sscanf(line.c_str(), "-Y %d +X %d", &H, &W) != 2 || W <= 0 || H <= 0) return false;
+    std::vector<unsigned char> rgbe((size_t)W * H * 4);
+    auto rd = [&](unsigned char* p, size_t n) { f.read((char*)p, (std::streamsize)n); return (bool)f; };
+    bool flat = W < 8 || W >= 32768;
+    for (int y = 0; y < H && !flat; ++y) {
+        unsigned char hdr[4];
+        if (!rd(hdr, 4)) return false;
+        if (hdr[0] != 2 || hdr[1] != 2 || (hdr[2] & 0x80)) {   // not RLE: these 4 bytes are the first pixel
+            if (y != 0) return false;
+            std::memcpy(&rgbe[0], hdr, 4);
+            if (!rd(&rgbe[4], rgbe.size() - 4)) return false;
+            flat = true;
+            break;
+        }
+        if (((int)hdr[2] << 8 | hdr[3]) != W) return false;
+        std::vector<unsigned char> sc((size_t)W * 4);
+        for (int c = 0; c < 4; ++c) {
+            int i = 0;
+            while (i < W) {
+                unsigned char cnt;
+                if (!rd(&cnt, 1)) return false;
+                if (cnt > 128) {
+                    unsigned char v;
+                    if (!rd(&v, 1)) return false;
+                    cnt -= 128;
+                    if (i + cnt > W) return false;
+                    for (int k = 0; k < cnt; ++k) sc[(size_t)(i++) * 4 + c] = v;
+                } else {
+                    if (cnt == 0 || i + cnt > W) return false;
+                    for (int k = 0; k < cnt; ++k) { unsigned char v; if (!rd(&v, 1)) return false; sc[(size_t)(i++) * 4 + c] = v; }
+                }
+            }
+        }
+        std::memcpy(&rgbe[(size_t)y * W * 4], sc.data(), sc.size());
+        if (y == H - 1) break;
+    }
+    if (flat && W >= 8 && W < 32768 && rgbe.empty()) return false;
+    if (flat && (W < 8 || W >= 32768) && !rd(rgbe.data(), rgbe.size())) return false;
+    data->assign((size_t)W * H * 3, 0.f);
+    for (int y = 0; y < H; ++y) {
+        int dy = H - 1 - y;   // vertical flip
+        for (int x = 0; x < W; ++x) {
+            const unsigned char* in = &rgbe[((size_t)y * W + x) * 4];
+            float* o = &(*data)[((size_t)dy * W + x) * 3];
+            if (in[3] != 0) {
+                float f1 = (float)std::ldexp(1.0f, in[3] - (int)(128 + 8));
+                o[0] = in[0] * f1; o[1] = in[1] * f1; o[2] = in[2] * f1;
+            }
+        }
+    }
+    *w = W; *h = H; *comp = 3;
+    return true;
+}
+}  // namespace
+
+SkyBoxLight::SkyBoxLight(const Transform& LightToWorld, const Point3f& worldCenter, float worldRadius, const char* file, int nSamples)
+    : Light(LightToWorld, MediumInterface(), nSamples), worldCenter(worldCenter), worldRadius(worldRadius) {
+    loadImage(file);   // as the reference: a missing file leaves a black sky
+}
+SkyBoxLight::SkyBoxLight(const Transform& LightToWorld, const Point3f& worldCenter, float worldRadius, int width, int height,
+                         int components, std::vector<float> d, int nSamples)
+    : Light(LightToWorld, MediumInterface(), nSamples), worldCenter(worldCenter), worldRadius(worldRadius),
+      imageWidth(width), imageHeight(height), nrComponents(components), data(std::move(d)) {
+    if ((size_t)width * height * components != data.size()) throw std::invalid_argument("SkyBoxLight: data size mismatch");
+}
+bool SkyBoxLight::loadImage(const char* imageFile) {
+    imageWidth = imageHeight = nrComponents = 0;
+    data.clear();
+    return imageFile && load_hdr(imageFile, &imageWidth, &imageHeight, &nrComponents, &data);
+}
+
+// ============================================================================ aggregate, scene, camera, sampler
+BVHAccel::BVHAccel(std::vector<std::shared_ptr<Primitive>> p, int maxPrimsInNode, SplitMethod splitMethod)
+    : maxPrimsInNode(std::min(255, maxPrimsInNode)), splitMethod(splitMethod), primitives(std::move(p)) {
+    if (splitMethod != SplitMethod::SAH) throw std::invalid_argument("BVHAccel: only SplitMethod::SAH is on the GPU path");
+}
+
+Scene::Scene(std::shared_ptr<Primitive> aggregate, const std::vector<std::shared_ptr<Light>>& lights)
+    : lights(lights), aggregate(std::move(aggregate)), id(g_sceneIds++) {
+    for (const auto& l : lights)
+        if (l->IsInfinite()) infiniteLights.push_back(l);
+}
+
+PerspectiveCamera::PerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& CameraToWorld, const Bounds2f& screenWindow,
+                                     float lensRadius, float focalDistance, float fov, const Medium* medium)
+    : RasterWidth(RasterWidth), RasterHeight(RasterHeight), CameraToWorld(CameraToWorld), screenWindow(screenWindow),
+      lensRadius(lensRadius), focalDistance(focalDistance), fov(fov), medium(medium) {}
+
+PerspectiveCamera* CreatePerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& cam2world, Medium* media) {
+    // Camera/Perspective.cpp:84-104
+    float frame = (float)RasterWidth / (float)RasterHeight;
+    Bounds2f screen;
+    if (frame > 1.f) { screen.pMin.x = -frame; screen.pMax.x = frame; screen.pMin.y = -1.f; screen.pMax.y = 1.f; }
+    else { screen.pMin.x = -1.f; screen.pMax.x = 1.f; screen.pMin.y = -1.f / frame; screen.pMax.y = 1.f / frame; }
+    return new PerspectiveCamera(RasterWidth, RasterHeight, cam2world, screen, 0.0f, 0.0f, 90.0f, media);
+}
+
+HaltonSampler::HaltonSampler(int nsamp, const Bounds2i& sampleBounds, bool sampleAtCenter)
+    : Sampler(nsamp), sampleBounds(sampleBounds) {
+    if (sampleAtCenter) throw std::invalid_argument("HaltonSampler: sampleAtCenter is not on the GPU path");
+}
+HaltonSampler* CreateHaltonSampler(const Bounds2i& sampleBounds) { return new HaltonSampler(16, sampleBounds, false); }
+
+// ============================================================================ flattening
+struct FlatScene {
+    pbr_scene_desc desc{};
+    std::vector<pbr_shape_desc> shapes;
+    std::vector<pbr_material_desc> materials;
+    std::vector<pbr_light_desc> lights;
+    std::vector<pbr_medium_desc> media;
+    std::vector<std::vector<int32_t>> indexRuns;
+    std::vector<std::shared_ptr<TriangleMesh>> meshes;   // keep P/N/UV alive
+    std::vector<std::shared_ptr<SkyBoxLight>> skies;     // keep env data alive
+    std::map<const Medium*, int> mediumIndex;
+};
+
+namespace {
+Spectrum spec(const SpectrumTexture& t, const char* what) {
+    if (!t) throw std::invalid_argument(std::string("material texture missing: ") + what);
+    return t->ConstantValue();
+}
+float flt(const FloatTexture& t, const char* what) {
+    if (!t) throw std::invalid_argument(std::string("material texture missing: ") + what);
+    return t->ConstantValue();
+}
+void put(float* d, const Spectrum& s) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
+
+pbr_material_desc material_desc(const Material* m) {
+    pbr_material_desc d;
+    std::memset(&d, 0, sizeof(d));
+    if (auto* x = dynamic_cast<const MatteMaterial*>(m)) {
+        d.type = PBR_MAT_MATTE;
+        put(d.Kd, spec(x->Kd, "Kd"));
+        d.sigma = flt(x->sigma, "sigma");
+    } else if (auto* x = dynamic_cast<const MirrorMaterial*>(m)) {
+        d.type = PBR_MAT_MIRROR;
+        put(d.Kr, spec(x->Kr, "Kr"));
+    } else if (auto* x = dynamic_cast<const GlassMaterial*>(m)) {
+        d.type = PBR_MAT_GLASS;
+        put(d.Kr, spec(x->Kr, "Kr"));
+        put(d.Kt, spec(x->Kt, "Kt"));
+        d.uroughness = flt(x->uRoughness, "uRoughness");
+        d.vroughness = flt(x->vRoughness, "vRoughness");
+        d.eta = flt(x->index, "index");
+        d.remap_roughness = x->remapRoughness;
+    } else if (auto* x = dynamic_cast<const MetalMaterial*>(m)) {
+        d.type = PBR_MAT_METAL;
+        put(d.metal_eta, spec(x->eta, "eta"));
+        put(d.metal_k, spec(x->k, "k"));
+        d.roughness = x->roughness ? x->roughness->ConstantValue() : 0.f;
+        d.has_uv_roughness = (x->uRoughness && x->vRoughness) ? 1 : 0;
+        if (d.has_uv_roughness) { d.uroughness = x->uRoughness->ConstantValue(); d.vroughness = x->vRoughness->ConstantValue(); }
+        else if (!x->roughness) throw std::invalid_argument("MetalMaterial: no roughness");
+        d.remap_roughness = x->remapRoughness;
+    } else if (auto* x = dynamic_cast<const PlasticMaterial*>(m)) {
+        d.type = PBR_MAT_PLASTIC;
+        put(d.Kd, spec(x->Kd, "Kd"));
+        put(d.Ks, spec(x->Ks, "Ks"));
+        d.roughness = flt(x->roughness, "roughness");
+        d.remap_roughness = x->remapRoughness;
+    } else {
+        throw std::invalid_argument("material type not on the GPU path");
+    }
+    return d;
+}
+}  // namespace
+
+int MediumIndex(const FlatScene& f, const Medium* m) {
+    if (!m) return -1;
+    auto it = f.mediumIndex.find(m);
+    if (it == f.mediumIndex.end()) throw std::invalid_argument("medium not part of the scene");
+    return it->second;
+}
+
+std::shared_ptr<FlatScene> FlattenScene(const Scene& scene, const Medium* cameraMedium) {
+    auto F = std::make_shared<FlatScene>();
+    auto* bvh = dynamic_cast<const BVHAccel*>(scene.GetAggregate().get());
+    if (!bvh) throw std::invalid_argument("Scene aggregate must be a BVHAccel");
+    const auto& prims = bvh->Primitives();
+    // media
+    auto addMedium = [&](const Medium* m) {
+        if (!m || F->mediumIndex.count(m)) return;
+        auto* h = dynamic_cast<const HomogeneousMedium*>(m);
+        if (!h) throw std::invalid_argument("only HomogeneousMedium is on the GPU path");
+        pbr_medium_desc d;
+        put(d.sigma_a, h->sigma_a);
+        put(d.sigma_s, h->sigma_s);
+        d.g = h->g;
+        F->mediumIndex[m] = (int)F->media.size();
+        F->media.push_back(d);
+    };
+    std::vector<const GeometricPrimitive*> gps;
+    gps.reserve(prims.size());
+    for (const auto& p : prims) {
+        auto* gp = dynamic_cast<const GeometricPrimitive*>(p.get());
+        if (!gp) throw std::invalid_argument("BVHAccel primitives must be GeometricPrimitives");
+        gps.push_back(gp);
+        addMedium(gp->mediumInterface.inside);
+        addMedium(gp->mediumInterface.outside);
+    }
+    for (const auto& l : scene.lights) { addMedium(l->mediumInterface.inside); addMedium(l->mediumInterface.outside); }
+    addMedium(cameraMedium);
+    // materials
+    std::map<const Material*, int> matIndex;
+    for (auto* gp : gps) {
+        const Material* m = gp->material.get();
+        if (!m || matIndex.count(m)) continue;
+        matIndex[m] = (int)F->materials.size();
+        F->materials.push_back(material_desc(m));
+    }
+    // lights: scene.lights order; area lights are bound to their shape below
+    std::unordered_map<const Light*, int> lightIndex;
+    for (size_t i = 0; i < scene.lights.size(); ++i) lightIndex[scene.lights[i].get()] = (int)i;
+    F->lights.resize(scene.lights.size());
+    std::vector<bool> boundArea(scene.lights.size(), false);
+    // shapes: maximal runs of consecutive triangles sharing mesh, transform, material, medium
+    // interface and consecutively numbered area lights
+    size_t i = 0;
+    while (i < gps.size()) {
+        const GeometricPrimitive* gp = gps[i];
+        pbr_shape_desc sd;
+        std::memset(&sd, 0, sizeof(sd));
+        sd.material = gp->material ? matIndex[gp->material.get()] : -1;
+        sd.medium_inside = MediumIndex(*F, gp->mediumInterface.inside);
+        sd.medium_outside = MediumIndex(*F, gp->mediumInterface.outside);
+        sd.reverse_orientation = gp->shape->reverseOrientation;
+        auto lightOf = [&](const GeometricPrimitive* g) -> int {
+            if (!g->areaLight) return -1;
+            auto it = lightIndex.find(g->areaLight.get());
+            if (it == lightIndex.end()) throw std::invalid_argument("area light is not in Scene::lights");
+            return it->second;
+        };
+        const int firstLight = lightOf(gp);
+        const int shapeIdx = (int)F->shapes.size();
+        if (auto* tri = dynamic_cast<const Triangle*>(gp->shape.get())) {
+            const auto& mesh = tri->mesh;
+            std::vector<int32_t> idx;
+            size_t j = i;
+            while (j < gps.size()) {
+                const GeometricPrimitive* g = gps[j];
+                auto* t = dynamic_cast<const Triangle*>(g->shape.get());
+                if (!t || t->mesh != mesh || t->reverseOrientation != tri->reverseOrientation || g->material != gp->material ||
+                    g->mediumInterface.inside != gp->mediumInterface.inside ||
+                    g->mediumInterface.outside != gp->mediumInterface.outside)
+                    break;
+                int li = lightOf(g);
+                int k = (int)(j - i);
+                if ((firstLight < 0) != (li < 0) || (firstLight >= 0 && li != firstLight + k)) break;
+                if (li >= 0) {
+                    auto* dl = dynamic_cast<const DiffuseAreaLight*>(g->areaLight.get());
+                    if (!dl || dl->shape.get() != g->shape.get()) throw std::invalid_argument("area light shape mismatch");
+                    pbr_light_desc& L = F->lights[li];
+                    std::memset(&L, 0, sizeof(L));
+                    L.type = PBR_LIGHT_DIFFUSE_AREA;
+                    fill_transform(dl->LightToWorld, &L.light_to_world);
+                    put(L.Le, dl->Lemit);
+                    L.shape = shapeIdx;
+                    L.triangle = k;
+                    L.two_sided = dl->twoSided;
+                    L.n_samples = dl->nSamples;
+                    L.medium_inside = MediumIndex(*F, dl->mediumInterface.inside);
+                    L.medium_outside = MediumIndex(*F, dl->mediumInterface.outside);
+                    boundArea[li] = true;
+                }
+                const int* v = &mesh->vertexIndices[(size_t)3 * t->triNumber];
+                idx.insert(idx.end(), v, v + 3);
+                ++j;
+            }
+            sd.type = PBR_SHAPE_TRIANGLE_MESH;
+            fill_transform(mesh->objectToWorld, &sd.object_to_world);
+            sd.n_triangles = (int)(j - i);
+            sd.n_vertices = mesh->nVertices;
+            F->indexRuns.push_back(std::move(idx));
+            sd.indices = F->indexRuns.back().data();
+            sd.P = mesh->p.data();
+            sd.N = mesh->n.empty() ? nullptr : mesh->n.data();
+            sd.UV = mesh->uv.empty() ? nullptr : mesh->uv.data();
+            sd.area_light_first = firstLight;
+            F->meshes.push_back(mesh);
+            i = j;
+        } else if (auto* sph = dynamic_cast<const Sphere*>(gp->shape.get())) {
+            if (firstLight >= 0) throw std::invalid_argument("sphere area lights are not on the GPU path");
+            sd.type = PBR_SHAPE_SPHERE;
+            fill_transform(*sph->ObjectToWorld, &sd.object_to_world);
+            sd.radius = sph->radius;
+            sd.area_light_first = -1;
+            ++i;
+        } else {
+            throw std::invalid_argument("shape type not on the GPU path");
+        }
+        F->shapes.push_back(sd);
+    }
+    // index runs were moved into a growing vector: re-point after all insertions
+    for (size_t s = 0, r = 0; s < F->shapes.size(); ++s)
+        if (F->shapes[s].type == PBR_SHAPE_TRIANGLE_MESH) F->shapes[s].indices = F->indexRuns[r++].data();
+    for (size_t li = 0; li < scene.lights.size(); ++li) {
+        const Light* l = scene.lights[li].get();
+        pbr_light_desc& L = F->lights[li];
+        if (auto* pl = dynamic_cast<const PointLight*>(l)) {
+            std::memset(&L, 0, sizeof(L));
+            L.type = PBR_LIGHT_POINT;
+            fill_transform(pl->LightToWorld, &L.light_to_world);
+            put(L.I, pl->I);
+            L.n_samples = pl->nSamples;
+            L.medium_inside = MediumIndex(*F, pl->mediumInterface.inside);
+            L.medium_outside = MediumIndex(*F, pl->mediumInterface.outside);
+        } else if (auto* sk = dynamic_cast<const SkyBoxLight*>(l)) {
+            std::memset(&L, 0, sizeof(L));
+            L.type = PBR_LIGHT_SKYBOX;
+            fill_transform(sk->LightToWorld, &L.light_to_world);
+            L.world_center[0] = sk->worldCenter.x; L.world_center[1] = sk->worldCenter.y; L.world_center[2] = sk->worldCenter.z;
+            L.world_radius = sk->worldRadius;
+            L.env_width = sk->imageWidth;
+            L.env_height = sk->imageHeight;
+            L.env_components = sk->nrComponents;
+            L.env_data = sk->data.empty() ? nullptr : sk->data.data();
+            L.n_samples = sk->nSamples;
+            L.medium_inside = L.medium_outside = -1;
+            F->skies.push_back(std::static_pointer_cast<SkyBoxLight>(scene.lights[li]));
+        } else if (dynamic_cast<const DiffuseAreaLight*>(l)) {
+            if (!boundArea[li]) throw std::invalid_argument("DiffuseAreaLight whose shape is not a scene triangle");
+        } else {
+            throw std::invalid_argument("light type not on the GPU path");
+        }
+    }
+    pbr_scene_desc& d = F->desc;
+    d.abi_version = PBR_HIP_ABI_VERSION;
+    d.n_shapes = (int)F->shapes.size();
+    d.shapes = F->shapes.data();
+    d.n_materials = (int)F->materials.size();
+    d.materials = F->materials.data();
+    d.n_lights = (int)F->lights.size();
+    d.lights = F->lights.data();
+    d.n_media = (int)F->media.size();
+    d.media = F->media.data();
+    d.max_prims_in_node = bvh->maxPrimsInNode;
+    return F;
+}
+
+const pbr_scene_desc* SceneDesc(const FlatScene& f) { return &f.desc; }
+
+// ============================================================================ integrators
+SamplerIntegrator::SamplerIntegrator(std::shared_ptr<const Camera> camera, std::shared_ptr<Sampler> sampler,
+                                     const Bounds2i& pixelBounds, FrameBuffer* m_FrameBuffer)
+    : camera(std::move(camera)), sampler(std::move(sampler)), pixelBounds(pixelBounds), m_FrameBuffer(m_FrameBuffer) {}
+
+SamplerIntegrator::~SamplerIntegrator() {
+    if (ctx) pbr_hip_destroy(ctx);
+}
+
+int WhittedIntegrator::IntegratorType() const { return PBR_INTEGRATOR_WHITTED; }
+int PathIntegrator::IntegratorType() const { return PBR_INTEGRATOR_PATH; }
+int VolPathIntegrator::IntegratorType() const { return PBR_INTEGRATOR_VOLPATH; }
+int PathIntegrator::LightStrategy() const {
+    // LightDistrib.cpp:10-21: "uniform" and "power"; "spatial" (the default) falls back to uniform
+    return lightSampleStrategy == "power" ? PBR_LIGHTS_POWER : PBR_LIGHTS_UNIFORM;
+}
+
+namespace {
+void check(pbr_hip_ctx* ctx, int rc, const char* what) {
+    if (rc == PBR_OK) return;
+    std::string msg = std::string(what) + " failed (" + std::to_string(rc) + ")";
+    if (ctx) msg += ": " + std::string(pbr_hip_last_error(ctx));
+    throw std::runtime_error(msg);
+}
+}  // namespace
+
+void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
+    auto t0 = std::chrono::steady_clock::now();
+    auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
+    if (!cam) throw std::invalid_argument("Render: only PerspectiveCamera is on the GPU path");
+    auto* halton = dynamic_cast<const HaltonSampler*>(sampler.get());
+    if (!halton) throw std::invalid_argument("Render: only HaltonSampler is on the GPU path");
+    const int W = pixelBounds.pMax.x, H = pixelBounds.pMax.y;   // the reference reads pMax only
+    if (W <= 0 || H <= 0 || W > cam->RasterWidth || H > cam->RasterHeight)
+        throw std::invalid_argument("Render: pixelBounds outside the camera raster");
+    // the device derives the screen window as CreatePerspectiveCamera does
+    float frame = (float)cam->RasterWidth / (float)cam->RasterHeight;
+    float sx = frame > 1.f ? frame : 1.f, sy = frame > 1.f ? 1.f : 1.f / frame;
+    if (cam->screenWindow.pMin.x != -sx || cam->screenWindow.pMax.x != sx || cam->screenWindow.pMin.y != -sy ||
+        cam->screenWindow.pMax.y != sy)
+        throw std::invalid_argument("Render: custom screen windows are not on the GPU path");
+    if (!ctx) check(nullptr, pbr_hip_create(device, &ctx), "pbr_hip_create");
+    auto flat = FlattenScene(scene, cam->medium);
+    if (uploadedScene != scene.Id()) {
+        check(ctx, pbr_hip_upload_scene(ctx, SceneDesc(*flat)), "pbr_hip_upload_scene");
+        uploadedScene = scene.Id();
+    }
+    pbr_render_desc rd;
+    std::memset(&rd, 0, sizeof(rd));
+    rd.integrator = IntegratorType();
+    rd.max_depth = MaxDepth();
+    rd.rr_threshold = RRThreshold();
+    rd.light_strategy = LightStrategy();
+    rd.sampler = PBR_SAMPLER_HALTON;
+    rd.spp = (int)halton->samplesPerPixel;
+    pbr_camera_desc& c = rd.camera;
+    c.width = cam->RasterWidth;
+    c.height = cam->RasterHeight;
+    fill_transform(cam->CameraToWorld, &c.camera_to_world);
+    c.fov = cam->fov;
+    c.lens_radius = cam->lensRadius;
+    c.focal_distance = cam->focalDistance;
+    c.medium = MediumIndex(*flat, cam->medium);
+    std::vector<pbr_tile> tl;
+    if (!tiles.empty()) {
+        for (const Bounds2i& b : tiles) tl.push_back({b.pMin.x, b.pMin.y, b.pMax.x, b.pMax.y});
+    } else {
+        tl.push_back({0, 0, W, H});
+    }
+    rd.n_tiles = (int)tl.size();
+    rd.tiles = tl.data();
+    size_t npx = 0;
+    for (const pbr_tile& t : tl) npx += (size_t)(t.x1 - t.x0) * (t.y1 - t.y0);
+    std::vector<float> rgb(npx * 3);
+    std::vector<uint8_t> rgba(npx * 4);
+    pbr_render_stats st;
+    check(ctx, pbr_hip_render(ctx, &rd, rgb.data(), rgba.data(), &st), "pbr_hip_render");
+    if (m_FrameBuffer) {
+        if (m_FrameBuffer->width != W || m_FrameBuffer->height != H || m_FrameBuffer->channals < 3)
+            throw std::invalid_argument("Render: FrameBuffer not initialised to the pixel bounds");
+        size_t k = 0;
+        for (const pbr_tile& t : tl)
+            for (int y = t.y0; y < t.y1; ++y)
+                for (int x = t.x0; x < t.x1; ++x, ++k)
+                    for (int ch = 0; ch < m_FrameBuffer->channals; ++ch) {
+                        // Integrator.cpp:341-344: set_uc(x, pMax.y - y - 1, ...) — the image is flipped
+                        m_FrameBuffer->set_uc(x, H - y - 1, ch, rgba[4 * k + ch]);
+                        m_FrameBuffer->set_fc(x, H - y - 1, ch, ch < 3 ? rgb[3 * k + ch] : 1.f);
+                    }
+    }
+    stats.seconds = st.seconds;
+    stats.kernel_ms = st.kernel_ms;
+    stats.samples = st.samples;
+    timeConsume = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    IntegratorRenderTime = (float)timeConsume;
+}
+
+}  // namespace PBR

@@ -1,0 +1,243 @@
+// host_api_test.cpp — the C++ host API (include/pbr/pbr.h) used exactly as the reference's
+// Main/main.cpp uses its classes, checked against the oracle (test infrastructure) on the same
+// flattened scene.
+//
+//   host_api_test cpu   no GPU needed: scene building, flattening, oracle sanity, Render fails loudly
+//   host_api_test gpu   renders through WhittedIntegrator / PathIntegrator / VolPathIntegrator on
+//                       the GPU and compares the FrameBuffer with the oracle (L∞ ≤ 1e-3, u8 ≤ 1)
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/pbr/pbr.h"
+#include "../../include/pbr_hip.h"
+#include "../../oracle/pbr_oracle.h"
+
+using namespace PBR;
+
+namespace {
+
+int failures = 0;
+void expect(bool ok, const std::string& what) {
+    std::printf("%s %s\n", ok ? "ok  " : "FAIL", what.c_str());
+    if (!ok) ++failures;
+}
+
+std::shared_ptr<Texture<Spectrum>> rgbTex(float r, float g, float b) {
+    float v[3] = {r, g, b};
+    return std::make_shared<ConstantTexture<Spectrum>>(Spectrum::FromRGB(v));
+}
+std::shared_ptr<Texture<float>> fTex(float v) { return std::make_shared<ConstantTexture<float>>(v); }
+
+struct Built {
+    std::vector<std::unique_ptr<Transform>> xf;   // shapes keep raw Transform pointers
+    std::vector<std::unique_ptr<Medium>> media;
+    std::unique_ptr<Scene> scene;
+    std::shared_ptr<Camera> cam;
+    const Medium* camMedium = nullptr;
+};
+
+const Transform* keep(Built& b, const Transform& t) {
+    b.xf.push_back(std::make_unique<Transform>(t));
+    return b.xf.back().get();
+}
+
+// C1 of SURVEY §8(d): two matte spheres, point light I=20 at (0,4,4), camera (0,0,5) → origin.
+void build_c1(Built& b, int W, int H) {
+    std::vector<std::shared_ptr<Primitive>> prims;
+    auto matte = std::make_shared<MatteMaterial>(rgbTex(0.5f, 0.5f, 0.5f), fTex(0.f), nullptr);
+    const Vector3f centres[2] = {Vector3f(-1.f, 0.f, 0.f), Vector3f(1.2f, 0.f, -1.f)};
+    for (const Vector3f& c : centres) {
+        const Transform* o2w = keep(b, Translate(c));
+        const Transform* w2o = keep(b, Inverse(*o2w));
+        auto s = std::make_shared<Sphere>(o2w, w2o, false, 1.f);
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, matte, nullptr, MediumInterface()));
+    }
+    std::vector<std::shared_ptr<Light>> lights;
+    lights.push_back(std::make_shared<PointLight>(Translate(Vector3f(0.f, 4.f, 4.f)), MediumInterface(), Spectrum(20.f)));
+    b.scene = std::make_unique<Scene>(std::make_shared<BVHAccel>(prims, 1), lights);
+    Transform lookat = LookAt(Point3f(0.f, 0.f, 5.f), Point3f(0.f, 0.f, 0.f), Vector3f(0.f, 1.f, 0.f));
+    b.cam = std::shared_ptr<Camera>(CreatePerspectiveCamera(W, H, Inverse(lookat), nullptr));
+}
+
+// A C3/C5-shaped scene: a small tetrahedral mesh (glass, optionally filled with a homogeneous
+// medium) over a matte floor, lit by a one-sided two-triangle area light at y = 2.45.
+void build_area(Built& b, int W, int H, bool medium) {
+    std::vector<std::shared_ptr<Primitive>> prims;
+    const Medium* inside = nullptr;
+    if (medium) {
+        b.media.push_back(std::make_unique<HomogeneousMedium>(Spectrum(0.5f), Spectrum(4.4f), -0.5f));
+        inside = b.media.back().get();
+    }
+    auto glass = std::make_shared<GlassMaterial>(rgbTex(1, 1, 1), rgbTex(1, 1, 1), fTex(0.1f), fTex(0.1f), fTex(1.5f), nullptr, false);
+    auto floorMat = std::make_shared<MatteMaterial>(rgbTex(0.6f, 0.6f, 0.6f), fTex(0.f), nullptr);
+    const Transform* id = keep(b, Transform());
+    const Point3f tp[4] = {Point3f(-0.8f, -0.9f, -0.5f), Point3f(0.8f, -0.9f, -0.5f), Point3f(0.f, -0.9f, 0.8f), Point3f(0.f, 0.6f, 0.f)};
+    const int ti[12] = {0, 2, 1, 0, 1, 3, 1, 2, 3, 2, 0, 3};
+    for (auto& s : CreateTriangleMesh(id, id, false, 4, ti, 4, tp, nullptr, nullptr, nullptr))
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, glass, nullptr, MediumInterface(inside, nullptr)));
+    const Point3f fp[4] = {Point3f(-5, -1, -5), Point3f(5, -1, -5), Point3f(5, -1, 5), Point3f(-5, -1, 5)};
+    const int fi[6] = {0, 2, 1, 0, 3, 2};
+    for (auto& s : CreateTriangleMesh(id, id, false, 2, fi, 4, fp, nullptr, nullptr, nullptr))
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, floorMat, nullptr, MediumInterface()));
+    // area light: quad facing down (reverseOrientation flips the normal to -y)
+    const Transform* lx = keep(b, Translate(Vector3f(0.f, 2.45f, 0.f)));
+    const Transform* lxi = keep(b, Inverse(*lx));
+    const Point3f lp[4] = {Point3f(-0.6f, 0, -0.6f), Point3f(0.6f, 0, -0.6f), Point3f(0.6f, 0, 0.6f), Point3f(-0.6f, 0, 0.6f)};
+    const int li[6] = {0, 1, 2, 0, 2, 3};
+    std::vector<std::shared_ptr<Light>> lights;
+    auto lightMat = std::make_shared<MatteMaterial>(rgbTex(0, 0, 0), fTex(0.f), nullptr);
+    for (auto& s : CreateTriangleMesh(lx, lxi, true, 2, li, 4, lp, nullptr, nullptr, nullptr)) {
+        auto area = std::make_shared<DiffuseAreaLight>(*lx, MediumInterface(), Spectrum(5.f), 5, s, false);
+        lights.push_back(area);
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, lightMat, area, MediumInterface()));
+    }
+    b.scene = std::make_unique<Scene>(std::make_shared<BVHAccel>(prims, 1), lights);
+    Transform lookat = LookAt(Point3f(0.f, 0.3f, 3.2f), Point3f(0.f, -0.3f, 0.f), Vector3f(0.f, 1.f, 0.f));
+    b.cam = std::shared_ptr<Camera>(CreatePerspectiveCamera(W, H, Inverse(lookat), nullptr));
+}
+
+// The same camera/render settings as SamplerIntegrator::Render builds, for the oracle.
+pbr_render_desc oracle_desc(const Built& b, const FlatScene& flat, int integrator, int spp, int depth, float rr) {
+    auto* cam = dynamic_cast<const PerspectiveCamera*>(b.cam.get());
+    pbr_render_desc rd;
+    std::memset(&rd, 0, sizeof(rd));
+    rd.integrator = integrator;
+    rd.max_depth = depth;
+    rd.rr_threshold = rr;
+    rd.sampler = PBR_SAMPLER_HALTON;
+    rd.spp = spp;
+    rd.camera.width = cam->RasterWidth;
+    rd.camera.height = cam->RasterHeight;
+    std::memcpy(rd.camera.camera_to_world.m, cam->CameraToWorld.GetMatrix().m, 64);
+    std::memcpy(rd.camera.camera_to_world.m_inv, cam->CameraToWorld.GetInverseMatrix().m, 64);
+    rd.camera.fov = cam->fov;
+    rd.camera.medium = MediumIndex(flat, cam->medium);
+    return rd;
+}
+
+// Renders `integrator` through the host API and compares its FrameBuffer with the oracle.
+void compare(const char* name, Built& b, std::shared_ptr<SamplerIntegrator> integ, FrameBuffer& fb, int itype, int spp,
+             int depth, float rr) {
+    double t = 0;
+    integ->Render(*b.scene, t);
+    auto flat = FlattenScene(*b.scene, nullptr);
+    pbr_render_desc rd = oracle_desc(b, *flat, itype, spp, depth, rr);
+    const int W = fb.width, H = fb.height;
+    std::vector<float> rgb((size_t)W * H * 3);
+    std::vector<uint8_t> rgba((size_t)W * H * 4);
+    double sec = 0;
+    int rc = oracle_render(SceneDesc(*flat), &rd, rgb.data(), rgba.data(), 0, &sec);
+    expect(rc == 0, std::string(name) + ": oracle render");
+    float linf = 0;
+    int u8 = 0;
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+            for (int c = 0; c < 3; ++c) {
+                size_t k = (size_t)(y * W + x);
+                size_t f = ((size_t)x + (size_t)(H - 1 - y) * W) * fb.channals + c;   // FrameBuffer is flipped
+                float d = std::fabs(fb.getFCbuffer()[f] - rgb[3 * k + c]);
+                if (!(d <= linf)) linf = std::isnan(d) ? 1e30f : d;
+                int du = std::abs((int)fb.getUCbuffer()[f] - (int)rgba[4 * k + c]);
+                if (du > u8) u8 = du;
+            }
+    char msg[256];
+    std::snprintf(msg, sizeof msg, "%s %dx%d %d spp: L_inf %.3g (<= 1e-3), 8-bit max diff %d (<= 1), %.2f ms on device", name, W, H,
+                  spp, linf, u8, integ->LastStats().kernel_ms);
+    expect(linf <= 1e-3f && u8 <= 1, msg);
+    expect(fb.getUCbuffer()[3] == 255, std::string(name) + ": alpha 255");
+}
+
+int run_cpu() {
+    Built b;
+    build_c1(b, 32, 32);
+    auto flat = FlattenScene(*b.scene, nullptr);
+    const pbr_scene_desc* d = SceneDesc(*flat);
+    expect(d->n_shapes == 2 && d->shapes[0].type == PBR_SHAPE_SPHERE && d->n_lights == 1 && d->n_materials == 1,
+           "C1 flattens to 2 spheres, 1 material, 1 point light");
+    pbr_render_desc rd = oracle_desc(b, *flat, PBR_INTEGRATOR_WHITTED, 1, 5, 1.f);
+    std::vector<float> rgb(32 * 32 * 3);
+    std::vector<uint8_t> rgba(32 * 32 * 4);
+    double sec;
+    expect(oracle_render(d, &rd, rgb.data(), rgba.data(), 1, &sec) == 0 && rgba[0] == 231,
+           "oracle on the flattened C1: corner is the F4 grey (231)");
+    Built a;
+    build_area(a, 16, 16, true);
+    auto flat2 = FlattenScene(*a.scene, nullptr);
+    const pbr_scene_desc* d2 = SceneDesc(*flat2);
+    expect(d2->n_shapes == 3 && d2->shapes[0].n_triangles == 4 && d2->shapes[2].area_light_first == 0 && d2->n_media == 1 &&
+               d2->shapes[0].medium_inside == 0 && d2->lights[1].triangle == 1,
+           "area-light scene flattens to mesh runs with bound lights and a medium");
+    // Render must fail loudly without a device (no CPU fallback)
+    FrameBuffer fb;
+    fb.InitBuffer(32, 32, 4);
+    auto sampler = std::make_shared<HaltonSampler>(1, Bounds2i(Point2i(0, 0), Point2i(32, 32)));
+    WhittedIntegrator w(5, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(32, 32)), &fb);
+    bool threw = false;
+    try {
+        double t;
+        w.Render(*b.scene, t);
+    } catch (const std::runtime_error& e) {
+        threw = std::string(e.what()).find("pbr_hip_create") != std::string::npos;
+        std::printf("     (%s)\n", e.what());
+    }
+    expect(threw, "Render without a GPU throws from pbr_hip_create");
+    Matrix4x4 m(2, 0, 0, 1, 0, 3, 0, 2, 0, 0, 4, 3, 0, 0, 0, 1);
+    Matrix4x4 p = Mul(m, Inverse(m));
+    bool ident = true;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) ident &= std::fabs(p.m[i][j] - (i == j ? 1.f : 0.f)) < 1e-6f;
+    expect(ident, "Matrix4x4 Inverse");
+    return failures ? 1 : 0;
+}
+
+int run_gpu() {
+    {
+        Built b;
+        const int W = 96, H = 64, spp = 4;
+        build_c1(b, W, H);
+        FrameBuffer fb;
+        fb.InitBuffer(W, H, 4);
+        auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        auto w = std::make_shared<WhittedIntegrator>(5, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), &fb);
+        compare("Whitted C1", b, w, fb, PBR_INTEGRATOR_WHITTED, spp, 5, 1.f);
+    }
+    {
+        Built b;
+        const int W = 48, H = 40, spp = 8;
+        build_area(b, W, H, false);
+        FrameBuffer fb;
+        fb.InitBuffer(W, H, 4);
+        auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        auto p = std::make_shared<PathIntegrator>(8, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &fb);
+        compare("Path glass + area light", b, p, fb, PBR_INTEGRATOR_PATH, spp, 8, 0.8f);
+    }
+    {
+        Built b;
+        const int W = 40, H = 32, spp = 8;
+        build_area(b, W, H, true);
+        FrameBuffer fb;
+        fb.InitBuffer(W, H, 4);
+        auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        auto v = std::make_shared<VolPathIntegrator>(10, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 1.f, "uniform", &fb);
+        compare("VolPath homogeneous medium", b, v, fb, PBR_INTEGRATOR_VOLPATH, spp, 10, 1.f);
+    }
+    return failures ? 1 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::string mode = argc > 1 ? argv[1] : "cpu";
+    try {
+        int rc = mode == "gpu" ? run_gpu() : run_cpu();
+        std::printf("%s: %d failure(s)\n", mode.c_str(), failures);
+        return rc;
+    } catch (const std::exception& e) {
+        std::printf("FAIL exception: %s\n", e.what());
+        return 2;
+    }
+}
