@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBR_HIP_ABI_VERSION 1
+#define PBR_HIP_ABI_VERSION 2
 
 /* ---- status codes ---- */
 enum {
@@ -181,6 +181,15 @@ typedef struct pbr_render_desc {
     int outputs_on_device;      /* 1: rgb_out/rgba_out are device pointers (e.g. torch tensors) */
     void* stream;               /* hipStream_t to launch on (NULL = context stream) */
     int collect_stats;          /* 1: also count BVH node visits / triangle tests (slower) */
+    /* PBR_SAMPLER_SOBOL (pbrt-v3 SobolSampler; the reference ships only its tables, F3):
+     * generator matrices in the layout of the reference's SobolMatrices32 (Sampler/SobolMatrices.h:
+     * 42-47: [dims][52] uint32 columns).  NULL → built-in matrices: dimensions 0 and 1 are the
+     * canonical ones (identical to SobolMatrices32's), dimensions >= 2 are Sobol' matrices from
+     * primitive polynomials in degree order with unit initial direction numbers — pass the
+     * reference's own SobolMatrices32 for its sequence.  spp is rounded up to a power of two
+     * (GlobalSampler(RoundUpPow2(spp))). */
+    const uint32_t* sobol_matrices;
+    int sobol_dims;
 } pbr_render_desc;
 
 typedef struct pbr_render_stats {
@@ -218,6 +227,8 @@ int pbr_hip_intersect(pbr_hip_ctx* ctx, int n, const float* rays, float* out, in
 /* Device build info: ABI version, gfx arch string. */
 int pbr_hip_abi_version(void);
 const char* pbr_hip_build_info(void);
+/* The built-in Sobol' generator matrices (SobolMatrices32 layout, dims × 52 uint32); host only. */
+int pbr_hip_sobol_matrices(int dims, uint32_t* out);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <stdexcept>
 #include <vector>
 
 namespace orc {
@@ -425,8 +426,123 @@ struct HaltonTables {
     }
 };
 
-// Sampler/Halton.cpp:30-92 + Sampler/Sampler.cpp:10-143 (GlobalSampler, no sample arrays)
+// pbrt-v3 SobolSampler (the reference ships only the tables, F3): SobolSampleFloat,
+// SobolIntervalToIndex and SampleDimension.  Matrices in SobolMatrices32 layout ([dims][52]).
+struct SobolO {
+    static constexpr int MatrixSize = 52;
+    std::vector<uint32_t> M;
+    int dims = 0, resolution = 1, log2Res = 0;
+    // built-in Sobol' matrices: dim 0 van der Corput, then one dimension per primitive polynomial
+    // over GF(2), enumerated by degree and coefficient value, initial direction numbers all 1
+    static bool primitive(uint32_t poly, int deg) {
+        uint64_t order = (1ull << deg) - 1;
+        auto mulmod = [&](uint64_t a, uint64_t b) {
+            uint64_t r = 0;
+            while (b) {
+                if (b & 1) r ^= a;
+                b >>= 1;
+                a <<= 1;
+                if (a >> deg & 1) a ^= poly;
+            }
+            return r;
+        };
+        auto xpow = [&](uint64_t e) {
+            uint64_t r = 1, x = (deg == 1) ? 1 : 2;   // x mod (x + 1) == 1
+            for (; e; e >>= 1) { if (e & 1) r = mulmod(r, x); x = mulmod(x, x); }
+            return r;
+        };
+        if (xpow(order) != 1) return false;
+        std::vector<uint64_t> factors;
+        uint64_t n = order;
+        for (uint64_t q = 2; q * q <= n; ++q)
+            if (n % q == 0) { factors.push_back(q); while (n % q == 0) n /= q; }
+        if (n > 1) factors.push_back(n);
+        for (uint64_t q : factors)
+            if (xpow(order / q) == 1) return false;
+        return true;
+    }
+    static void builtin(int nDims, std::vector<uint32_t>* out) {
+        out->assign((size_t)nDims * MatrixSize, 0);
+        for (int c = 0; c < 32; ++c) (*out)[c] = 1u << (31 - c);
+        int d = 1;
+        for (int deg = 1; d < nDims; ++deg)
+            for (uint32_t a = 0; a < (1u << (deg - 1)) && d < nDims; ++a) {
+                uint32_t poly = (1u << deg) | (a << 1) | 1u;
+                if (!primitive(poly, deg)) continue;
+                std::vector<uint64_t> m(MatrixSize + 1, 1);
+                for (int k = deg + 1; k <= MatrixSize; ++k) {   // Bratley-Fox recurrence
+                    uint64_t v = m[k - deg] ^ (m[k - deg] << deg);
+                    for (int i = 1; i < deg; ++i)
+                        if ((poly >> (deg - i)) & 1u) v ^= m[k - i] << i;
+                    m[k] = v;
+                }
+                // 32-bit columns of v_k = m_k / 2^k: index bits >= 32 keep v_k's top 32 bits
+                for (int c = 0; c < MatrixSize; ++c)
+                    (*out)[(size_t)d * MatrixSize + c] = (uint32_t)(c < 32 ? m[c + 1] << (31 - c) : m[c + 1] >> (c - 31));
+                ++d;
+            }
+    }
+    void init(const uint32_t* user, int userDims, int w, int h) {
+        if (user) { M.assign(user, user + (size_t)userDims * MatrixSize); dims = userDims; }
+        else { builtin(1024, &M); dims = 1024; }
+        resolution = 1; log2Res = 0;
+        while (resolution < std::max(w, h)) { resolution <<= 1; ++log2Res; }
+    }
+    // the first two dimensions' top log2Res bits of index bit c, as one 2m-bit word (x high, y low)
+    uint64_t pixelColumn(int c) const {
+        int m = log2Res;
+        uint64_t x = M[c] >> (32 - m), y = M[MatrixSize + c] >> (32 - m);
+        return (x << m) | y;
+    }
+    // SobolIntervalToIndex: the sample of `frame` whose dims 0/1 fall in pixel (px, py); solved by
+    // Gaussian elimination on the 2m×2m system every call
+    int64_t GetIndexForSample(int px, int py, int64_t frame) const {
+        const int m = log2Res;
+        if (m == 0) return 0;   // as pbrt-v3's SobolIntervalToIndex
+        const int n = 2 * m;
+        uint64_t target = ((uint64_t)px << m) | (uint64_t)py;
+        for (int k = 0; (frame >> k) != 0; ++k)
+            if ((frame >> k) & 1) target ^= pixelColumn(n + k);
+        // rows r of [A | t]: A[r] bit c = bit r of column c
+        std::vector<uint64_t> A(n);
+        std::vector<int> t(n);
+        for (int r = 0; r < n; ++r) {
+            A[r] = 0;
+            for (int c = 0; c < n; ++c) A[r] |= ((pixelColumn(c) >> r) & 1ull) << c;
+            t[r] = (int)((target >> r) & 1ull);
+        }
+        for (int c = 0; c < n; ++c) {
+            int piv = -1;
+            for (int r = c; r < n; ++r) if ((A[r] >> c) & 1ull) { piv = r; break; }
+            if (piv < 0) throw std::runtime_error("Sobol dims 0/1 singular");
+            std::swap(A[c], A[piv]);
+            std::swap(t[c], t[piv]);
+            for (int r = 0; r < n; ++r)
+                if (r != c && ((A[r] >> c) & 1ull)) { A[r] ^= A[c]; t[r] ^= t[c]; }
+        }
+        uint64_t j = 0;
+        for (int c = 0; c < n; ++c) j |= (uint64_t)t[c] << c;
+        return (int64_t)(((uint64_t)frame << n) | j);
+    }
+    float SampleDimension(int64_t index, int dim, int px, int py) const {
+        if (dim >= dims) return 0.f;   // pbrt aborts here
+        uint32_t v = 0;
+        uint64_t a = (uint64_t)index;
+        for (int i = dim * MatrixSize; a != 0; a >>= 1, ++i)
+            if (a & 1) v ^= M[i];
+        float s = fmin_((float)v * 0x1p-32f, OneMinusEpsilon);
+        if (dim == 0 || dim == 1) {
+            s = s * resolution + 0;   // sampleBounds.pMin == 0
+            s = Clampf(s - (float)(dim == 0 ? px : py), 0.f, OneMinusEpsilon);
+        }
+        return s;
+    }
+};
+
+// Sampler/Halton.cpp:30-92 + Sampler/Sampler.cpp:10-143 (GlobalSampler, no sample arrays); with
+// sob set the same GlobalSampler bookkeeping drives the Sobol sampler instead.
 struct Halton {
+    const SobolO* sob = nullptr;
     const HaltonTables* tab;
     int baseScales[2], baseExponents[2], sampleStride, multInverse[2];
     int64_t spp;
@@ -464,6 +580,7 @@ struct Halton {
         return index;
     }
     int64_t GetIndexForSample(int px, int py, int64_t sampleNum) {
+        if (sob) return sob->GetIndexForSample(px, py, sampleNum);
         int64_t off = 0;
         if (sampleStride > 1) {
             int pm[2] = {px % 128, py % 128};
@@ -478,6 +595,7 @@ struct Halton {
         return off + sampleNum * sampleStride;
     }
     float SampleDimension(int64_t index, int dim) const {
+        if (sob) return sob->SampleDimension(index, dim, px, py);
         if (dim == 0) return RadicalInverseBase2((uint64_t)(index >> baseExponents[0]));
         if (dim == 1) return RadicalInverseB(3, (uint64_t)(index / baseScales[1]));
         if (dim >= (int)tab->primes.size()) return 0;   // beyond PrimeTableSize: UB in the reference

@@ -1544,6 +1544,9 @@ static Spec SampleLi(const Ctx& c, const Camera& cam, Halton& sampler, int x, in
 struct RenderSetup {
     std::unique_ptr<Scene> scene;
     HaltonTables tab;
+    SobolO sob;
+    bool sobol = false;
+    int spp = 0;          // GlobalSampler samplesPerPixel (Sobol: RoundUpPow2)
     Camera cam;
     Ctx ctx;
     std::vector<pbr_tile> tiles;
@@ -1551,7 +1554,15 @@ struct RenderSetup {
     size_t nPixels = 0;
 };
 static void Setup(RenderSetup& rs, const pbr_scene_desc* sd, const pbr_render_desc* rd) {
-    if (rd->sampler != PBR_SAMPLER_HALTON) throw std::runtime_error("oracle: only the Halton sampler is restated");
+    if (rd->sampler != PBR_SAMPLER_HALTON && rd->sampler != PBR_SAMPLER_SOBOL) throw std::runtime_error("oracle: unknown sampler");
+    rs.sobol = rd->sampler == PBR_SAMPLER_SOBOL;
+    rs.spp = rd->spp;
+    if (rs.sobol) {
+        int p2 = 1;
+        while (p2 < rs.spp) p2 <<= 1;
+        rs.spp = p2;                                  // SobolSampler: GlobalSampler(RoundUpPow2(spp))
+        rs.sob.init(rd->sobol_matrices, rd->sobol_dims, rd->camera.width, rd->camera.height);
+    }
     rs.scene = BuildScene(sd);
     rs.tab.init(DimsNeeded(rd));
     rs.cam.init(rd->camera);
@@ -1579,7 +1590,7 @@ static int RenderImpl(const pbr_scene_desc* sd, const pbr_render_desc* rd, float
         RenderSetup rs;
         Setup(rs, sd, rd);
         auto t0 = std::chrono::steady_clock::now();
-        int spp = rd->spp;
+        int spp = rs.spp;
         // flat list of pixels
         std::vector<std::pair<int, int>> px;
         px.reserve(rs.nPixels);
@@ -1596,6 +1607,7 @@ static int RenderImpl(const pbr_scene_desc* sd, const pbr_render_desc* rd, float
             if (counters) tl_counters = &local;
             Halton sampler;
             sampler.init(&rs.tab, spp, rd->camera.width, rd->camera.height);
+            if (rs.sobol) sampler.sob = &rs.sob;
 #pragma omp for schedule(dynamic, 16)
             for (long i = 0; i < (long)px.size(); ++i) {
                 int x = px[i].first, y = px[i].second;
@@ -1639,7 +1651,8 @@ int oracle_li_pixel(const pbr_scene_desc* sd, const pbr_render_desc* rd, int x, 
         RenderSetup rs;
         Setup(rs, sd, rd);
         Halton sampler;
-        sampler.init(&rs.tab, rd->spp, rd->camera.width, rd->camera.height);
+        sampler.init(&rs.tab, rs.spp, rd->camera.width, rd->camera.height);
+        if (rs.sobol) sampler.sob = &rs.sob;
         sampler.StartPixel(x, y);
         sampler.SetSampleNumber(sample);
         Spec L = SampleLi(rs.ctx, rs.cam, sampler, x, y);
@@ -1662,6 +1675,29 @@ int oracle_halton(int width, int height, int spp, int n, const int32_t* q, float
         int64_t idx = h.GetIndexForSample(q[4 * i], q[4 * i + 1], q[4 * i + 2]);
         out[i] = h.SampleDimension(idx, q[4 * i + 3]);
     }
+    return 0;
+}
+
+int oracle_sobol(int width, int height, int n, const int32_t* q, const uint32_t* matrices, int dims, float* out,
+                 int64_t* index_out) {
+    try {
+        SobolO s;
+        s.init(matrices, dims, width, height);
+        for (int i = 0; i < n; ++i) {
+            int64_t idx = s.GetIndexForSample(q[4 * i], q[4 * i + 1], q[4 * i + 2]);
+            if (index_out) index_out[i] = idx;
+            out[i] = s.SampleDimension(idx, q[4 * i + 3], q[4 * i], q[4 * i + 1]);
+        }
+        return 0;
+    } catch (const std::exception&) {
+        return PBR_E_INVALID;
+    }
+}
+
+int oracle_sobol_matrices(int dims, uint32_t* out) {
+    std::vector<uint32_t> m;
+    SobolO::builtin(dims, &m);
+    std::memcpy(out, m.data(), m.size() * 4);
     return 0;
 }
 

@@ -36,6 +36,12 @@ int oracle_render_stats(const pbr_scene_desc* scene, const pbr_render_desc* desc
                         uint64_t* counters /* [4]: rays, node_visits, prim_tests, shading */);
 /* Halton SampleDimension for (px, py, sample, dim) quadruples, image bounds (0,0)-(w,h). */
 int oracle_halton(int width, int height, int spp, int n, const int32_t* px_py_s_dim, float* out);
+/* pbrt-v3 SobolSampler: index (SobolIntervalToIndex) and SampleDimension for (px, py, sample, dim)
+ * quadruples at raster (width, height); matrices in SobolMatrices32 layout, NULL → built-in. */
+int oracle_sobol(int width, int height, int n, const int32_t* px_py_s_dim, const uint32_t* matrices, int dims,
+                 float* out, int64_t* index_out);
+/* The built-in Sobol' generator matrices (dims × 52 uint32). */
+int oracle_sobol_matrices(int dims, uint32_t* out);
 /* Radical inverse permutation table for the first n_primes primes (RNG default seed). */
 int oracle_halton_perms(int n_primes, uint16_t* out, int* n_out);
 /* Camera rays (o.xyz, d.xyz) for raster positions pfilm (x,y). */

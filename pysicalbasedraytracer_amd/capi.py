@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 PBR_OK = 0
 PBR_E_INVALID = -1
@@ -144,6 +144,8 @@ class RenderDesc(C.Structure):
         ("outputs_on_device", C.c_int),
         ("stream", C.c_void_p),
         ("collect_stats", C.c_int),
+        ("sobol_matrices", C.POINTER(C.c_uint32)),
+        ("sobol_dims", C.c_int),
     ]
 
 
@@ -178,6 +180,7 @@ EXPORTS = {
     "pbr_hip_intersect": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
     "pbr_hip_abi_version": (C.c_int, []),
     "pbr_hip_build_info": (C.c_char_p, []),
+    "pbr_hip_sobol_matrices": (C.c_int, [C.c_int, C.POINTER(C.c_uint32)]),
 }
 
 PACKAGE_DIR = os.path.dirname(os.path.abspath(__file__))

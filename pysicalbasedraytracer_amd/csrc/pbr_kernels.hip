@@ -27,7 +27,8 @@ using namespace pbr;
 namespace {
 
 // ---------------------------------------------------------------- sampler (Sampler/Sampler.cpp)
-struct SState { uint32_t index; int dim; };
+// index: the GlobalSampler's intervalSampleIndex; px, py: the current pixel (Sobol dims 0/1 remap)
+struct SState { uint32_t index; int dim; int px, py; };
 
 __host__ __device__ __forceinline__ HaltonParams hparams(const DeviceSampler& s) {
     HaltonParams h;
@@ -53,8 +54,44 @@ __device__ void stage_halton_lds(const DeviceSampler& s) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) s_halton_perm[i] = s.perms[i];
 }
 
+// pbrt-v3 SobolSampler::SampleDimension (Sobol.cpp) over SobolSampleFloat (LowDiscrepancy.h):
+// XOR of the generator columns of the set index bits, v·2^-32 narrowed, dims 0/1 remapped into
+// the pixel.  Dimensions beyond the matrices read 0 (pbrt aborts there).
+__device__ __forceinline__ float sobol_dimension(const DeviceSampler& s, uint32_t index, int dim, int px, int py) {
+    if (dim >= s.nSobolDims) return 0.f;
+    const uint32_t* M = s.sobol + (size_t)dim * kSobolMatrixSize;
+    uint32_t v = 0;
+    for (int c = 0; index != 0; index >>= 1, ++c)
+        if (index & 1u) v ^= M[c];
+    float f = mn((float)v * 2.3283064365386963e-10f, kOneMinusEpsilon);
+    if (dim <= 1) {
+        f = f * (float)s.sobolRes;   // + sampleBounds.pMin[dim] == 0
+        f = clampf(f - (float)(dim == 0 ? px : py), 0.f, kOneMinusEpsilon);
+    }
+    return f;
+}
+// SobolIntervalToIndex (LowDiscrepancy.h) via the GF(2) tables of sobol_pixel_tables
+__device__ __forceinline__ uint32_t sobol_index(const DeviceSampler& s, int px, int py, uint32_t frame) {
+    const int m = s.sobolLog2Res;
+    if (m == 0) return 0;   // pbrt-v3 returns 0 here (a 1×1 raster repeats sample 0)
+    const uint32_t* T = s.sobolPix;
+    uint32_t delta = 0;
+    for (int k = 0; (frame >> k) != 0u; ++k)
+        if ((frame >> k) & 1u) delta ^= T[2 * m + k];
+    uint32_t b = (((uint32_t)px << m) | (uint32_t)py) ^ delta, j = 0;
+    for (int r = 0; b != 0; b >>= 1, ++r)
+        if (b & 1u) j ^= T[r];
+    return (frame << (2 * m)) | j;
+}
+// GlobalSampler::StartPixel / SetSampleNumber: the global index of sample s of pixel (x, y)
+__device__ __forceinline__ uint32_t sample_index(const DeviceSampler& smp, int x, int y, int s) {
+    if (smp.type == PBR_SAMPLER_SOBOL) return sobol_index(smp, x, y, (uint32_t)s);
+    return halton_pixel_offset(hparams(smp), x, y) + (uint32_t)s * (uint32_t)smp.stride;   // Halton.cpp:61-81
+}
+
 template <bool LDS = false>
-__device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int dim) {
+__device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int dim, int px = 0, int py = 0) {
+    if (s.type == PBR_SAMPLER_SOBOL) return sobol_dimension(s, index, dim, px, py);
     // HaltonSampler::SampleDimension (Halton.cpp:83-92)
     if (dim == 0) return radical_inverse_2(index >> s.baseExp0);
     if (dim == 1) return radical_inverse_b(3u, 0x55555555u, div_prime(index, (uint32_t)s.baseScale1, 0xffffffffu / (uint32_t)s.baseScale1));
@@ -70,12 +107,14 @@ __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32
 // GlobalSampler::Get1D/Get2D (Sampler.cpp:131-143): with no requested sample arrays
 // arrayStartDim == arrayEndDim == 5, so only a Get2D that would straddle dimension 5 is moved.
 template <bool LDS = false>
-__device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) { return sample_dimension<LDS>(s, st.index, st.dim++); }
+__device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) {
+    return sample_dimension<LDS>(s, st.index, st.dim++, st.px, st.py);
+}
 template <bool LDS = false>
 __device__ __forceinline__ void get2d(const DeviceSampler& s, SState& st, float* a, float* b) {
     if (st.dim == 4) st.dim = 5;
-    *a = sample_dimension<LDS>(s, st.index, st.dim);
-    *b = sample_dimension<LDS>(s, st.index, st.dim + 1);
+    *a = sample_dimension<LDS>(s, st.index, st.dim, st.px, st.py);
+    *b = sample_dimension<LDS>(s, st.index, st.dim + 1, st.px, st.py);
     st.dim += 2;
 }
 
@@ -476,9 +515,10 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
             pixel_xy(P, pixBase + lp, &x, &y);
             // GlobalSampler::StartPixel/SetSampleNumber (Sampler.cpp:97-130)
             SState st;
-            st.index = halton_pixel_offset(hparams(P.smp), x, y) +
-                       (uint32_t)s * (uint32_t)P.smp.stride;
+            st.index = sample_index(P.smp, x, y, s);
             st.dim = 0;
+            st.px = x;
+            st.py = y;
             // GetCameraSample (Sampler.cpp:10-21): pFilm, time, pLens
             float u0, u1, l0, l1;
             get2d(P.smp, st, &u0, &u1);
@@ -516,8 +556,8 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
 __global__ void k_sampler_values(DeviceSampler smp, HaltonParams hp, int n, const int32_t* q, float* out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint32_t idx = halton_pixel_offset(hp, q[4 * i], q[4 * i + 1]) + (uint32_t)q[4 * i + 2] * (uint32_t)hp.stride;
-    out[i] = sample_dimension(smp, idx, q[4 * i + 3]);
+    uint32_t idx = sample_index(smp, q[4 * i], q[4 * i + 1], q[4 * i + 2]);
+    out[i] = sample_dimension(smp, idx, q[4 * i + 3], q[4 * i], q[4 * i + 1]);
 }
 __global__ void k_camera_rays(DeviceCamera cam, int n, const float* pf, float* out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -578,6 +618,10 @@ struct pbr_hip_ctx {
     HaltonTables halton;
     DevBuf dNodes, dWide, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
+    DevBuf dSobol, dSobolPix;          // active Sobol matrices, pixel tables
+    std::vector<uint32_t> sobolBuiltin;
+    const uint32_t* sobolSrc = nullptr;  // what dSobol holds (user pointer or the built-in table)
+    int sobolSrcDims = 0, sobolPixM = -1;
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
     // wavefront queues and per-sample records (pbr_wavefront.h)
     DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
@@ -637,6 +681,47 @@ DeviceSampler device_sampler(pbr_hip_ctx* ctx, int type, int spp, int w, int h) 
     s.primeSums = (const uint32_t*)ctx->dPrimeSums.p;
     s.perms = (const uint16_t*)ctx->dPerms.p;
     return s;
+}
+
+// SobolSampler(spp, sampleBounds) (Sobol.h): resolution = RoundUpPow2(max(w, h)); matrices from
+// the caller (the reference's SobolMatrices32) or the built-in ones; GF(2) pixel tables per m.
+int prepare_sobol(pbr_hip_ctx* ctx, const uint32_t* user, int userDims, int w, int h, DeviceSampler* s) {
+    const uint32_t* src = user;
+    int dims = userDims;
+    if (!user) {
+        if (ctx->sobolBuiltin.empty()) build_sobol_matrices(1024, &ctx->sobolBuiltin);
+        src = ctx->sobolBuiltin.data();
+        dims = 1024;
+    }
+    if (dims < 2) return set_err(ctx, PBR_E_INVALID, "Sobol needs at least 2 dimensions of matrices");
+    if (src != ctx->sobolSrc || dims != ctx->sobolSrcDims) {
+        HIP_TRY(ctx->dSobol.ensure((size_t)dims * kSobolMatrixSize * 4));
+        HIP_TRY(hipMemcpyAsync(ctx->dSobol.p, src, (size_t)dims * kSobolMatrixSize * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        ctx->sobolSrc = src;
+        ctx->sobolSrcDims = dims;
+        ctx->sobolPixM = -1;
+    }
+    int res = 1, m = 0;
+    while (res < std::max(w, h)) { res <<= 1; ++m; }
+    if (m != ctx->sobolPixM) {
+        std::vector<uint32_t> t;
+        try {
+            sobol_pixel_tables(src, m, &t);
+        } catch (const std::exception& e) {
+            return set_err(ctx, PBR_E_UNSUPPORTED, e.what());
+        }
+        if (t.empty()) t.push_back(0);
+        HIP_TRY(ctx->dSobolPix.upload(t, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        ctx->sobolPixM = m;
+    }
+    s->sobol = (const uint32_t*)ctx->dSobol.p;
+    s->nSobolDims = dims;
+    s->sobolLog2Res = m;
+    s->sobolRes = res;
+    s->sobolPix = (const uint32_t*)ctx->dSobolPix.p;
+    return PBR_OK;
 }
 
 int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
@@ -743,6 +828,14 @@ int pbr_hip_abi_version(void) { return PBR_HIP_ABI_VERSION; }
 #endif
 const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 wavefront+megakernel src " PBR_SRC_HASH; }
 
+int pbr_hip_sobol_matrices(int dims, uint32_t* out) {
+    if (dims < 1 || dims > 4096 || !out) return PBR_E_INVALID;
+    std::vector<uint32_t> m;
+    build_sobol_matrices(dims, &m);
+    std::memcpy(out, m.data(), m.size() * 4);
+    return PBR_OK;
+}
+
 int pbr_hip_create(int device, pbr_hip_ctx** out) {
     if (!out) return PBR_E_INVALID;
     *out = nullptr;
@@ -818,8 +911,19 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (d->max_depth < 0) return set_err(ctx, PBR_E_INVALID, "max_depth must be >= 0");
     if (d->integrator < PBR_INTEGRATOR_WHITTED || d->integrator > PBR_INTEGRATOR_VOLPATH)
         return set_err(ctx, PBR_E_INVALID, "unknown integrator");
-    if (d->sampler != PBR_SAMPLER_HALTON) return set_err(ctx, PBR_E_UNSUPPORTED, "only the Halton sampler is available in this build");
-    if ((long long)d->spp * (long long)31104 >= (1ll << 32)) return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
+    if (d->sampler != PBR_SAMPLER_HALTON && d->sampler != PBR_SAMPLER_SOBOL) return set_err(ctx, PBR_E_INVALID, "unknown sampler");
+    // SobolSampler rounds spp up to a power of two (GlobalSampler(RoundUpPow2(spp)), Sobol.h)
+    int spp = d->spp;
+    if (d->sampler == PBR_SAMPLER_SOBOL) {
+        int p2 = 1;
+        while (p2 < spp) p2 <<= 1;
+        spp = p2;
+        int res = 1, m = 0;
+        while (res < std::max(d->camera.width, d->camera.height)) { res <<= 1; ++m; }
+        if (((uint64_t)spp << (2 * m)) > (1ull << 32)) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol sample index beyond 32 bits");
+    } else if ((long long)spp * (long long)31104 >= (1ll << 32)) {
+        return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
+    }
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = d->stream ? (hipStream_t)d->stream : ctx->stream;
@@ -836,12 +940,16 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         if (rc) return rc;
     }
     P.S = device_scene(ctx);
-    P.smp = device_sampler(ctx, d->sampler, d->spp, d->camera.width, d->camera.height);
+    P.smp = device_sampler(ctx, d->sampler, spp, d->camera.width, d->camera.height);
+    if (d->sampler == PBR_SAMPLER_SOBOL) {
+        int rc = prepare_sobol(ctx, d->sobol_matrices, d->sobol_dims, d->camera.width, d->camera.height, &P.smp);
+        if (rc) return rc;
+    }
     P.integrator = d->integrator;
     P.maxDepth = d->max_depth;
     P.rrThreshold = d->rr_threshold;
-    P.spp = d->spp;
-    P.ppb = d->spp >= 256 ? 1 : 256 / d->spp;
+    P.spp = spp;
+    P.ppb = spp >= 256 ? 1 : 256 / spp;
     // tiles
     std::vector<int32_t> tiles;
     std::vector<long long> starts;
@@ -924,7 +1032,7 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         stats->kernel_ms = ms;
         stats->film_ms = 0;
         stats->seconds = std::chrono::duration<double>(t1 - t0).count();
-        stats->samples = (uint64_t)npx * (uint64_t)d->spp;
+        stats->samples = (uint64_t)npx * (uint64_t)spp;
         stats->rays = hs[0];
         stats->node_visits = hs[1];
         stats->prim_tests = hs[2];
@@ -949,9 +1057,13 @@ int pbr_hip_get_bvh(pbr_hip_ctx* ctx, void* nodes_out, int* n_nodes, int32_t* pr
 
 int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height, int spp, int n, const int32_t* q, float* out) {
     if (!ctx || !q || !out || n < 0 || width <= 0 || height <= 0) return PBR_E_INVALID;
-    if (sampler != PBR_SAMPLER_HALTON) return set_err(ctx, PBR_E_UNSUPPORTED, "only Halton");
+    if (sampler != PBR_SAMPLER_HALTON && sampler != PBR_SAMPLER_SOBOL) return set_err(ctx, PBR_E_INVALID, "unknown sampler");
     HIP_TRY(hipSetDevice(ctx->device));
     DeviceSampler s = device_sampler(ctx, sampler, spp, width, height);
+    if (sampler == PBR_SAMPLER_SOBOL) {
+        int rc = prepare_sobol(ctx, nullptr, 0, width, height, &s);
+        if (rc) return rc;
+    }
     HaltonParams hp = hparams(s);
     HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 16));
     HIP_TRY(ctx->dScratchOut.ensure((size_t)n * 4));

@@ -92,6 +92,7 @@ struct DeviceSampler {
     int nSobolDims;
     int sobolLog2Res;              // log2 of the power-of-two resolution
     int sobolRes;
+    const uint32_t* sobolPix;      // sobol_pixel_tables: T_low^-1 columns [2m], T_high columns
     int ldsDims;                   // Halton dimensions a kernel may stage in LDS (<= 64)
 };
 

@@ -647,4 +647,98 @@ void halton_params(int resX, int resY, DeviceSampler* s) {   // HaltonSampler ct
     s->ratio1 = s->stride / scale[1];
 }
 
+// ---------------------------------------------------------------- Sobol (pbrt-v3 SobolSampler)
+// Built-in generator matrices: column c of dimension d is the direction number v_{c+1} of a
+// Sobol' sequence.  Dimension 0 is van der Corput, dimension 1 the polynomial x + 1 (both equal to
+// the reference's SobolMatrices32 rows); dimensions >= 2 use the primitive polynomials of degree
+// 2, 3, ... in increasing coefficient order with all initial direction numbers m_k = 1.
+namespace {
+bool gf2_primitive(uint32_t poly, int deg) {   // poly includes the x^deg and 1 terms
+    const uint64_t order = (1ull << deg) - 1;
+    auto mulmod = [&](uint32_t a, uint32_t b) {
+        uint32_t r = 0;
+        for (int i = 0; i < deg; ++i) {
+            if (b & (1u << i)) r ^= a;
+            a <<= 1;
+            if (a & (1u << deg)) a ^= poly;
+        }
+        return r;
+    };
+    auto powx = [&](uint64_t e) {
+        uint32_t r = 1, b = 2 % (1u << deg);
+        if (deg == 1) b = 2 ^ poly;
+        while (e) { if (e & 1) r = mulmod(r, b); b = mulmod(b, b); e >>= 1; }
+        return r;
+    };
+    if (powx(order) != 1) return false;
+    uint64_t n = order;
+    for (uint64_t q = 2; q * q <= n; ++q) {
+        if (n % q) continue;
+        if (powx(order / q) == 1) return false;
+        while (n % q == 0) n /= q;
+    }
+    if (n > 1 && powx(order / n) == 1) return false;
+    return true;
+}
+}  // namespace
+
+void build_sobol_matrices(int nDims, std::vector<uint32_t>* out) {
+    out->assign((size_t)nDims * kSobolMatrixSize, 0u);
+    uint32_t* M = out->data();
+    for (int c = 0; c < 32 && nDims > 0; ++c) M[c] = 0x80000000u >> c;
+    int d = 1;
+    for (int deg = 1; d < nDims && deg < 31; ++deg) {
+        for (uint32_t a = 0; a < (1u << (deg - 1)) && d < nDims; ++a) {
+            uint32_t poly = (1u << deg) | (a << 1) | 1u;
+            if (!gf2_primitive(poly, deg)) continue;
+            uint64_t m[kSobolMatrixSize + 1];
+            for (int k = 1; k <= kSobolMatrixSize; ++k) {
+                if (k <= deg) { m[k] = 1; continue; }
+                uint64_t v = m[k - deg] ^ (m[k - deg] << deg);
+                for (int i = 1; i < deg; ++i)
+                    if ((a >> (deg - 1 - i)) & 1u) v ^= m[k - i] << i;
+                m[k] = v;
+            }
+            // 32-bit columns of v_k = m_k / 2^k (index bits >= 32 keep v_k's top 32 bits)
+            for (int c = 0; c < kSobolMatrixSize; ++c)
+                M[(size_t)d * kSobolMatrixSize + c] = (uint32_t)(c < 32 ? m[c + 1] << (31 - c) : m[c + 1] >> (c - 31));
+            ++d;
+        }
+    }
+}
+
+// SobolIntervalToIndex at resolution 2^m, restated as a GF(2) solve: the top m bits of
+// dimensions 0 and 1 of sample index i are T·i; with i = (frame << 2m) | j the low block of T is
+// invertible (the first two dimensions form a (0,2)-sequence), so j = T_low^-1 (p ^ T_high·frame)
+// with p = (px << m) | py.  out = T_low^-1 columns [2m], then T_high columns [32 - 2m].
+void sobol_pixel_tables(const uint32_t* mats, int m, std::vector<uint32_t>* out) {
+    out->clear();
+    if (m <= 0) return;
+    if (2 * m > 32) fail("Sobol resolution too large");
+    const int n = 2 * m;
+    auto col = [&](int c) -> uint32_t {   // the 2m-bit image of index bit c
+        uint32_t x = mats[c] >> (32 - m), y = mats[kSobolMatrixSize + c] >> (32 - m);
+        return (x << m) | y;
+    };
+    // Gauss-Jordan on [T_low | I] by columns: rows are bit positions
+    std::vector<uint32_t> A(n), inv(n);
+    for (int c = 0; c < n; ++c) { A[c] = col(c); inv[c] = 1u << c; }   // column c of T_low and of I
+    // solve via column operations: reduce A's columns to the unit vectors
+    for (int r = 0; r < n; ++r) {
+        int piv = -1;
+        for (int c = r; c < n; ++c)
+            if ((A[c] >> r) & 1u) { piv = c; break; }
+        if (piv < 0) fail("Sobol dimensions 0/1 are not a (0,2)-sequence");
+        std::swap(A[r], A[piv]);
+        std::swap(inv[r], inv[piv]);
+        for (int c = 0; c < n; ++c)
+            if (c != r && ((A[c] >> r) & 1u)) { A[c] ^= A[r]; inv[c] ^= inv[r]; }
+    }
+    // now T_low · inv[r] (as a combination of index bits) = unit vector e_r: inv[r] is the index
+    // bit pattern that produces pixel bit r
+    out->resize(32);
+    for (int r = 0; r < n; ++r) (*out)[r] = inv[r];
+    for (int k = 0; k < 32 - n; ++k) (*out)[n + k] = col(n + k);
+}
+
 }  // namespace pbr

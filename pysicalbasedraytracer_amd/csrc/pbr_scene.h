@@ -58,4 +58,10 @@ struct HaltonTables {
 void build_halton_tables(int nPrimes, HaltonTables* t);
 void halton_params(int resX, int resY, DeviceSampler* s);
 
+// Sobol (pbrt-v3 SobolSampler): built-in generator matrices [nDims][kSobolMatrixSize] and the
+// pixel → sample-index tables for resolution 2^m (see pbr_scene.cpp).
+constexpr int kSobolMatrixSize = 52;
+void build_sobol_matrices(int nDims, std::vector<uint32_t>* out);
+void sobol_pixel_tables(const uint32_t* mats, int m, std::vector<uint32_t>* out);
+
 }  // namespace pbr

@@ -103,8 +103,10 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
     int x, y;
     pixel_xy(P, W.chunkPix0 + lp, &x, &y);
     SState st;
-    st.index = halton_pixel_offset(hparams(P.smp), x, y) + (uint32_t)s * (uint32_t)P.smp.stride;
+    st.index = sample_index(P.smp, x, y, s);
     st.dim = 0;
+    st.px = x;
+    st.py = y;
     float u0, u1, l0, l1;
     get2d(P.smp, st, &u0, &u1);
     get1d(P.smp, st);
@@ -207,6 +209,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                     SState st;
                     st.index = W.sampleIndex[id];
                     st.dim = dim;
+                    st.px = st.py = 0;   // dims >= 2 only past the camera
                     {   // the single light (WhittedIntegrator.cpp:39-54)
                         float a, b;
                         get2d<true>(P.smp, st, &a, &b);

@@ -381,9 +381,16 @@ def camera(width, height, eye, look, up=(0.0, 1.0, 0.0), fov=90.0):
 
 
 def render_desc(cam, integrator, spp, max_depth, rr_threshold=1.0, light_strategy=capi.LIGHTS_UNIFORM,
-                sampler=capi.SAMPLER_HALTON, tiles=None):
+                sampler=capi.SAMPLER_HALTON, tiles=None, sobol_matrices=None):
+    """sobol_matrices: optional uint32 array in SobolMatrices32 layout ([dims][52]); None → the
+    library's built-in matrices."""
     d = capi.RenderDesc(integrator=integrator, max_depth=max_depth, rr_threshold=rr_threshold,
                         light_strategy=light_strategy, sampler=sampler, spp=spp, camera=cam)
+    if sobol_matrices is not None:
+        arr = np.ascontiguousarray(sobol_matrices, dtype=np.uint32)
+        d.sobol_matrices = arr.ctypes.data_as(C.POINTER(C.c_uint32))
+        d.sobol_dims = arr.size // 52
+        d._sobol_keep = arr
     if tiles:
         arr = (capi.Tile * len(tiles))(*[capi.Tile(*t) for t in tiles])
         d.n_tiles = len(tiles)
@@ -435,7 +442,7 @@ def config_c3(width=1920, height=1080, spp=256, mesh=None):
     Pl, Il = quad(2.45, 1.4, flip=True)
     s.area_light_mesh(Pl, Il, (5.0, 5.0, 5.0), white, n_samples=5)
     cam = camera(width, height, (0.0, 0.55, 2.6), (0.0, -0.25, 0.0))
-    return s, render_desc(cam, capi.INTEGRATOR_PATH, spp, 8, rr_threshold=0.8)
+    return s, render_desc(cam, capi.INTEGRATOR_PATH, spp, 8, rr_threshold=0.8, sampler=capi.SAMPLER_SOBOL)
 
 
 def config_c4(width=3840, height=2160, spp=1024, mesh=None):

@@ -31,6 +31,9 @@ def load():
     lib.oracle_render_stats.argtypes = [P(capi.SceneDesc), P(capi.RenderDesc), C.c_int, P(C.c_uint64)]
     lib.oracle_halton.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_int32), P(C.c_float)]
     lib.oracle_halton_perms.argtypes = [C.c_int, P(C.c_uint16), P(C.c_int)]
+    lib.oracle_sobol.argtypes = [C.c_int, C.c_int, C.c_int, P(C.c_int32), P(C.c_uint32), C.c_int, P(C.c_float),
+                                 P(C.c_int64)]
+    lib.oracle_sobol_matrices.argtypes = [C.c_int, P(C.c_uint32)]
     lib.oracle_camera_rays.argtypes = [P(capi.CameraDesc), C.c_int, P(C.c_float), P(C.c_float)]
     lib.oracle_build_bvh.argtypes = [P(capi.SceneDesc), C.c_void_p, P(C.c_int), P(C.c_int32), P(C.c_int)]
     lib.oracle_intersect.argtypes = [P(capi.SceneDesc), C.c_int, P(C.c_float), P(C.c_float), C.c_int]
@@ -72,6 +75,26 @@ def halton(width, height, spp, queries):
     q = np.ascontiguousarray(queries, dtype=np.int32).reshape(-1, 4)
     out = np.empty(q.shape[0], dtype=np.float32)
     assert lib.oracle_halton(width, height, spp, q.shape[0], capi.iptr(q), capi.fptr(out)) == 0
+    return out
+
+
+def sobol(width, height, queries, matrices=None):
+    """(values, indices) of the Sobol sampler for (px, py, sample, dim) queries."""
+    q = np.ascontiguousarray(queries, dtype=np.int32).reshape(-1, 4)
+    out = np.empty(q.shape[0], np.float32)
+    idx = np.empty(q.shape[0], np.int64)
+    m = None if matrices is None else np.ascontiguousarray(matrices, dtype=np.uint32)
+    rc = load().oracle_sobol(width, height, q.shape[0], q.ctypes.data_as(C.POINTER(C.c_int32)),
+                             None if m is None else m.ctypes.data_as(C.POINTER(C.c_uint32)),
+                             0 if m is None else m.size // 52, out.ctypes.data_as(C.POINTER(C.c_float)),
+                             idx.ctypes.data_as(C.POINTER(C.c_int64)))
+    assert rc == 0
+    return out, idx
+
+
+def sobol_matrices(dims):
+    out = np.empty(dims * 52, np.uint32)
+    assert load().oracle_sobol_matrices(dims, out.ctypes.data_as(C.POINTER(C.c_uint32))) == 0
     return out
 
 

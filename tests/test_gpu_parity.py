@@ -220,3 +220,49 @@ def test_wavefront_equals_megakernel(hip, monkeypatch):
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32))
     assert np.array_equal(wf8, mk8)
+
+
+SOBOL = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "sobol_kats.json")))
+
+
+def test_sobol_kats_on_device(hip):
+    """Sample index + dims 0/1 of the reference-table fixture (32-bit index cases), on the device."""
+    for c in SOBOL["cases"]:
+        (w, h), (px, py), s = c["raster"], c["pixel"], c["sample"]
+        if c["index"] >= 2 ** 32:
+            continue
+        v = hip.sampler_values(w, h, 1, [(px, py, s, 0), (px, py, s, 1)], sampler=capi.SAMPLER_SOBOL)
+        assert ["%08x" % u for u in v.view(np.uint32)] == [c["dim0"], c["dim1"]], c
+
+
+def test_sobol_random_queries_bit_exact(hip):
+    rng = np.random.default_rng(5)
+    for (w, h, spp) in [(1920, 1080, 256), (256, 256, 16), (100, 37, 8), (1, 1, 4)]:
+        q = np.stack([rng.integers(0, w, 4000), rng.integers(0, h, 4000), rng.integers(0, spp, 4000),
+                      rng.integers(0, 1024, 4000)], axis=1).astype(np.int32)
+        g = hip.sampler_values(w, h, spp, q, sampler=capi.SAMPLER_SOBOL)
+        c, _ = O.sobol(w, h, q)
+        assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+
+
+def test_c3_path_halton(hip):
+    s, rd = scenes.config_c3(96, 54, 8, mesh=small_dragon(64))
+    rd2 = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                             capi.SAMPLER_HALTON)
+    render_pair(hip, s, rd2)
+
+
+def test_sobol_caller_matrices_and_pow2_spp(hip):
+    """Matrices passed through the ABI (here: the built-in table with dimensions >= 2 replaced by
+    seeded random ones) drive both sides; a non-power-of-two spp is rounded up (6 → 8)."""
+    rng = np.random.default_rng(11)
+    m = O.sobol_matrices(128)
+    m[104:] = rng.integers(0, 2 ** 32, m.size - 104, dtype=np.uint64).astype(np.uint32)
+    s, rd = scenes.config_c3(64, 40, 6, mesh=small_dragon(40))
+    rd2 = scenes.render_desc(rd.camera, rd.integrator, 6, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                             capi.SAMPLER_SOBOL, sobol_matrices=m)
+    hip.upload(s)
+    g, g8, st = hip.render(rd2)
+    c, c8, _ = O.render(s, rd2)
+    compare(g, c, g8, c8)
+    assert st.samples == 64 * 40 * 8

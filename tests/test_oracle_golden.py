@@ -126,3 +126,39 @@ def test_watertight_triangle_edge_tie_later_wins():
     # tMax equal to the hit distance is still a hit
     tie = O.triangle_test(tri, np.array([0.25, 0.25, 1, 0, 0, -1, 1.0], np.float32))
     assert tie[0] == 1
+
+
+SOBOL = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "sobol_kats.json")))
+
+
+def test_sobol_index_and_pixel_dims_bit_exact():
+    """pbrt-v3 SobolIntervalToIndex + SampleDimension dims 0/1 as evaluated with the reference's own
+    VdCSobolMatrices / SobolMatrices32 (tests/golden/make_sobol_kats.py), reproduced by the
+    oracle's GF(2) solve at five rasters including 1×1 (index 0) and 3840×2160."""
+    for c in SOBOL["cases"]:
+        (w, h), (px, py), s = c["raster"], c["pixel"], c["sample"]
+        v, idx = O.sobol(w, h, [(px, py, s, 0), (px, py, s, 1)])
+        assert int(idx[0]) == c["index"], c
+        assert ["%08x" % u for u in v.view(np.uint32)] == [c["dim0"], c["dim1"]], c
+
+
+def test_sobol_builtin_dims01_are_the_references():
+    """The built-in matrices' dimensions 0 and 1 (all 52 columns) hash to the reference's
+    SobolMatrices32 rows; the device library's host builder produces the oracle's table."""
+    import ctypes as C
+    import hashlib
+    m = O.sobol_matrices(1024)
+    assert hashlib.sha256(m[:104].tobytes()).hexdigest() == SOBOL["dims01_sha256"]
+    d = np.empty(1024 * 52, np.uint32)
+    assert capi.load_library().pbr_hip_sobol_matrices(1024, d.ctypes.data_as(C.POINTER(C.c_uint32))) == 0
+    assert np.array_equal(d, m)
+
+
+def test_sobol_samples_land_in_their_pixel():
+    """Every sample's dims 0/1 offsets lie in [0, 1): the interval→index mapping is a bijection per pixel."""
+    rng = np.random.default_rng(3)
+    q = [(int(rng.integers(300)), int(rng.integers(200)), s, d) for _ in range(40) for s in range(16) for d in (0, 1)]
+    v, idx = O.sobol(300, 200, q)
+    assert np.all((v >= 0) & (v < 1))
+    # distinct samples of one pixel have distinct indices with the sample number in the high bits
+    assert np.all(idx.reshape(-1, 16, 2)[:, :, 0] >> 18 == np.arange(16))
