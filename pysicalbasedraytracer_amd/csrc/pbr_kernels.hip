@@ -812,7 +812,8 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gstride, blk, 0, s, W);
             else hipLaunchKernelGGL(k_wf_extend<0>, gstride, blk, 0, s, W);
         }
-        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + 3) / 4), blk, 0, s, W);
+        const int pb = finish_pixels(spp);
+        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + pb - 1) / pb), blk, 0, s, W);
     }
     HIP_TRY(hipGetLastError());
     return PBR_OK;

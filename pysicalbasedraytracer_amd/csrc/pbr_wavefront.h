@@ -317,43 +317,59 @@ __global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
     }
 }
 
-// Fold the recursion and run the film: one wave per pixel, lane = sample (coalesced record reads),
-// then lanes 0-2 each add one channel of the 64 folded values in sample order (the reference's
-// colObj += Li order; Spectrum addition is per channel).
+// Fold the recursion and run the film.  A workgroup takes finishPixels() whole pixels (<= 2048
+// samples): one thread per sample folds L_k = A_k + ((F_k·L_{k+1})·c_k)/pdf_k deepest-first
+// (coalesced record reads) into LDS laid out [pixel][channel][sample] with a pitch of spp + 1
+// (conflict-free), then one thread per (pixel, channel) adds that pixel's samples in sample order
+// — the reference's colObj += Li order; Spectrum addition is per channel — and one thread per
+// pixel runs the film.
+constexpr int kFinishSamples = 2048;
+__host__ __device__ inline int finish_pixels(int spp) {
+    int pb = kFinishSamples / spp;
+    return pb < 1 ? 1 : (pb > 64 ? 64 : pb);
+}
 template <int DUMMY>
 __global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
-    __shared__ float lds[4][64 * 3];
+    __shared__ float lds[3 * (kFinishSamples + 64)];
+    __shared__ float sum[64 * 3];
     const KParams& P = W.P;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int lp = blockIdx.x * 4 + wave;
-    if (lp >= W.chunkPix) return;          // wave-uniform
-    float accC = 0.0f;   // lane c < 3: channel c of the pixel sum
-    for (int base = 0; base < P.spp; base += 64) {
-        int s = base + lane;
-        rgb L = sp(0.f);
-        if (s < P.spp) {
-            int id = lp * P.spp + s;
-            int dpt = W.depthOf[id];
+    const int spp = P.spp, pitch = min(spp, kFinishSamples) + 1;
+    const int pb = finish_pixels(spp);
+    const int lp0 = blockIdx.x * pb;
+    const int npx = min(pb, W.chunkPix - lp0);
+    // spp > kFinishSamples: one pixel per block, folded and summed in slices of kFinishSamples
+    const int slice = min(spp, kFinishSamples);
+    float acc = 0.f;   // thread t < 3·npx: channel t%3 of pixel t/3
+    for (int s0 = 0; s0 < spp; s0 += slice) {
+        const int ns = npx * min(slice, spp - s0);
+        for (int t = threadIdx.x; t < ns; t += blockDim.x) {
+            const int p = spp <= kFinishSamples ? t / spp : 0, k = spp <= kFinishSamples ? t - p * spp : s0 + t;
+            const int id = (lp0 + p) * spp + k;
+            const int dpt = W.depthOf[id];
             float4 a = W.recA[(size_t)dpt * W.cap + id];
-            L = sp3(a.x, a.y, a.z);
+            rgb L = sp3(a.x, a.y, a.z);
             if (a.w != 0.f) L = L + sp(0.f);
-            for (int k = dpt - 1; k >= 0; --k) {
-                size_t ri = (size_t)k * W.cap + id;
+            for (int lv = dpt - 1; lv >= 0; --lv) {
+                size_t ri = (size_t)lv * W.cap + id;
                 float4 A = W.recA[ri], F = W.recF[ri];
                 float pdf = W.recP[ri];
                 L = sp3(A.x, A.y, A.z) + sp3(F.x, F.y, F.z) * L * F.w / pdf;
             }
+            const int kk = k - s0;
+            lds[(p * 3 + 0) * pitch + kk] = L.r;
+            lds[(p * 3 + 1) * pitch + kk] = L.g;
+            lds[(p * 3 + 2) * pitch + kk] = L.b;
         }
-        lds[wave][3 * lane] = L.r; lds[wave][3 * lane + 1] = L.g; lds[wave][3 * lane + 2] = L.b;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (lane < 3) {
-            int cnt = P.spp - base < 64 ? P.spp - base : 64;
-            for (int k = 0; k < cnt; ++k) accC = accC + lds[wave][3 * k + lane];
+        __syncthreads();
+        if ((int)threadIdx.x < 3 * npx) {
+            const int n = min(slice, spp - s0);
+            const float* row = lds + threadIdx.x * pitch;
+            for (int k = 0; k < n; ++k) acc = acc + row[k];
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __syncthreads();
     }
-    float r = __shfl(accC, 0), g = __shfl(accC, 1), b = __shfl(accC, 2);
-    if (lane == 0) film_out(P, W.chunkPix0 + lp, sp3(r, g, b));
+    if ((int)threadIdx.x < 3 * npx) sum[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < npx)
+        film_out(P, W.chunkPix0 + lp0 + threadIdx.x, sp3(sum[3 * threadIdx.x], sum[3 * threadIdx.x + 1], sum[3 * threadIdx.x + 2]));
 }
