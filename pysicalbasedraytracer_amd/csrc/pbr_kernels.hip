@@ -740,7 +740,11 @@ int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
 // Wavefront Whitted: chunks of ~2^23 samples, per level shade → shadow → extend (pbr_wavefront.h).
 int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const int spp = P.spp;
-    long long chunkPix = std::max(1LL, (1LL << 23) / spp);
+    // samples per chunk: queue + record memory ≈ 370 B per sample at depth 5 (12 GB at 2^25);
+    // measured on C2: 2^23 29.4 ms, 2^24 28.1, 2^25 26.6, 2^27 (whole frame) 26.6
+    int chunkLog2 = 25;
+    if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
+    long long chunkPix = std::max(1LL, (1LL << chunkLog2) / spp);
     if (chunkPix > P.nPixels) chunkPix = P.nPixels;
     const size_t cap = (size_t)chunkPix * spp;
     // segment capacity: a shade workgroup processes at most ceil(cap / (kWfBlocks·256)) rounds of 256
@@ -786,6 +790,18 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         return q;
     };
     const dim3 blk(256), gstride(kWfBlocks);
+    // The queue consumers (extend, shadow) run exactly one resident wave of workgroups: a grid of
+    // kWfBlocks would leave a partial second round (2048 = 1.33 × the 1536 resident at 6/CU).
+    auto resident = [&](const void* fn) {
+        int perCU = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, fn, 256, 0) != hipSuccess || perCU <= 0) perCU = 4;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
+        return dim3((unsigned)(perCU * cus));
+    };
+    const char* ePers = getenv("PBR_RESIDENT_GRID");
+    const bool pers = !(ePers && ePers[0] == '0');
+    const dim3 gShadow = pers ? resident(shortStack ? (const void*)k_wf_shadow<kShortStack> : (const void*)k_wf_shadow<0>) : gstride;
+    const dim3 gExtend = pers ? resident(shortStack ? (const void*)k_wf_extend<kShortStack> : (const void*)k_wf_extend<0>) : gstride;
     for (long long p0 = 0; p0 < P.nPixels; p0 += chunkPix) {
         W.chunkPix0 = p0;
         W.chunkPix = (int)std::min<long long>(chunkPix, P.nPixels - p0);
@@ -804,13 +820,13 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, s, W, l0);
             else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, s, W, l0);
             else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, s, W, l0);
-            if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gstride, blk, 0, s, W);
-            else hipLaunchKernelGGL(k_wf_shadow<0>, gstride, blk, 0, s, W);
+            if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, s, W);
+            else hipLaunchKernelGGL(k_wf_shadow<0>, gShadow, blk, 0, s, W);
             if (level + 1 == maxLevels) break;
             cur ^= 1;
             W.cur = queue(cur);
-            if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gstride, blk, 0, s, W);
-            else hipLaunchKernelGGL(k_wf_extend<0>, gstride, blk, 0, s, W);
+            if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, s, W);
+            else hipLaunchKernelGGL(k_wf_extend<0>, gExtend, blk, 0, s, W);
         }
         const int pb = finish_pixels(spp);
         hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + pb - 1) / pb), blk, 0, s, W);
