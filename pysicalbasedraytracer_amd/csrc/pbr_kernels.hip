@@ -771,6 +771,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     W.recA = (float4*)ctx->wRecA.p; W.recF = (float4*)ctx->wRecF.p; W.recP = (float*)ctx->wRecP.p;
     W.depthOf = (int*)ctx->wDepth.p;
     W.sampleIndex = (uint32_t*)ctx->wIndex.p;
+    W.initRecords = ctx->host.anyNoMaterial ? 1 : 0;
     // Halton dims one sample reaches: 5 camera + 4 per level (light 2D, SpecularReflect 2D)
     W.P.smp.ldsDims = std::min(kLdsDims, 5 + 4 * levels + 2);
     int lobes = 0;

@@ -227,9 +227,11 @@ PBR_HD uint32_t halton_pixel_offset(const HaltonParams& h, int px, int py) {
     for (int i = 0; i < h.baseExp0; ++i) { d0 = d0 * 2 + (v & 1u); v >>= 1; }
     uint32_t d1 = 0; v = (uint32_t)pm1;
     for (int i = 0; i < h.baseExp1; ++i) { uint32_t q = v / 3u; d1 = d1 * 3 + (v - q * 3u); v = q; }
-    uint64_t off = (uint64_t)d0 * (uint64_t)h.scaleRatio0 * (uint64_t)h.mult0 +
-                   (uint64_t)d1 * (uint64_t)h.scaleRatio1 * (uint64_t)h.mult1;
-    return (uint32_t)(off % (uint64_t)h.stride);
+    // d_i < baseScale_i, scaleRatio_i = stride / baseScale_i, mult_i < baseScale_i: each term is
+    // below baseScale_i · stride <= 243 · 31104, so the sum fits 32 bits and the reference's
+    // 64-bit arithmetic (Halton.cpp:61-81) gives the same value
+    uint32_t off = d0 * (uint32_t)h.scaleRatio0 * (uint32_t)h.mult0 + d1 * (uint32_t)h.scaleRatio1 * (uint32_t)h.mult1;
+    return off % (uint32_t)h.stride;
 }
 
 }  // namespace pbr

@@ -47,6 +47,7 @@ struct WfParams {
     int* depthOf;          // deepest level of each sample
     uint32_t* sampleIndex; // Halton global index of each sample (GlobalSampler::SetSampleNumber)
     int cap;               // record stride (>= nSamples)
+    int initRecords;       // some primitive has no material (Whitted's pass-through branch)
 };
 
 // LDS counter; the wave's lanes must be converged
@@ -117,10 +118,11 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
     bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(st.dim, 0)));
-    W.cur.id[q] = q;
-    W.sampleIndex[q] = st.index;
-    W.depthOf[q] = 0;                          // a sample dropped by the level cap reads black
-    W.recA[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    W.sampleIndex[q] = st.index;   // the level-0 queue is dense: queue slot == sample id
+    if (W.initRecords) {           // only pass-through levels can leave a sample without records
+        W.depthOf[q] = 0;          // a sample dropped by the level cap reads black
+        W.recA[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
 }
 
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
         rgb contrib = sp(0.f);
         if (active) {
             float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
-            id = W.cur.id[q];
+            id = level0 ? q : W.cur.id[q];
             int dd = __float_as_int(d.w);
             dim = dd & 0xffff;
             depth = dd >> 16;
