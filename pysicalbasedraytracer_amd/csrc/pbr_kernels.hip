@@ -551,6 +551,7 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
 }
 
 #include "pbr_wavefront.h"
+#include "pbr_wavefront_path.h"
 
 // ---------------------------------------------------------------- introspection kernels
 __global__ void k_sampler_values(DeviceSampler smp, HaltonParams hp, int n, const int32_t* q, float* out) {
@@ -625,6 +626,8 @@ struct pbr_hip_ctx {
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
     // wavefront queues and per-sample records (pbr_wavefront.h)
     DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
+    // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
+    DevBuf wpO, wpD, wpId, wdId, sL, sBeta, rA, rB, rBeta, rLi, rFlags, rLight;
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
 };
@@ -836,6 +839,101 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     return PBR_OK;
 }
 
+// Wavefront Path: per bounce shade → shadow → probe → resolve → extend (pbr_wavefront_path.h).
+int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
+    const int spp = P.spp;
+    int chunkLog2 = 25;   // ≈ 290 B of queues + state per sample: 9.7 GB per chunk
+    if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
+    long long chunkPix = std::max(1LL, (1LL << chunkLog2) / spp);
+    if (chunkPix > P.nPixels) chunkPix = P.nPixels;
+    const size_t cap = (size_t)chunkPix * spp;
+    const int segCap = (int)((cap + (size_t)kWfBlocks * 256 - 1) / ((size_t)kWfBlocks * 256) * 256);
+    const size_t qcap = std::max(cap, (size_t)segCap * kWfBlocks);
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(ctx->wqO[k].ensure(qcap * 16)); HIP_TRY(ctx->wqD[k].ensure(qcap * 16));
+        HIP_TRY(ctx->wqId[k].ensure(qcap * 4)); HIP_TRY(ctx->wqHit[k].ensure(qcap * 16));
+    }
+    HIP_TRY(ctx->wsO.ensure(qcap * 16)); HIP_TRY(ctx->wsD.ensure(qcap * 16)); HIP_TRY(ctx->wsId.ensure(qcap * 4));
+    HIP_TRY(ctx->wpO.ensure(qcap * 16)); HIP_TRY(ctx->wpD.ensure(qcap * 16)); HIP_TRY(ctx->wpId.ensure(qcap * 4));
+    HIP_TRY(ctx->wdId.ensure(qcap * 4));
+    HIP_TRY(ctx->sL.ensure(cap * 16)); HIP_TRY(ctx->sBeta.ensure(cap * 16));
+    HIP_TRY(ctx->rA.ensure(cap * 16)); HIP_TRY(ctx->rB.ensure(cap * 16)); HIP_TRY(ctx->rBeta.ensure(cap * 16));
+    HIP_TRY(ctx->rLi.ensure(cap * 16)); HIP_TRY(ctx->rFlags.ensure(cap * 4)); HIP_TRY(ctx->rLight.ensure(cap * 4));
+    HIP_TRY(ctx->wIndex.ensure(cap * 4));
+    HIP_TRY(ctx->wCnt.ensure(5 * kWfBlocks * sizeof(int)));
+    int* cnt = (int*)ctx->wCnt.p;   // segment counts: ray queues 0/1, shadow, probe, direct
+    WfpParams X;
+    std::memset(&X, 0, sizeof(X));
+    WfParams& W = X.W;
+    W.P = P;
+    W.so = (float4*)ctx->wsO.p; W.sd = (float4*)ctx->wsD.p; W.sid = (int*)ctx->wsId.p;
+    W.shadowSeg = cnt + 2 * kWfBlocks;
+    W.segCap = segCap;
+    W.sampleIndex = (uint32_t*)ctx->wIndex.p;
+    W.cap = (int)cap;
+    X.po = (float4*)ctx->wpO.p; X.pd = (float4*)ctx->wpD.p; X.pid = (int*)ctx->wpId.p;
+    X.probeSeg = cnt + 3 * kWfBlocks;
+    X.directId = (int*)ctx->wdId.p;
+    X.directSeg = cnt + 4 * kWfBlocks;
+    X.stL = (float4*)ctx->sL.p; X.stBeta = (float4*)ctx->sBeta.p;
+    X.dA = (float4*)ctx->rA.p; X.dB = (float4*)ctx->rB.p; X.dBeta = (float4*)ctx->rBeta.p; X.dLi = (float4*)ctx->rLi.p;
+    X.dFlags = (int*)ctx->rFlags.p; X.dLight = (int*)ctx->rLight.p;
+    HIP_TRY(hipMemsetAsync(X.dFlags, 0, cap * 4, s));
+    // Path: 5 camera dims + per bounce 1 + 2 + 2 (light) + 2 (BSDF) + 1 (RR)
+    W.P.smp.ldsDims = std::min(kLdsDims, 5 + 8 * std::max(1, P.maxDepth) + 2);
+    if (const char* e = getenv("PBR_HALTON_LDS")) if (e[0] == '0') W.P.smp.ldsDims = 0;
+    int lobes = 0;
+    for (const MatTemplate& m : ctx->host.materials)
+        for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
+    const bool simple = (lobes & ~kSimpleLobes) == 0;
+    const char* eMats = getenv("PBR_MATS_LDS");
+    const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
+    auto queue = [&](int k) {
+        WfQueue q;
+        q.o = (float4*)ctx->wqO[k].p; q.d = (float4*)ctx->wqD[k].p; q.id = (int*)ctx->wqId[k].p; q.hit = (float4*)ctx->wqHit[k].p;
+        q.segCount = cnt + k * kWfBlocks;
+        return q;
+    };
+    auto resident = [&](const void* fn) {
+        int perCU = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, fn, 256, 0) != hipSuccess || perCU <= 0) perCU = 4;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
+        return dim3((unsigned)(perCU * cus));
+    };
+    const dim3 blk(256), gshade(kWfBlocks);
+    const dim3 gShadow = resident((const void*)k_wfp_shadow<kShortStack>), gProbe = resident((const void*)k_wfp_probe<kShortStack>);
+    const dim3 gExtend = resident((const void*)k_wf_extend<kShortStack>), gResolve = resident((const void*)k_wfp_resolve);
+    const int maxLevels = std::max(1, P.maxDepth) + 1 + (ctx->host.anyNoMaterial ? 8 : 0);
+    for (long long p0 = 0; p0 < P.nPixels; p0 += chunkPix) {
+        W.chunkPix0 = p0;
+        W.chunkPix = (int)std::min<long long>(chunkPix, P.nPixels - p0);
+        W.nSamples = W.chunkPix * spp;
+        int cur = 0;
+        W.cur = queue(0);
+        hipLaunchKernelGGL(k_wfp_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, s, X);
+        for (int level = 0; level < maxLevels; ++level) {
+            W.cur = queue(cur);
+            W.next = queue(cur ^ 1);
+            const int l0 = level == 0 ? 1 : 0;
+            if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, s, X, l0);
+            else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, s, X, l0);
+            else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, s, X, l0);
+            else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, s, X, l0);
+            hipLaunchKernelGGL(k_wfp_shadow<kShortStack>, gShadow, blk, 0, s, X);
+            hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, s, X);
+            hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, s, X);
+            if (level + 1 == maxLevels) break;
+            cur ^= 1;
+            W.cur = queue(cur);
+            hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, s, W);
+        }
+        const int pb = finish_pixels(spp);
+        hipLaunchKernelGGL(k_wfp_finish, dim3((W.chunkPix + pb - 1) / pb), blk, 0, s, X);
+    }
+    HIP_TRY(hipGetLastError());
+    return PBR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1015,6 +1113,7 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         const char* wfEnv = getenv("PBR_WAVEFRONT");
         bool wavefront = d->integrator == PBR_INTEGRATOR_WHITTED && !st && ctx->host.lights.size() == 1 &&
                          d->max_depth <= kWfMaxDepth && !(wfEnv && wfEnv[0] == '0');
+        bool wavefrontPath = d->integrator == PBR_INTEGRATOR_PATH && !st && d->max_depth <= 120 && !(wfEnv && wfEnv[0] == '0');
         // waves per SIMD the megakernel is compiled for: trades VGPRs for scratch (PBR_OCC=1|2|4)
         int occ = 2;   // measured: 2 waves/SIMD beats 1 by 1.78x on C2 and ties 4
         if (const char* e = getenv("PBR_OCC")) occ = atoi(e);
@@ -1025,6 +1124,9 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     else hipLaunchKernelGGL((k_render<I, false, 1>), grid, block, 0, s, P);
         if (wavefront) {
             int rc = render_wavefront(ctx, P, s);
+            if (rc) return rc;
+        } else if (wavefrontPath) {
+            int rc = render_wavefront_path(ctx, P, s);
             if (rc) return rc;
         } else switch (d->integrator) {
         case PBR_INTEGRATOR_WHITTED: PBR_LAUNCH(PBR_INTEGRATOR_WHITTED) break;

@@ -1,0 +1,378 @@
+// pbr_wavefront_path.h — wavefront schedule for PathIntegrator::Li (PathIntegrator.cpp:32-110) with
+// UniformSampleOneLight / EstimateDirect (Integrator.cpp:46-177).  Included by pbr_kernels.hip
+// after pbr_wavefront.h (queues, segment scan, wave_push, the camera/extend kernels).
+//
+// Per bounce k:
+//   k_wfp_shade    emission (bounce 0 / after specular), BSDF, the one-light estimate's two
+//                  candidate terms — light sample (needs a shadow ray) and BSDF sample (needs a
+//                  probe ray) — and the continuation (BSDF sample, beta update, Russian roulette)
+//   k_wfp_shadow   any-hit for the light-sample rays → "visible" flag in the direct record
+//   k_wfp_probe    closest hit for the BSDF-sample rays → the radiance the sampled light shows there
+//   k_wfp_resolve  Ld = [A if visible] + [f·Li·weight/scatteringPdf]; L += beta · (Ld / pmf)
+//   k_wf_extend    closest hit for the continuation queue (shared with Whitted)
+// then k_wfp_finish sums each pixel's per-sample L in sample order and runs the film.
+//
+// L and beta live per sample; every L update happens in the reference's order (emission of
+// bounce k, direct light of bounce k, emission of bounce k+1, ...), so the per-sample radiance is
+// bit-identical to the recursive megakernel's.  Sampler dimensions travel in the ray queue.
+#pragma once
+
+constexpr int kWfpAPending = 1, kWfpBPending = 2, kWfpVisible = 4;
+
+struct WfpParams {
+    WfParams W;            // queues (cur/next rays, shadow), chunk geometry, sample index table
+    // probe queue (segmented): origin+tMax, dir, sample id
+    float4* po; float4* pd; int* pid; int* probeSeg;
+    int* directId; int* directSeg;   // samples with a pending direct-light estimate
+    float4* stL;           // L.rgb
+    float4* stBeta;        // beta.rgb, etaScale
+    float4* dA;            // light-sample term f·Li·w/lightPdf (if unoccluded), pmf
+    float4* dB;            // BSDF-sample f (× |cos|), weight
+    float4* dBeta;         // beta at the estimate, scatteringPdf
+    float4* dLi;           // probe result: Li at the BSDF-sampled direction
+    int* dFlags;           // kWfp* bits
+    int* dLight;           // light index of the estimate
+};
+
+__device__ __forceinline__ int pack_path(int dim, int bounces, bool specular) {
+    return (dim & 0xffff) | ((bounces & 0x7f) << 16) | (specular ? (1 << 23) : 0);
+}
+
+template <int SHORT>
+__global__ __launch_bounds__(256) void k_wfp_camera_extend(WfpParams X) {
+    WfParams& W = X.W;
+    const KParams& P = W.P;
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= W.nSamples) return;
+    int lp = q / P.spp, s = q - lp * P.spp;
+    int x, y;
+    pixel_xy(P, W.chunkPix0 + lp, &x, &y);
+    SState st;
+    st.index = sample_index(P.smp, x, y, s);
+    st.dim = 0;
+    st.px = x;
+    st.py = y;
+    float u0, u1, l0, l1;
+    get2d(P.smp, st, &u0, &u1);
+    get1d(P.smp, st);
+    get2d(P.smp, st, &l0, &l1);
+    Ray r = camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
+    HitRec h;
+    Counters c;
+    bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
+    W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
+    W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_path(st.dim, 0, false)));
+    W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
+    W.sampleIndex[q] = st.index;
+    X.stL[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    X.stBeta[q] = make_float4(1.f, 1.f, 1.f, 1.f);
+}
+
+// One bounce of PathIntegrator::Li for every queued ray.
+template <int LOBES, bool MATS_LDS, int OCC = (LOBES & ~kSimpleLobes) ? 2 : 3>
+__global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0) {
+    WfParams& W = X.W;
+    const KParams& P = W.P;
+    const DeviceScene& S = P.S;
+    stage_halton_lds(P.smp);
+    const MatTemplate* mats = S.materials;
+    if constexpr (MATS_LDS) {
+        constexpr int words = (int)(sizeof(MatTemplate) / 4);
+        const int n = 2 * S.nMaterials * words;
+        const uint32_t* src = (const uint32_t*)S.materials;
+        uint32_t* dst = (uint32_t*)s_mats;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+        mats = s_mats;
+    }
+    __shared__ int s_push[4];   // shadow, probe, direct, next
+    if (threadIdx.x < 4) s_push[threadIdx.x] = 0;
+    __syncthreads();
+    const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
+    const int stride = gridDim.x * blockDim.x;
+    const int nIter = (n + stride - 1) / stride;
+    const int base = blockIdx.x * W.segCap;
+    for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
+        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const bool active = i < n;
+        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
+        bool pushShadow = false, pushProbe = false, pushDirect = false, pushNext = false;
+        int id = 0, dim = 0, bounces = 0;
+        bool specularBounce = false;
+        Ray shadow, probe, cont;
+        if (active) {
+            float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
+            id = level0 ? q : W.cur.id[q];
+            const int dd = __float_as_int(d.w);
+            dim = dd & 0xffff;
+            bounces = (dd >> 16) & 0x7f;
+            specularBounce = (dd >> 23) & 1;
+            Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+            const int slot = __float_as_int(hr.x);
+            const bool found = slot >= 0;
+            float4 lv = X.stL[id], bv = X.stBeta[id];
+            rgb L = sp3(lv.x, lv.y, lv.z), beta = sp3(bv.x, bv.y, bv.z);
+            float etaScale = bv.w;
+            Isect isect;
+            if (found) {
+                int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
+                if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
+                else triangle_si(S, slot, ray, hr.y, hr.z, hr.w, flags, &isect);
+                isect.slot = slot;
+                isect.medIn = isect.medOut = -1;
+            }
+            if (bounces == 0 || specularBounce) {
+                if (found) L = L + beta * si_Le(S, isect, -ray.d);
+                else for (int k = 0; k < S.nInfinite; ++k) L = L + beta * light_Le(S, S.lights[S.infinite[k]], ray);
+            }
+            bool alive = found && bounces < P.maxDepth;
+            BSDF bsdf;
+            if (alive && !make_bsdf(S, mats, isect, true, &bsdf)) {
+                cont = spawn_ray(isect, ray.d);   // isect.SpawnRay(ray.d); bounces-- then ++: same bounce
+                pushNext = true;
+                alive = false;
+            } else if (alive) {
+                SState st;
+                st.index = W.sampleIndex[id];
+                st.dim = dim;
+                st.px = st.py = 0;
+                const f3 wo = isect.wo;
+                if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0 && S.nLights > 0) {
+                    // UniformSampleOneLight: light choice, then EstimateDirect's two strategies
+                    float pmf;
+                    const int li = sample_light(S, get1d<true>(P.smp, st), &pmf);
+                    if (pmf != 0) {
+                        float uL0, uL1, uS0, uS1;
+                        get2d<true>(P.smp, st, &uL0, &uL1);
+                        get2d<true>(P.smp, st, &uS0, &uS1);
+                        const DLight& light = S.lights[li];
+                        const bool delta = light.type == LT_POINT;
+                        const int flagsNS = BSDF_ALL & ~BSDF_SPECULAR;
+                        int dflags = 0;
+                        f3 wi = mk(0, 0, 0);
+                        float lightPdf = 0, scatteringPdf = 0;
+                        VisPt vis;
+                        rgb Li = sample_li(S, light, isect, uL0, uL1, &wi, &lightPdf, &vis);
+                        rgb A = sp(0.f);
+                        if (lightPdf > 0 && !black(Li)) {
+                            rgb f = bsdf_f<LOBES>(bsdf, wo, wi, flagsNS) * absdot(wi, isect.sn);
+                            scatteringPdf = bsdf_pdf<LOBES>(bsdf, wo, wi, flagsNS);
+                            if (!black(f)) {
+                                if (delta) A = f * Li / lightPdf;
+                                else {
+                                    float fp = 1 * lightPdf, gp = 1 * scatteringPdf;
+                                    float weight = (fp * fp) / (fp * fp + gp * gp);
+                                    A = f * Li * weight / lightPdf;
+                                }
+                                shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
+                                pushShadow = true;
+                                dflags |= kWfpAPending;
+                            }
+                        }
+                        rgb fB = sp(0.f);
+                        float weightB = 1.f;
+                        if (!delta) {
+                            int stype = 0;
+                            fB = bsdf_sample<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
+                            fB = fB * absdot(wi, isect.sn);
+                            const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
+                            if (!black(fB) && scatteringPdf > 0) {
+                                bool probeIt = true;
+                                if (!sampledSpecular) {
+                                    float lp = pdf_li(S, light, isect, wi);
+                                    if (lp == 0) probeIt = false;
+                                    else {
+                                        float fp = 1 * scatteringPdf, gp = 1 * lp;
+                                        weightB = (fp * fp) / (fp * fp + gp * gp);
+                                    }
+                                }
+                                if (probeIt) {
+                                    probe = spawn_ray(isect, wi);
+                                    pushProbe = true;
+                                    dflags |= kWfpBPending;
+                                }
+                            }
+                        }
+                        if (dflags) {
+                            X.dA[id] = make_float4(A.r, A.g, A.b, pmf);
+                            X.dB[id] = make_float4(fB.r, fB.g, fB.b, weightB);
+                            X.dBeta[id] = make_float4(beta.r, beta.g, beta.b, scatteringPdf);
+                            X.dFlags[id] = dflags;
+                            X.dLight[id] = li;
+                            pushDirect = true;
+                        }
+                    }
+                }
+                // BSDF sample for the path (PathIntegrator.cpp:80-105): wo is -ray.d here, not the
+                // normalised isect.wo the light estimate uses
+                const f3 woPath = -ray.d;
+                f3 wi = mk(0, 0, 0);
+                float pdf = 0;
+                int flags = 0;
+                float u0, u1;
+                get2d<true>(P.smp, st, &u0, &u1);
+                rgb f = bsdf_sample<LOBES>(bsdf, woPath, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
+                if (!(black(f) || pdf == 0.f)) {
+                    beta = beta * (f * absdot(wi, isect.sn) / pdf);
+                    specularBounce = (flags & BSDF_SPECULAR) != 0;
+                    if ((flags & BSDF_SPECULAR) && (flags & BSDF_TRANSMISSION)) {
+                        float eta = bsdf.mt->eta;
+                        etaScale *= (dot(woPath, isect.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                    }
+                    cont = spawn_ray(isect, wi);
+                    bool stop = false;
+                    rgb rrBeta = beta * etaScale;
+                    if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
+                        float qq = mx((float).05, 1 - maxval(rrBeta));
+                        if (get1d<true>(P.smp, st) < qq) stop = true;
+                        else beta = beta / (1 - qq);
+                    }
+                    if (!stop) {
+                        pushNext = true;
+                        bounces += 1;
+                    }
+                }
+                dim = st.dim;
+                X.stBeta[id] = make_float4(beta.r, beta.g, beta.b, etaScale);
+            }
+            X.stL[id] = make_float4(L.r, L.g, L.b, 0.f);
+        }
+        const int si = base + wave_push(&s_push[0], pushShadow);
+        if (pushShadow) {
+            W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
+            W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, 0.f);
+            W.sid[si] = id;
+        }
+        const int pi = base + wave_push(&s_push[1], pushProbe);
+        if (pushProbe) {
+            X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
+            X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
+            X.pid[pi] = id;
+        }
+        const int di = base + wave_push(&s_push[2], pushDirect);
+        if (pushDirect) X.directId[di] = id;
+        const int ni = base + wave_push(&s_push[3], pushNext);
+        if (pushNext) {
+            W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
+            W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_path(dim, bounces, specularBounce)));
+            W.next.id[ni] = id;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        W.shadowSeg[blockIdx.x] = s_push[0];
+        X.probeSeg[blockIdx.x] = s_push[1];
+        X.directSeg[blockIdx.x] = s_push[2];
+        W.next.segCount[blockIdx.x] = s_push[3];
+    }
+}
+
+// VisibilityTester::Unoccluded for the light-sample rays
+template <int SHORT>
+__global__ __launch_bounds__(256) void k_wfp_shadow(WfpParams X) {
+    WfParams& W = X.W;
+    const int n = seg_scan(W.shadowSeg);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int q = seg_pos(W.segCap, i);
+        float4 o = W.so[q], d = W.sd[q];
+        Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+        HitRec h;
+        Counters c;
+        if (!traverse<true, false, SHORT>(W.P.S, r, &h, &c)) {
+            const int id = W.sid[q];
+            X.dFlags[id] |= kWfpVisible;   // the only writer of this sample's record in this launch
+        }
+    }
+}
+
+// EstimateDirect's BSDF-sampled ray: closest hit; Li = the sampled light's emission if that is
+// what it hits (si.Le), light.Le(ray) if it escapes (Light::Le, F4 for non-infinite lights).
+template <int SHORT>
+__global__ __launch_bounds__(256) void k_wfp_probe(WfpParams X) {
+    WfParams& W = X.W;
+    const DeviceScene& S = W.P.S;
+    const int n = seg_scan(X.probeSeg);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int q = seg_pos(W.segCap, i);
+        float4 o = X.po[q], d = X.pd[q];
+        Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+        const int id = X.pid[q];
+        const int li = X.dLight[id];
+        HitRec h;
+        Counters c;
+        rgb Li2 = sp(0.f);
+        if (traverse<false, false, SHORT>(S, ray, &h, &c)) {
+            if (S.primInfo[h.slot].z == li) {
+                Isect lightIsect;
+                int flags = __float_as_int(S.triVerts[3 * (size_t)h.slot].w);
+                if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)h.slot].x)], ray, ray.tMax, &lightIsect);
+                else triangle_si(S, h.slot, ray, h.b0, h.b1, h.b2, flags, &lightIsect);
+                lightIsect.slot = h.slot;
+                Li2 = si_Le(S, lightIsect, -ray.d);
+            }
+        } else {
+            Li2 = light_Le(S, S.lights[li], ray);
+        }
+        X.dLi[id] = make_float4(Li2.r, Li2.g, Li2.b, 0.f);
+    }
+}
+
+// Ld = [A if the light sample is unoccluded] + [f·Li·weight/scatteringPdf if Li is not black];
+// L += beta · (Ld / pmf) — UniformSampleOneLight's division, then PathIntegrator's beta product.
+__global__ __launch_bounds__(256) void k_wfp_resolve(WfpParams X) {
+    WfParams& W = X.W;
+    const int n = seg_scan(X.directSeg);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int id = X.directId[seg_pos(W.segCap, i)];
+        const int fl = X.dFlags[id];
+        const float4 a = X.dA[id], bt = X.dBeta[id];
+        rgb Ld = sp(0.f);
+        if ((fl & kWfpAPending) && (fl & kWfpVisible)) Ld = Ld + sp3(a.x, a.y, a.z);
+        if (fl & kWfpBPending) {
+            const float4 li = X.dLi[id], b = X.dB[id];
+            const rgb Li2 = sp3(li.x, li.y, li.z);
+            if (!black(Li2)) Ld = Ld + sp3(b.x, b.y, b.z) * Li2 * b.w / bt.w;
+        }
+        const rgb beta = sp3(bt.x, bt.y, bt.z);
+        const rgb direct = beta * (Ld / a.w);
+        float4 L = X.stL[id];
+        L.x = L.x + direct.r; L.y = L.y + direct.g; L.z = L.z + direct.b;
+        X.stL[id] = L;
+        X.dFlags[id] = 0;
+    }
+}
+
+// Per-pixel in-order sum of the per-sample L (colObj += Li) and the film; layout as k_wf_finish.
+__global__ __launch_bounds__(256) void k_wfp_finish(WfpParams X) {
+    WfParams& W = X.W;
+    __shared__ float lds[3 * (kFinishSamples + 64)];
+    __shared__ float sum[64 * 3];
+    const KParams& P = W.P;
+    const int spp = P.spp, pitch = min(spp, kFinishSamples) + 1;
+    const int pb = finish_pixels(spp);
+    const int lp0 = blockIdx.x * pb;
+    const int npx = min(pb, W.chunkPix - lp0);
+    const int slice = min(spp, kFinishSamples);
+    float acc = 0.f;
+    for (int s0 = 0; s0 < spp; s0 += slice) {
+        const int ns = npx * min(slice, spp - s0);
+        for (int t = threadIdx.x; t < ns; t += blockDim.x) {
+            const int p = spp <= kFinishSamples ? t / spp : 0, k = spp <= kFinishSamples ? t - p * spp : s0 + t;
+            const float4 L = X.stL[(lp0 + p) * spp + k];
+            const int kk = k - s0;
+            lds[(p * 3 + 0) * pitch + kk] = L.x;
+            lds[(p * 3 + 1) * pitch + kk] = L.y;
+            lds[(p * 3 + 2) * pitch + kk] = L.z;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < 3 * npx) {
+            const int cnt = min(slice, spp - s0);
+            const float* row = lds + threadIdx.x * pitch;
+            for (int k = 0; k < cnt; ++k) acc = acc + row[k];
+        }
+        __syncthreads();
+    }
+    if ((int)threadIdx.x < 3 * npx) sum[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < npx)
+        film_out(P, W.chunkPix0 + lp0 + threadIdx.x, sp3(sum[3 * threadIdx.x], sum[3 * threadIdx.x + 1], sum[3 * threadIdx.x + 2]));
+}
