@@ -552,6 +552,7 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
 
 #include "pbr_wavefront.h"
 #include "pbr_wavefront_path.h"
+#include "pbr_wavefront_volpath.h"
 
 // ---------------------------------------------------------------- introspection kernels
 __global__ void k_sampler_values(DeviceSampler smp, HaltonParams hp, int n, const int32_t* q, float* out) {
@@ -628,6 +629,7 @@ struct pbr_hip_ctx {
     DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
     // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
     DevBuf wpO, wpD, wpId, wdId, sL, sBeta, rA, rB, rBeta, rLi, rFlags, rLight;
+    DevBuf wtO, wtD, wtP, wtE, wtN, wtId, rLiA, rTr, rWA;   // VolPath transmittance walk
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
 };
@@ -840,7 +842,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
 }
 
 // Wavefront Path: per bounce shade → shadow → probe → resolve → extend (pbr_wavefront_path.h).
-int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
+int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol) {
     const int spp = P.spp;
     int chunkLog2 = 25;   // ≈ 290 B of queues + state per sample: 9.7 GB per chunk
     if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
@@ -860,11 +862,21 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     HIP_TRY(ctx->rA.ensure(cap * 16)); HIP_TRY(ctx->rB.ensure(cap * 16)); HIP_TRY(ctx->rBeta.ensure(cap * 16));
     HIP_TRY(ctx->rLi.ensure(cap * 16)); HIP_TRY(ctx->rFlags.ensure(cap * 4)); HIP_TRY(ctx->rLight.ensure(cap * 4));
     HIP_TRY(ctx->wIndex.ensure(cap * 4));
-    HIP_TRY(ctx->wCnt.ensure(5 * kWfBlocks * sizeof(int)));
-    int* cnt = (int*)ctx->wCnt.p;   // segment counts: ray queues 0/1, shadow, probe, direct
-    WfpParams X;
-    std::memset(&X, 0, sizeof(X));
+    HIP_TRY(ctx->wCnt.ensure(6 * kWfBlocks * sizeof(int)));
+    int* cnt = (int*)ctx->wCnt.p;   // segment counts: ray queues 0/1, shadow, probe, direct, Tr walk
+    WfvParams V;
+    std::memset(&V, 0, sizeof(V));
+    WfpParams& X = V.X;
     WfParams& W = X.W;
+    if (vol) {
+        HIP_TRY(ctx->wtO.ensure(qcap * 16)); HIP_TRY(ctx->wtD.ensure(qcap * 16)); HIP_TRY(ctx->wtP.ensure(qcap * 16));
+        HIP_TRY(ctx->wtE.ensure(qcap * 16)); HIP_TRY(ctx->wtN.ensure(qcap * 16)); HIP_TRY(ctx->wtId.ensure(qcap * 4));
+        HIP_TRY(ctx->rLiA.ensure(cap * 16)); HIP_TRY(ctx->rTr.ensure(cap * 16)); HIP_TRY(ctx->rWA.ensure(cap * 4));
+        V.to = (float4*)ctx->wtO.p; V.td = (float4*)ctx->wtD.p; V.tp = (float4*)ctx->wtP.p;
+        V.te = (float4*)ctx->wtE.p; V.tn = (float4*)ctx->wtN.p; V.tid = (int*)ctx->wtId.p;
+        V.trSeg = cnt + 5 * kWfBlocks;
+        V.dLiA = (float4*)ctx->rLiA.p; V.dTr = (float4*)ctx->rTr.p; V.dWA = (float*)ctx->rWA.p;
+    }
     W.P = P;
     W.so = (float4*)ctx->wsO.p; W.sd = (float4*)ctx->wsD.p; W.sid = (int*)ctx->wsId.p;
     W.shadowSeg = cnt + 2 * kWfBlocks;
@@ -915,13 +927,23 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             W.cur = queue(cur);
             W.next = queue(cur ^ 1);
             const int l0 = level == 0 ? 1 : 0;
-            if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, s, X, l0);
-            else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, s, X, l0);
-            else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, s, X, l0);
-            else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, s, X, l0);
-            hipLaunchKernelGGL(k_wfp_shadow<kShortStack>, gShadow, blk, 0, s, X);
-            hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, s, X);
-            hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, s, X);
+            if (vol) {
+                if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, s, V, l0);
+                else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, s, V, l0);
+                else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, s, V, l0);
+                else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, s, V, l0);
+                hipLaunchKernelGGL(k_wfv_tr<kShortStack>, gShadow, blk, 0, s, V);
+                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, s, X);
+                hipLaunchKernelGGL(k_wfv_resolve, gResolve, blk, 0, s, V);
+            } else {
+                if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, s, X, l0);
+                else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, s, X, l0);
+                else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, s, X, l0);
+                else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, s, X, l0);
+                hipLaunchKernelGGL(k_wfp_shadow<kShortStack>, gShadow, blk, 0, s, X);
+                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, s, X);
+                hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, s, X);
+            }
             if (level + 1 == maxLevels) break;
             cur ^= 1;
             W.cur = queue(cur);
@@ -1113,7 +1135,8 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         const char* wfEnv = getenv("PBR_WAVEFRONT");
         bool wavefront = d->integrator == PBR_INTEGRATOR_WHITTED && !st && ctx->host.lights.size() == 1 &&
                          d->max_depth <= kWfMaxDepth && !(wfEnv && wfEnv[0] == '0');
-        bool wavefrontPath = d->integrator == PBR_INTEGRATOR_PATH && !st && d->max_depth <= 120 && !(wfEnv && wfEnv[0] == '0');
+        bool wavefrontPath = (d->integrator == PBR_INTEGRATOR_PATH || d->integrator == PBR_INTEGRATOR_VOLPATH) && !st &&
+                             d->max_depth <= 120 && ctx->host.media.size() / 10 < 255 && !(wfEnv && wfEnv[0] == '0');
         // waves per SIMD the megakernel is compiled for: trades VGPRs for scratch (PBR_OCC=1|2|4)
         int occ = 2;   // measured: 2 waves/SIMD beats 1 by 1.78x on C2 and ties 4
         if (const char* e = getenv("PBR_OCC")) occ = atoi(e);
@@ -1126,7 +1149,7 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
             int rc = render_wavefront(ctx, P, s);
             if (rc) return rc;
         } else if (wavefrontPath) {
-            int rc = render_wavefront_path(ctx, P, s);
+            int rc = render_wavefront_path(ctx, P, s, d->integrator == PBR_INTEGRATOR_VOLPATH);
             if (rc) return rc;
         } else switch (d->integrator) {
         case PBR_INTEGRATOR_WHITTED: PBR_LAUNCH(PBR_INTEGRATOR_WHITTED) break;

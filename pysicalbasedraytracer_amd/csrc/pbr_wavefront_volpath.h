@@ -1,0 +1,357 @@
+// pbr_wavefront_volpath.h — wavefront schedule for VolPathIntegrator::Li (VolPathIntegrator.cpp:
+// 21-107) over homogeneous media.  Included after pbr_wavefront_path.h; shares its queues, camera
+// kernel, probe kernel (the BSDF/phase-sampled ray of EstimateDirect is a plain Scene::Intersect,
+// Integrator.cpp:159) and finish.  Differences from the Path schedule:
+//   * rays carry their medium (packed into the queue's dim word);
+//   * every bounce first samples the ray's medium (HomogeneousMedium::Sample, two Get1D), which can
+//     turn the bounce into a medium interaction (HG phase function instead of a BSDF);
+//   * the light sample's visibility is VisibilityTester::Tr (Light.cpp:31-47): k_wfv_tr walks the
+//     shadow ray through medium interfaces, multiplying homogeneous transmittance, and the
+//     resolve multiplies Li by it before the !IsBlack test, in the reference's op order.
+#pragma once
+
+constexpr int kWfvDelta = 8;   // dFlags: the estimate's light is a delta light
+
+struct WfvParams {
+    WfpParams X;
+    // transmittance-walk queue (segmented): origin+tMax, dir + medium, target p, pError, n, id
+    float4* to; float4* td; float4* tp; float4* te; float4* tn; int* tid; int* trSeg;
+    float4* dLiA;          // light sample Li.rgb, lightPdf
+    float4* dTr;           // transmittance to the light sample
+    float* dWA;            // MIS weight of the light sample
+};
+
+__device__ __forceinline__ int pack_vol(int dim, int bounces, bool specular, int medium) {
+    return pack_path(dim, bounces, specular) | ((medium + 1) << 24);
+}
+
+// Scene::Intersect's medium interface on a hit (Primitive.cpp:30-34)
+__device__ __forceinline__ void set_interface(const DeviceScene& S, Isect* it, int rayMedium) {
+    int4 info = S.primInfo[it->slot];
+    int mi = (int)(short)(info.w & 0xffff), mo = (int)(short)((info.w >> 16) & 0xffff);
+    if (mi != mo) { it->medIn = mi; it->medOut = mo; }
+    else { it->medIn = rayMedium; it->medOut = rayMedium; }
+}
+
+template <int LOBES, bool MATS_LDS, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0) {
+    WfpParams& X = V.X;
+    WfParams& W = X.W;
+    const KParams& P = W.P;
+    const DeviceScene& S = P.S;
+    stage_halton_lds(P.smp);
+    const MatTemplate* mats = S.materials;
+    if constexpr (MATS_LDS) {
+        constexpr int words = (int)(sizeof(MatTemplate) / 4);
+        const int n = 2 * S.nMaterials * words;
+        const uint32_t* src = (const uint32_t*)S.materials;
+        uint32_t* dst = (uint32_t*)s_mats;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+        mats = s_mats;
+    }
+    __shared__ int s_push[4];   // transmittance walk, probe, direct, next
+    if (threadIdx.x < 4) s_push[threadIdx.x] = 0;
+    __syncthreads();
+    const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
+    const int stride = gridDim.x * blockDim.x;
+    const int nIter = (n + stride - 1) / stride;
+    const int base = blockIdx.x * W.segCap;
+    for (int it = 0; it < nIter; ++it) {
+        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const bool active = i < n;
+        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
+        bool pushTr = false, pushProbe = false, pushDirect = false, pushNext = false;
+        int id = 0, dim = 0, bounces = 0;
+        bool specularBounce = false;
+        Ray shadow, probe, cont;
+        VisPt vis;
+        if (active) {
+            float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
+            id = level0 ? q : W.cur.id[q];
+            const int dd = __float_as_int(d.w);
+            dim = dd & 0xffff;
+            bounces = (dd >> 16) & 0x7f;
+            specularBounce = (dd >> 23) & 1;
+            const int medium = ((dd >> 24) & 0xff) - 1;
+            Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, medium);
+            const int slot = __float_as_int(hr.x);
+            const bool found = slot >= 0;
+            float4 lv = X.stL[id], bv = X.stBeta[id];
+            rgb L = sp3(lv.x, lv.y, lv.z), beta = sp3(bv.x, bv.y, bv.z);
+            float etaScale = bv.w;
+            SState st;
+            st.index = W.sampleIndex[id];
+            st.dim = dim;
+            st.px = st.py = 0;
+            Isect isect;
+            if (found) {
+                int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
+                if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
+                else triangle_si(S, slot, ray, hr.y, hr.z, hr.w, flags, &isect);
+                isect.slot = slot;
+                set_interface(S, &isect, ray.medium);
+            }
+            // HomogeneousMedium::Sample (HomogeneousMedium.cpp:15-45)
+            bool mediumEvent = false;
+            Isect mi;
+            float g = 0;
+            if (ray.medium >= 0) {
+                const float* md = S.media + 10 * ray.medium;
+                int channel = (int)(get1d<true>(P.smp, st) * 3);
+                if (channel > 2) channel = 2;
+                float dist = -t_log(1 - get1d<true>(P.smp, st)) / md[6 + channel];
+                float t = mn(dist / len(ray.d), ray.tMax);
+                bool sampled = t < ray.tMax;
+                if (sampled) {
+                    mi.p = ray.o + ray.d * t; mi.wo = -ray.d; mi.n = mk(0, 0, 0); mi.pError = mk(0, 0, 0);
+                    mi.sn = mk(0, 0, 0); mi.dpdu = mk(0, 0, 0);
+                    mi.medIn = mi.medOut = ray.medium; mi.slot = -1;
+                    g = md[9];
+                    mediumEvent = true;
+                }
+                rgb Tr = exp_s(sp3(-md[6], -md[7], -md[8]) * mn(t, kMaxFloat) * len(ray.d));
+                rgb density = sampled ? (sp3(md[6], md[7], md[8]) * Tr) : Tr;
+                float pdf = 0;
+                pdf += density.r; pdf += density.g; pdf += density.b;
+                pdf *= 1 / (float)3;
+                if (pdf == 0) pdf = 1;
+                beta = beta * (sampled ? (Tr * sp3(md[3], md[4], md[5]) / pdf) : (Tr / pdf));
+            }
+            bool alive = !black(beta), doRR = false;
+            BSDF bsdf;
+            const Isect* ip = mediumEvent ? &mi : &isect;
+            bool estimate = false;
+            if (alive && mediumEvent) {
+                if (bounces >= P.maxDepth) alive = false;
+                else estimate = true;
+            } else if (alive) {
+                if (bounces == 0 || specularBounce) {
+                    if (found) L = L + beta * si_Le(S, isect, -ray.d);
+                    else for (int k = 0; k < S.nInfinite; ++k) L = L + beta * light_Le(S, S.lights[S.infinite[k]], ray);
+                }
+                if (!found || bounces >= P.maxDepth) alive = false;
+                else if (!make_bsdf(S, mats, isect, true, &bsdf)) {
+                    cont = spawn_ray(isect, ray.d);   // bounces--; continue: no Russian roulette
+                    pushNext = true;
+                    alive = false;
+                } else {
+                    estimate = true;
+                }
+            }
+            if (estimate && S.nLights > 0) {
+                // UniformSampleOneLight(handleMedia = true) / EstimateDirect
+                const Isect& ref = *ip;
+                float pmf;
+                const int li = sample_light(S, get1d<true>(P.smp, st), &pmf);
+                if (pmf != 0) {
+                    float uL0, uL1, uS0, uS1;
+                    get2d<true>(P.smp, st, &uL0, &uL1);
+                    get2d<true>(P.smp, st, &uS0, &uS1);
+                    const DLight& light = S.lights[li];
+                    const bool delta = light.type == LT_POINT;
+                    const int flagsNS = BSDF_ALL & ~BSDF_SPECULAR;
+                    int dflags = delta ? kWfvDelta : 0;
+                    f3 wi = mk(0, 0, 0);
+                    float lightPdf = 0, scatteringPdf = 0, weightA = 0;
+                    rgb Li = sample_li(S, light, ref, uL0, uL1, &wi, &lightPdf, &vis);
+                    rgb fA = sp(0.f);
+                    if (lightPdf > 0 && !black(Li)) {
+                        if (!mediumEvent) {
+                            fA = bsdf_f<LOBES>(bsdf, ref.wo, wi, flagsNS) * absdot(wi, ref.sn);
+                            scatteringPdf = bsdf_pdf<LOBES>(bsdf, ref.wo, wi, flagsNS);
+                        } else {
+                            fA = sp(phase_hg(dot(ref.wo, wi), g));
+                        }
+                        if (!black(fA)) {
+                            float fp = 1 * lightPdf, gp = 1 * scatteringPdf;
+                            weightA = (fp * fp) / (fp * fp + gp * gp);
+                            shadow = spawn_ray_to(ref, vis.p, vis.pError, vis.n);
+                            pushTr = true;
+                            dflags |= kWfpAPending;
+                        }
+                    }
+                    rgb fB = sp(0.f);
+                    float weightB = 1.f;
+                    if (!delta) {
+                        bool sampledSpecular = false;
+                        if (!mediumEvent) {
+                            int stype = 0;
+                            fB = bsdf_sample<LOBES>(bsdf, ref.wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
+                            fB = fB * absdot(wi, ref.sn);
+                            sampledSpecular = (stype & BSDF_SPECULAR) != 0;
+                        } else {
+                            float p = hg_sample(g, ref.wo, &wi, uS0, uS1);
+                            fB = sp(p);
+                            scatteringPdf = p;
+                        }
+                        if (!black(fB) && scatteringPdf > 0) {
+                            bool probeIt = true;
+                            if (!sampledSpecular) {
+                                float lp = pdf_li(S, light, ref, wi);
+                                if (lp == 0) probeIt = false;
+                                else {
+                                    float fp = 1 * scatteringPdf, gp = 1 * lp;
+                                    weightB = (fp * fp) / (fp * fp + gp * gp);
+                                }
+                            }
+                            if (probeIt) {
+                                probe = spawn_ray(ref, wi);
+                                pushProbe = true;
+                                dflags |= kWfpBPending;
+                            }
+                        }
+                    }
+                    if (dflags & (kWfpAPending | kWfpBPending)) {
+                        X.dA[id] = make_float4(fA.r, fA.g, fA.b, pmf);
+                        V.dLiA[id] = make_float4(Li.r, Li.g, Li.b, lightPdf);
+                        V.dWA[id] = weightA;
+                        X.dB[id] = make_float4(fB.r, fB.g, fB.b, weightB);
+                        X.dBeta[id] = make_float4(beta.r, beta.g, beta.b, scatteringPdf);
+                        X.dFlags[id] = dflags;
+                        X.dLight[id] = li;
+                        pushDirect = true;
+                    }
+                }
+            }
+            if (estimate) {
+                if (mediumEvent) {   // HenyeyGreenstein::Sample_p, then the ray leaves the interaction
+                    f3 wo = -ray.d, wi;
+                    float u0, u1;
+                    get2d<true>(P.smp, st, &u0, &u1);
+                    hg_sample(g, wo, &wi, u0, u1);
+                    cont = spawn_ray(mi, wi);
+                    specularBounce = false;
+                    doRR = true;
+                } else {
+                    const f3 wo = -ray.d;
+                    f3 wi = mk(0, 0, 0);
+                    float pdf = 0;
+                    int flags = 0;
+                    float u0, u1;
+                    get2d<true>(P.smp, st, &u0, &u1);
+                    rgb f = bsdf_sample<LOBES>(bsdf, wo, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
+                    if (!(black(f) || pdf == 0.f)) {
+                        beta = beta * (f * absdot(wi, isect.sn) / pdf);
+                        specularBounce = (flags & BSDF_SPECULAR) != 0;
+                        if ((flags & BSDF_SPECULAR) && (flags & BSDF_TRANSMISSION)) {
+                            float eta = bsdf.mt->eta;
+                            etaScale *= (dot(wo, isect.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                        }
+                        cont = spawn_ray(isect, wi);
+                        doRR = true;
+                    }
+                }
+            }
+            if (doRR) {
+                bool stop = false;
+                rgb rrBeta = beta * etaScale;
+                if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
+                    float qq = mx((float).05, 1 - maxval(rrBeta));
+                    if (get1d<true>(P.smp, st) < qq) stop = true;
+                    else beta = beta / (1 - qq);
+                }
+                if (!stop) {
+                    pushNext = true;
+                    bounces += 1;
+                }
+            }
+            dim = st.dim;
+            X.stBeta[id] = make_float4(beta.r, beta.g, beta.b, etaScale);
+            X.stL[id] = make_float4(L.r, L.g, L.b, 0.f);
+        }
+        const int ti = base + wave_push(&s_push[0], pushTr);
+        if (pushTr) {
+            V.to[ti] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
+            V.td[ti] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(shadow.medium));
+            V.tp[ti] = make_float4(vis.p.x, vis.p.y, vis.p.z, 0.f);
+            V.te[ti] = make_float4(vis.pError.x, vis.pError.y, vis.pError.z, 0.f);
+            V.tn[ti] = make_float4(vis.n.x, vis.n.y, vis.n.z, 0.f);
+            V.tid[ti] = id;
+        }
+        const int pi = base + wave_push(&s_push[1], pushProbe);
+        if (pushProbe) {
+            X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
+            X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
+            X.pid[pi] = id;
+        }
+        const int di = base + wave_push(&s_push[2], pushDirect);
+        if (pushDirect) X.directId[di] = id;
+        const int ni = base + wave_push(&s_push[3], pushNext);
+        if (pushNext) {
+            W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
+            W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_vol(dim, bounces, specularBounce, cont.medium)));
+            W.next.id[ni] = id;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        V.trSeg[blockIdx.x] = s_push[0];
+        X.probeSeg[blockIdx.x] = s_push[1];
+        X.directSeg[blockIdx.x] = s_push[2];
+        W.next.segCount[blockIdx.x] = s_push[3];
+    }
+}
+
+// VisibilityTester::Tr (Light.cpp:31-47): walk to the light sample through medium interfaces
+template <int SHORT>
+__global__ __launch_bounds__(256) void k_wfv_tr(WfvParams V) {
+    WfpParams& X = V.X;
+    const DeviceScene& S = X.W.P.S;
+    const int n = seg_scan(V.trSeg);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int q = seg_pos(X.W.segCap, i);
+        float4 o = V.to[q], d = V.td[q], tp = V.tp[q], te = V.te[q], tn = V.tn[q];
+        const f3 p1 = mk(tp.x, tp.y, tp.z), e1 = mk(te.x, te.y, te.z), n1 = mk(tn.x, tn.y, tn.z);
+        Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, __float_as_int(d.w));
+        rgb Tr = sp(1.f);
+        for (int guard = 0; guard < 256; ++guard) {
+            HitRec h;
+            Counters c;
+            const bool hit = traverse<false, false, SHORT>(S, ray, &h, &c);
+            if (hit && S.primInfo[h.slot].y >= 0) { Tr = sp(0.0f); break; }
+            if (ray.medium >= 0) Tr = Tr * medium_tr(S, ray.medium, ray);
+            if (!hit) break;
+            Isect isect;
+            int flags = __float_as_int(S.triVerts[3 * (size_t)h.slot].w);
+            if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)h.slot].x)], ray, ray.tMax, &isect);
+            else triangle_si(S, h.slot, ray, h.b0, h.b1, h.b2, flags, &isect);
+            isect.slot = h.slot;
+            set_interface(S, &isect, ray.medium);
+            ray = spawn_ray_to(isect, p1, e1, n1);
+        }
+        V.dTr[V.tid[q]] = make_float4(Tr.r, Tr.g, Tr.b, 0.f);
+    }
+}
+
+// Ld = [f·(Li·Tr)·w/lightPdf if Li·Tr is not black] + [f·Li·w/scatteringPdf if Li is not black];
+// L += beta · (Ld / pmf)
+__global__ __launch_bounds__(256) void k_wfv_resolve(WfvParams V) {
+    WfpParams& X = V.X;
+    const int n = seg_scan(X.directSeg);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int id = X.directId[seg_pos(X.W.segCap, i)];
+        const int fl = X.dFlags[id];
+        const float4 a = X.dA[id], bt = X.dBeta[id];
+        rgb Ld = sp(0.f);
+        if (fl & kWfpAPending) {
+            const float4 la = V.dLiA[id], tr = V.dTr[id];
+            const rgb Lt = sp3(la.x, la.y, la.z) * sp3(tr.x, tr.y, tr.z);
+            if (!black(Lt)) {
+                const rgb fA = sp3(a.x, a.y, a.z);
+                if (fl & kWfvDelta) Ld = Ld + fA * Lt / la.w;
+                else Ld = Ld + fA * Lt * V.dWA[id] / la.w;
+            }
+        }
+        if (fl & kWfpBPending) {
+            const float4 li = X.dLi[id], b = X.dB[id];
+            const rgb Li2 = sp3(li.x, li.y, li.z);
+            if (!black(Li2)) Ld = Ld + sp3(b.x, b.y, b.z) * Li2 * b.w / bt.w;
+        }
+        const rgb beta = sp3(bt.x, bt.y, bt.z);
+        const rgb direct = beta * (Ld / a.w);
+        float4 L = X.stL[id];
+        L.x = L.x + direct.r; L.y = L.y + direct.g; L.z = L.z + direct.b;
+        X.stL[id] = L;
+        X.dFlags[id] = 0;
+    }
+}

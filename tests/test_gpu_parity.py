@@ -287,3 +287,16 @@ def test_wavefront_path_equals_megakernel(hip, monkeypatch, config):
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
     assert np.array_equal(wf8, mk8)
+
+
+def test_wavefront_volpath_equals_megakernel(hip, monkeypatch):
+    """The wavefront VolPath schedule (medium sampling, HG phase, transmittance walks through the
+    glass dragon's medium interface) matches the megakernel bit for bit (C5 shape)."""
+    s, rd = scenes.config_c5(80, 45, 8, mesh=small_dragon(40))
+    hip.upload(s)
+    monkeypatch.setenv("PBR_WAVEFRONT", "1")
+    wf, wf8, _ = hip.render(rd)
+    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    mk, mk8, _ = hip.render(rd)
+    assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
+    assert np.array_equal(wf8, mk8)
