@@ -164,8 +164,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": ("wavefront frame: k_wf_camera_extend, (k_wf_shade, k_wf_shadow, k_wf_extend) per level, "
-                                    "k_wf_finish, per 2^23-sample chunk" if rd.integrator == 0 else "k_render megakernel"),
+                         "kernel": ["wavefront frame: k_wf_camera_extend, (k_wf_shade, k_wf_shadow, k_wf_extend) per "
+                                    "level, k_wf_finish, per 2^25-sample chunk",
+                                    "wavefront frame: k_wfp_camera_extend, (k_wfp_shade, k_wfp_shadow, k_wfp_probe, "
+                                    "k_wfp_resolve, k_wf_extend) per bounce, k_wfp_finish, per 2^25-sample chunk",
+                                    "wavefront frame: k_wfp_camera_extend, (k_wfv_shade, k_wfv_tr, k_wfp_probe, "
+                                    "k_wfv_resolve, k_wf_extend) per bounce, k_wfp_finish, per 2^25-sample chunk"][rd.integrator],
                          "kernel_ms": round(k_ms, 3),
                          "bytes_per_sample": round(alg_bytes / samples_rank, 1),
                          "model": "per sample: 32*node_tests + 48*prim_tests + 96*rays + 64*shading_events "
