@@ -95,14 +95,17 @@ def main():
     r.upload(scene)
     upload_s = time.time() - t0
 
-    stream = torch.cuda.current_stream(dev)
+    # a real stream (torch's default one has handle 0, which the C-ABI reads as "context stream")
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     rgb = torch.empty((npx, 3), dtype=torch.float32, device=dev)
     rgba = torch.empty((npx, 4), dtype=torch.uint8, device=dev)
     # multi-GPU: rank 0 gathers the packed tile spans over RCCL and scatters them into the frame
     exchange = FrameGather(W, H, world, dev) if world > 1 else None
 
     def step():
-        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+        # asynchronous: the frame is enqueued on `stream` and the next one queues behind it
+        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
         if exchange is not None:
             exchange(rgb, rank)
 
@@ -118,21 +121,20 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    kernel_ms = []
+    # HIP events bracket each frame's launches on the render stream; read after the final sync
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for ev0, ev1 in evs:
         ev0.record(stream)
-        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
         ev1.record(stream)
         if exchange is not None:
             exchange(rgb, rank)
-        torch.cuda.synchronize(dev)
-        kernel_ms.append(ev0.elapsed_time(ev1))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    kernel_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

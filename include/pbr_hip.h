@@ -179,7 +179,10 @@ typedef struct pbr_render_desc {
     int n_tiles;
     const pbr_tile* tiles;
     int outputs_on_device;      /* 1: rgb_out/rgba_out are device pointers (e.g. torch tensors) */
-    void* stream;               /* hipStream_t to launch on (NULL = context stream) */
+    void* stream;               /* hipStream_t to launch on (NULL = context stream).  With
+                                 * outputs_on_device, collect_stats == 0 and stats == NULL the call
+                                 * is asynchronous: it returns once the frame is enqueued on `stream`
+                                 * and the caller synchronises (frames queue back to back). */
     int collect_stats;          /* 1: also count BVH node visits / triangle tests (slower) */
     /* PBR_SAMPLER_SOBOL (pbrt-v3 SobolSampler; the reference ships only its tables, F3):
      * generator matrices in the layout of the reference's SobolMatrices32 (Sampler/SobolMatrices.h:

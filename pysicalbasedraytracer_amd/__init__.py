@@ -68,14 +68,18 @@ class HipRenderer:
                                              out_rgba.ctypes.data if rgba else None, C.byref(st)), "render")
         return out_rgb, out_rgba, st
 
-    def render_device(self, rdesc, rgb_ptr: int, rgba_ptr: int, stream: int | None = None, stats=False):
-        """Render straight into device buffers (e.g. torch tensors' data_ptr()) on `stream`."""
-        st = capi.RenderStats()
+    def render_device(self, rdesc, rgb_ptr: int, rgba_ptr: int, stream: int | None = None, stats=False,
+                      sync=True):
+        """Render straight into device buffers (e.g. torch tensors' data_ptr()) on `stream`.
+
+        sync=False (and stats=False): the frame is only enqueued on `stream` — the caller
+        synchronises — and None is returned; frames then run back to back on the device."""
         rdesc.outputs_on_device = 1
         rdesc.stream = stream
         rdesc.collect_stats = int(stats)
+        st = capi.RenderStats() if (sync or stats) else None
         self._check(self.lib.pbr_hip_render(self.ctx, C.byref(rdesc), rgb_ptr or None, rgba_ptr or None,
-                                            C.byref(st)), "render")
+                                            C.byref(st) if st is not None else None), "render")
         return st
 
     def get_bvh(self):

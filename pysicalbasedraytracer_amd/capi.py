@@ -197,6 +197,13 @@ def load_library(path: str | None = None) -> C.CDLL:
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError(f"libpbr_hip.so not built at {p}; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: torch bundles its own libamdhip64 (same soname as /opt/rocm's).
+    # Whichever loads first serves both, and torch fails to initialise ("No HIP GPUs are
+    # available") on the newer system runtime, so let torch load first when it is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(p)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(lib, name)

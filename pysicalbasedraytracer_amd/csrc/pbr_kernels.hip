@@ -625,6 +625,10 @@ struct pbr_hip_ctx {
     const uint32_t* sobolSrc = nullptr;  // what dSobol holds (user pointer or the built-in table)
     int sobolSrcDims = 0, sobolPixM = -1;
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
+    std::vector<int32_t> tilesHost;      // what dTiles / dTileStart hold (re-uploaded on change only)
+    std::vector<long long> startsHost;
+    hipStream_t lastStream = nullptr;    // stream of the last asynchronous render (may still run)
+    bool inFlight = false;
     // wavefront queues and per-sample records (pbr_wavefront.h)
     DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
     // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
@@ -645,6 +649,13 @@ int set_err(pbr_hip_ctx* c, int code, const std::string& msg) {
         hipError_t e_ = (expr);                                                              \
         if (e_ != hipSuccess) return set_err(ctx, PBR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
+
+// Wait for an asynchronous render still reading the context's buffers (see pbr_hip_render).
+int drain(pbr_hip_ctx* ctx) {
+    if (ctx->inFlight) HIP_TRY(hipStreamSynchronize(ctx->lastStream));
+    ctx->inFlight = false;
+    return PBR_OK;
+}
 
 DeviceScene device_scene(pbr_hip_ctx* ctx) {
     const HostScene& h = ctx->host;
@@ -700,6 +711,7 @@ int prepare_sobol(pbr_hip_ctx* ctx, const uint32_t* user, int userDims, int w, i
     }
     if (dims < 2) return set_err(ctx, PBR_E_INVALID, "Sobol needs at least 2 dimensions of matrices");
     if (src != ctx->sobolSrc || dims != ctx->sobolSrcDims) {
+        if (int rc = drain(ctx)) return rc;
         HIP_TRY(ctx->dSobol.ensure((size_t)dims * kSobolMatrixSize * 4));
         HIP_TRY(hipMemcpyAsync(ctx->dSobol.p, src, (size_t)dims * kSobolMatrixSize * 4, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -710,6 +722,7 @@ int prepare_sobol(pbr_hip_ctx* ctx, const uint32_t* user, int userDims, int w, i
     int res = 1, m = 0;
     while (res < std::max(w, h)) { res <<= 1; ++m; }
     if (m != ctx->sobolPixM) {
+        if (int rc = drain(ctx)) return rc;
         std::vector<uint32_t> t;
         try {
             sobol_pixel_tables(src, m, &t);
@@ -734,8 +747,10 @@ int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
     float fi = 0;
     light_distribution(ctx->host, strategy, &cdf, &func, &fi);
     if (func.empty()) func.push_back(0.f);
+    if (int rc = drain(ctx)) return rc;
     HIP_TRY(ctx->dCdf.upload(cdf, ctx->stream));
     HIP_TRY(ctx->dFunc.upload(func, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));   // the host vectors die on return
     ctx->funcInt = fi;
     ctx->curStrategy = strategy;
     return PBR_OK;
@@ -1002,6 +1017,7 @@ int pbr_hip_create(int device, pbr_hip_ctx** out) {
 int pbr_hip_destroy(pbr_hip_ctx* ctx) {
     if (!ctx) return PBR_E_INVALID;
     (void)hipSetDevice(ctx->device);
+    (void)drain(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1016,6 +1032,7 @@ const char* pbr_hip_last_error(const pbr_hip_ctx* ctx) { return ctx ? ctx->err.c
 int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     if (!ctx) return PBR_E_INVALID;
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
     try {
         build_host_scene(desc, &ctx->host);
     } catch (const std::exception& e) {
@@ -1107,8 +1124,19 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         starts.push_back(0);
         npx = (long long)d->camera.width * d->camera.height;
     }
-    HIP_TRY(ctx->dTiles.upload(tiles, s));
-    HIP_TRY(ctx->dTileStart.upload(starts, s));
+    // Device-output renders without host-side stats return without synchronising, so frames can
+    // queue back to back.  The context's queues are reused by every frame: a render on another
+    // stream first drains the previous one.
+    if (ctx->lastStream != s) {
+        if (int rc = drain(ctx)) return rc;
+    }
+    if (tiles != ctx->tilesHost || starts != ctx->startsHost) {
+        HIP_TRY(hipStreamSynchronize(s));   // an earlier async copy may still read the host copies
+        ctx->tilesHost = tiles;
+        ctx->startsHost = starts;
+        HIP_TRY(ctx->dTiles.upload(ctx->tilesHost, s));
+        HIP_TRY(ctx->dTileStart.upload(ctx->startsHost, s));
+    }
     P.tiles = (const int4*)ctx->dTiles.p;
     P.tileStart = (const long long*)ctx->dTileStart.p;
     P.nTiles = (int)starts.size();
@@ -1166,7 +1194,13 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     }
     unsigned long long hs[4] = {0, 0, 0, 0};
     if (d->collect_stats) HIP_TRY(hipMemcpyAsync(hs, ctx->dStats.p, sizeof(hs), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (!d->outputs_on_device || d->collect_stats || stats) {
+        HIP_TRY(hipStreamSynchronize(s));
+    } else {
+        ctx->inFlight = true;
+        ctx->lastStream = s;
+        return PBR_OK;
+    }
     auto t1 = std::chrono::steady_clock::now();
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));

@@ -300,3 +300,30 @@ def test_wavefront_volpath_equals_megakernel(hip, monkeypatch):
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
     assert np.array_equal(wf8, mk8)
+
+
+def test_async_device_frames(hip):
+    """Device-output renders without stats only enqueue the frame: frames queued back to back on
+    one stream, a tile change between them, and a frame on a second stream (which drains the
+    first) all equal the synchronous host renders bit for bit."""
+    import torch
+    s, rd = scenes.config_c2(128, 72, 4, mesh=small_dragon(48))
+    hip.upload(s)
+    full, _, _ = hip.render(rd)
+    tiles = tile_grid(128, 72, 32)
+    mine = [t for i, t in enumerate(tiles) if i % 2 == 0]
+    rdt = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, tiles=mine)
+    part, _, _ = hip.render(rdt)
+    dev = torch.device("cuda", 0)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    outs = []
+    for k, (desc, n) in enumerate([(rd, 128 * 72), (rdt, len(part)), (rd, 128 * 72), (rdt, len(part))]):
+        rgb = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        rgba = torch.empty((n, 4), dtype=torch.uint8, device=dev)
+        st = s1 if k < 3 else s2
+        with torch.cuda.stream(st):
+            assert hip.render_device(desc, rgb.data_ptr(), rgba.data_ptr(), stream=st.cuda_stream, sync=False) is None
+        outs.append((st, rgb))
+    torch.cuda.synchronize(dev)
+    for (st, rgb), want in zip(outs, [full, part, full, part]):
+        assert np.array_equal(rgb.cpu().numpy().view(np.uint32), want.view(np.uint32))
