@@ -209,7 +209,17 @@ __device__ __forceinline__ bool node_slab(f3 lo, f3 hi, const Ray& r, f3 inv, bo
 // Short traversal stack in LDS for the 256-lane wavefront kernels: entries [0, SHORT) live in LDS
 // ([entry][lane], conflict-free), deeper ones in the private (scratch) array.  Only where entries
 // are kept changes; the visit order does not.
-constexpr int kShortStack = 8;
+// LDS entries of the traversal short stack and the minimum 256-lane workgroups per CU the
+// traversal kernels are compiled for: 6 entries (12 KB) + the 8-KB segment scan fit 7 workgroups
+// per CU in LDS, and 7 × 4 waves per CU leave each lane 72 VGPRs.  Measured on C2: 8/1 25.71 ms,
+// 8/6 25.30, 6/7 25.22, 5/8 25.63, 4/8 25.65 (the deeper entries live in scratch).
+#ifndef PBR_SHORT_STACK_DEPTH
+#define PBR_SHORT_STACK_DEPTH 6
+#endif
+#ifndef PBR_TRAV_OCC
+#define PBR_TRAV_OCC 7
+#endif
+constexpr int kShortStack = PBR_SHORT_STACK_DEPTH;
 __shared__ int s_trav_ref[kShortStack * 256];
 __shared__ float s_trav_t[kShortStack * 256];
 

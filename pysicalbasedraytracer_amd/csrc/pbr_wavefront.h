@@ -96,7 +96,7 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 }
 
 template <int SHORT>
-__global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams W) {
     const KParams& P = W.P;
     int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= W.nSamples) return;
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void k_wf_camera_extend(WfParams W) {
 }
 
 template <int SHORT>
-__global__ __launch_bounds__(256) void k_wf_extend(WfParams W) {
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_extend(WfParams W) {
     const int n = seg_scan(W.cur.segCount);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
 
 // any-hit for the shadow queue; a visible light adds its contribution to the emitting level
 template <int SHORT>
-__global__ __launch_bounds__(256) void k_wf_shadow(WfParams W) {
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);

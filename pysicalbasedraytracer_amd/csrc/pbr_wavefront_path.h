@@ -39,7 +39,7 @@ __device__ __forceinline__ int pack_path(int dim, int bounces, bool specular) {
 }
 
 template <int SHORT>
-__global__ __launch_bounds__(256) void k_wfp_camera_extend(WfpParams X) {
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpParams X) {
     WfParams& W = X.W;
     const KParams& P = W.P;
     int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
 
 // VisibilityTester::Unoccluded for the light-sample rays
 template <int SHORT>
-__global__ __launch_bounds__(256) void k_wfp_shadow(WfpParams X) {
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_shadow(WfpParams X) {
     WfParams& W = X.W;
     const int n = seg_scan(W.shadowSeg);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void k_wfp_shadow(WfpParams X) {
 // EstimateDirect's BSDF-sampled ray: closest hit; Li = the sampled light's emission if that is
 // what it hits (si.Le), light.Le(ray) if it escapes (Light::Le, F4 for non-infinite lights).
 template <int SHORT>
-__global__ __launch_bounds__(256) void k_wfp_probe(WfpParams X) {
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_probe(WfpParams X) {
     WfParams& W = X.W;
     const DeviceScene& S = W.P.S;
     const int n = seg_scan(X.probeSeg);

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
 
 // VisibilityTester::Tr (Light.cpp:31-47): walk to the light sample through medium interfaces
 template <int SHORT>
-__global__ __launch_bounds__(256) void k_wfv_tr(WfvParams V) {
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfv_tr(WfvParams V) {
     WfpParams& X = V.X;
     const DeviceScene& S = X.W.P.S;
     const int n = seg_scan(V.trSeg);

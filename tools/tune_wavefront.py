@@ -15,7 +15,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from pysicalbasedraytracer_amd import HipRenderer, capi, scenes  # noqa: E402
+from pysicalbasedraytracer_amd import HipRenderer, capi, scenes, tiles_for_rank  # noqa: E402
 
 
 def main():
@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--lib", default=None, help="an experimental build of libpbr_hip.so")
+    ap.add_argument("--shard", default=None, help="R/N: render only rank R's tiles of an N-GPU job "
+                                                   "(per-rank frame time of the sharded bench)")
     ap.add_argument("variants", nargs="*", default=[""])
     a = ap.parse_args()
     if a.lib:
@@ -30,12 +32,19 @@ def main():
     print("build:", capi.load_library().pbr_hip_build_info().decode(), flush=True)
     scene, rd = scenes.CONFIGS[a.config]()
     W, H, spp = rd.camera.width, rd.camera.height, rd.spp
+    npx = W * H
+    if a.shard:
+        rk, n = (int(x) for x in a.shard.split("/"))
+        tiles = tiles_for_rank(W, H, rk, n)
+        rd = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                                rd.sampler, tiles=tiles)
+        npx = sum((t[2] - t[0]) * (t[3] - t[1]) for t in tiles)
     r = HipRenderer(0)
     r.upload(scene)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
-    rgb = torch.empty((W * H, 3), dtype=torch.float32, device=dev)
-    rgba = torch.empty((W * H, 4), dtype=torch.uint8, device=dev)
+    rgb = torch.empty((npx, 3), dtype=torch.float32, device=dev)
+    rgba = torch.empty((npx, 4), dtype=torch.uint8, device=dev)
     ref = None
     for v in a.variants:
         env = dict(kv.split("=") for kv in v.split(",") if kv)
@@ -55,7 +64,9 @@ def main():
         if ref is None:
             ref = out
         m = float(np.median(ms))
-        print(f"{a.config} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  {W * H * spp / m / 1e3:8.1f} Msamples/s  {same}", flush=True)
+        tag = f" shard {a.shard} ({npx} px)" if a.shard else ""
+        print(f"{a.config}{tag} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  "
+              f"{npx * spp / m / 1e3:8.1f} Msamples/s  {same}", flush=True)
         for k, old in saved.items():
             if old is None:
                 os.environ.pop(k, None)
