@@ -610,6 +610,18 @@ struct DevBuf {
     }
 };
 
+// Wavefront queues, per-sample state and records of one chunk lane (pbr_wavefront*.h).
+struct WfBufs {
+    DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
+    DevBuf wsO2, wsD2, wsC2, wsId2;   // Whitted: second shadow queue (levels alternate)
+    // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
+    DevBuf wpO, wpD, wpId, wdId, sL, sBeta, rA, rB, rBeta, rLi, rFlags, rLight;
+    DevBuf wtO, wtD, wtP, wtE, wtN, wtId, rLiA, rTr, rWA;   // VolPath transmittance walk
+};
+// Chunks alternate between two lanes (own buffers, own stream) so one chunk's launch tails overlap
+// the other's work — what keeps a small per-GPU shard of a multi-GPU frame efficient.
+constexpr int kWfLanes = 2;
+
 struct pbr_hip_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -629,11 +641,13 @@ struct pbr_hip_ctx {
     std::vector<long long> startsHost;
     hipStream_t lastStream = nullptr;    // stream of the last asynchronous render (may still run)
     bool inFlight = false;
-    // wavefront queues and per-sample records (pbr_wavefront.h)
-    DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
-    // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
-    DevBuf wpO, wpD, wpId, wdId, sL, sBeta, rA, rB, rBeta, rLi, rFlags, rLight;
-    DevBuf wtO, wtD, wtP, wtE, wtN, wtId, rLiA, rTr, rWA;   // VolPath transmittance walk
+    // wavefront buffers of the two chunk lanes, and the lane-1 stream with its fork/join events
+    WfBufs wb[kWfLanes];
+    hipStream_t side = nullptr;
+    hipEvent_t evFork = nullptr, evJoin = nullptr;
+    // Whitted: per lane, a stream for the shadow rays and per-level events (shade done, shadow done)
+    hipStream_t shadowStream[kWfLanes] = {};
+    hipEvent_t evShade[kWfLanes][kWfMaxDepth + 2] = {}, evShadow[kWfLanes][kWfMaxDepth + 2] = {};
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
 };
@@ -757,43 +771,67 @@ int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
 }
 
 
-// Wavefront Whitted: chunks of ~2^23 samples, per level shade → shadow → extend (pbr_wavefront.h).
+// Chunking of the wavefront schedules: at most 2^chunkLog2 samples per chunk; chunks alternate
+// over the lanes.  Measured on C2: two lanes 23.4 ms vs 24.9 for one; forcing a one-chunk
+// (1/8-frame shard) frame into two concurrent half chunks was slower (4.00 vs 3.86 ms).
+struct WfChunks {
+    long long chunkPix = 1;
+    int lanes = 1;
+    size_t cap = 0;   // samples of the largest chunk
+    int segCap = 0;   // capacity of one queue segment
+    size_t qcap = 0;  // queue entries
+};
+WfChunks wf_chunks(const KParams& P) {
+    WfChunks c;
+    int chunkLog2 = 25;
+    if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
+    c.lanes = kWfLanes;
+    if (const char* e = getenv("PBR_LANES")) c.lanes = std::min(kWfLanes, std::max(1, atoi(e)));
+    c.chunkPix = std::max(1LL, (1LL << chunkLog2) / P.spp);
+    if (c.chunkPix >= P.nPixels) {   // one chunk: splitting a small frame only adds launch tails
+        c.chunkPix = P.nPixels;
+        c.lanes = 1;
+    }
+    c.cap = (size_t)c.chunkPix * P.spp;
+    // a shade workgroup processes at most ceil(cap / (kWfBlocks·256)) rounds of 256
+    c.segCap = (int)((c.cap + (size_t)kWfBlocks * 256 - 1) / ((size_t)kWfBlocks * 256) * 256);
+    c.qcap = std::max(c.cap, (size_t)c.segCap * kWfBlocks);
+    return c;
+}
+// Fork lane 1 off `s` at the start of a frame, join it back at the end.
+int wf_fork(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
+    if (lanes < 2) return PBR_OK;
+    if (!ctx->side) {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->evJoin, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(ctx->evFork, s));
+    HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->evFork, 0));
+    return PBR_OK;
+}
+int wf_join(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
+    if (lanes < 2) return PBR_OK;
+    HIP_TRY(hipEventRecord(ctx->evJoin, ctx->side));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->evJoin, 0));
+    return PBR_OK;
+}
+dim3 resident_grid(pbr_hip_ctx* ctx, const void* fn) {
+    int perCU = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, fn, 256, 0) != hipSuccess || perCU <= 0) perCU = 4;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
+    return dim3((unsigned)(perCU * cus));
+}
+
+// Wavefront Whitted: chunks of up to 2^25 samples on two lanes, per level shade → shadow → extend
+// (pbr_wavefront.h).
 int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const int spp = P.spp;
     // samples per chunk: queue + record memory ≈ 370 B per sample at depth 5 (12 GB at 2^25);
-    // measured on C2: 2^23 29.4 ms, 2^24 28.1, 2^25 26.6, 2^27 (whole frame) 26.6
-    int chunkLog2 = 25;
-    if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
-    long long chunkPix = std::max(1LL, (1LL << chunkLog2) / spp);
-    if (chunkPix > P.nPixels) chunkPix = P.nPixels;
-    const size_t cap = (size_t)chunkPix * spp;
-    // segment capacity: a shade workgroup processes at most ceil(cap / (kWfBlocks·256)) rounds of 256
-    const int segCap = (int)((cap + (size_t)kWfBlocks * 256 - 1) / ((size_t)kWfBlocks * 256) * 256);
-    const size_t qcap = std::max(cap, (size_t)segCap * kWfBlocks);
-    for (int k = 0; k < 2; ++k) {
-        HIP_TRY(ctx->wqO[k].ensure(qcap * 16)); HIP_TRY(ctx->wqD[k].ensure(qcap * 16));
-        HIP_TRY(ctx->wqId[k].ensure(qcap * 4)); HIP_TRY(ctx->wqHit[k].ensure(qcap * 16));
-    }
-    HIP_TRY(ctx->wsO.ensure(qcap * 16)); HIP_TRY(ctx->wsD.ensure(qcap * 16));
-    HIP_TRY(ctx->wsC.ensure(qcap * 16)); HIP_TRY(ctx->wsId.ensure(qcap * 4));
+    // measured on C2 (one lane): 2^23 29.4 ms, 2^24 28.1, 2^25 26.6, 2^27 (whole frame) 26.6
+    const WfChunks ch = wf_chunks(P);
+    const size_t cap = ch.cap, qcap = ch.qcap;
     const int levels = P.maxDepth < 1 ? 1 : P.maxDepth;
-    HIP_TRY(ctx->wRecA.ensure(cap * 16 * levels)); HIP_TRY(ctx->wRecF.ensure(cap * 16 * levels));
-    HIP_TRY(ctx->wRecP.ensure(cap * 4 * levels)); HIP_TRY(ctx->wDepth.ensure(cap * 4));
-    HIP_TRY(ctx->wIndex.ensure(cap * 4));
-    HIP_TRY(ctx->wCnt.ensure(3 * kWfBlocks * sizeof(int)));
-    int* cnt = (int*)ctx->wCnt.p;   // segment counts: queue 0, queue 1, shadow queue
-    WfParams W;
-    std::memset(&W, 0, sizeof(W));
-    W.P = P;
-    W.so = (float4*)ctx->wsO.p; W.sd = (float4*)ctx->wsD.p; W.sc = (float4*)ctx->wsC.p; W.sid = (int*)ctx->wsId.p;
-    W.shadowSeg = cnt + 2 * kWfBlocks;
-    W.segCap = segCap;
-    W.recA = (float4*)ctx->wRecA.p; W.recF = (float4*)ctx->wRecF.p; W.recP = (float*)ctx->wRecP.p;
-    W.depthOf = (int*)ctx->wDepth.p;
-    W.sampleIndex = (uint32_t*)ctx->wIndex.p;
-    W.initRecords = ctx->host.anyNoMaterial ? 1 : 0;
-    // Halton dims one sample reaches: 5 camera + 4 per level (light 2D, SpecularReflect 2D)
-    W.P.smp.ldsDims = std::min(kLdsDims, 5 + 4 * levels + 2);
     int lobes = 0;
     for (const MatTemplate& m : ctx->host.materials)
         for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
@@ -803,172 +841,238 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const bool shortStack = !(eStack && eStack[0] == '0');
     const char* eMats = getenv("PBR_MATS_LDS");
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
-    W.cap = (int)cap;
-    auto queue = [&](int k) {
+    // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
+    const int maxLevels = levels + (ctx->host.anyNoMaterial ? 2 : 0);
+    // Shadow rays of level L run on a second stream, overlapping extend(L+1) and shade(L+1) (they
+    // only read what shade(L) wrote); the shadow queue alternates between two buffers by level.
+    // Default: when the frame is one chunk (no lane overlap).  Measured on C2: a 1/8 shard
+    // 3.97 → 3.54 ms; the whole frame (two lanes) 23.43 → 23.76 ms, so off there.
+    const char* eOv = getenv("PBR_SHADOW_STREAM");
+    const bool shadowOverlap = (eOv ? eOv[0] == '1' : ch.lanes == 1) && maxLevels <= kWfMaxDepth + 2;
+    WfParams WL[kWfLanes];
+    int* cntL[kWfLanes];
+    for (int l = 0; l < ch.lanes; ++l) {
+        WfBufs& B = ctx->wb[l];
+        for (int k = 0; k < 2; ++k) {
+            HIP_TRY(B.wqO[k].ensure(qcap * 16)); HIP_TRY(B.wqD[k].ensure(qcap * 16));
+            HIP_TRY(B.wqId[k].ensure(qcap * 4)); HIP_TRY(B.wqHit[k].ensure(qcap * 16));
+        }
+        HIP_TRY(B.wsO.ensure(qcap * 16)); HIP_TRY(B.wsD.ensure(qcap * 16));
+        HIP_TRY(B.wsC.ensure(qcap * 16)); HIP_TRY(B.wsId.ensure(qcap * 4));
+        HIP_TRY(B.wRecA.ensure(cap * 16 * levels)); HIP_TRY(B.wRecF.ensure(cap * 16 * levels));
+        HIP_TRY(B.wRecP.ensure(cap * 4 * levels)); HIP_TRY(B.wDepth.ensure(cap * 4));
+        HIP_TRY(B.wIndex.ensure(cap * 4));
+        if (shadowOverlap) {
+            HIP_TRY(B.wsO2.ensure(qcap * 16)); HIP_TRY(B.wsD2.ensure(qcap * 16));
+            HIP_TRY(B.wsC2.ensure(qcap * 16)); HIP_TRY(B.wsId2.ensure(qcap * 4));
+            if (!ctx->shadowStream[l]) {
+                HIP_TRY(hipStreamCreateWithFlags(&ctx->shadowStream[l], hipStreamNonBlocking));
+                for (int k = 0; k < kWfMaxDepth + 2; ++k) {
+                    HIP_TRY(hipEventCreateWithFlags(&ctx->evShade[l][k], hipEventDisableTiming));
+                    HIP_TRY(hipEventCreateWithFlags(&ctx->evShadow[l][k], hipEventDisableTiming));
+                }
+            }
+        }
+        HIP_TRY(B.wCnt.ensure(4 * kWfBlocks * sizeof(int)));
+        int* cnt = cntL[l] = (int*)B.wCnt.p;   // segment counts: queue 0, queue 1, shadow queues 0, 1
+        WfParams& W = WL[l];
+        std::memset(&W, 0, sizeof(W));
+        W.P = P;
+        W.so = (float4*)B.wsO.p; W.sd = (float4*)B.wsD.p; W.sc = (float4*)B.wsC.p; W.sid = (int*)B.wsId.p;
+        W.shadowSeg = cnt + 2 * kWfBlocks;
+        W.segCap = ch.segCap;
+        W.recA = (float4*)B.wRecA.p; W.recF = (float4*)B.wRecF.p; W.recP = (float*)B.wRecP.p;
+        W.depthOf = (int*)B.wDepth.p;
+        W.sampleIndex = (uint32_t*)B.wIndex.p;
+        W.initRecords = ctx->host.anyNoMaterial ? 1 : 0;
+        // Halton dims one sample reaches: 5 camera + 4 per level (light 2D, SpecularReflect 2D)
+        W.P.smp.ldsDims = std::min(kLdsDims, 5 + 4 * levels + 2);
+        W.cap = (int)cap;
+    }
+    auto queue = [&](int l, int k) {
+        WfBufs& B = ctx->wb[l];
         WfQueue q;
-        q.o = (float4*)ctx->wqO[k].p; q.d = (float4*)ctx->wqD[k].p; q.id = (int*)ctx->wqId[k].p; q.hit = (float4*)ctx->wqHit[k].p;
-        q.segCount = cnt + k * kWfBlocks;
+        q.o = (float4*)B.wqO[k].p; q.d = (float4*)B.wqD[k].p; q.id = (int*)B.wqId[k].p; q.hit = (float4*)B.wqHit[k].p;
+        q.segCount = cntL[l] + k * kWfBlocks;
         return q;
     };
     const dim3 blk(256), gstride(kWfBlocks);
     // The queue consumers (extend, shadow) run exactly one resident wave of workgroups: a grid of
     // kWfBlocks would leave a partial second round (2048 = 1.33 × the 1536 resident at 6/CU).
-    auto resident = [&](const void* fn) {
-        int perCU = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, fn, 256, 0) != hipSuccess || perCU <= 0) perCU = 4;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
-        return dim3((unsigned)(perCU * cus));
-    };
     const char* ePers = getenv("PBR_RESIDENT_GRID");
     const bool pers = !(ePers && ePers[0] == '0');
-    const dim3 gShadow = pers ? resident(shortStack ? (const void*)k_wf_shadow<kShortStack> : (const void*)k_wf_shadow<0>) : gstride;
-    const dim3 gExtend = pers ? resident(shortStack ? (const void*)k_wf_extend<kShortStack> : (const void*)k_wf_extend<0>) : gstride;
-    for (long long p0 = 0; p0 < P.nPixels; p0 += chunkPix) {
+    const dim3 gShadow = pers ? resident_grid(ctx, shortStack ? (const void*)k_wf_shadow<kShortStack> : (const void*)k_wf_shadow<0>) : gstride;
+    const dim3 gExtend = pers ? resident_grid(ctx, shortStack ? (const void*)k_wf_extend<kShortStack> : (const void*)k_wf_extend<0>) : gstride;
+    if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
+    int chunk = 0;
+    for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
+        const int l = chunk % ch.lanes;
+        const hipStream_t st = l ? ctx->side : s;
+        WfParams& W = WL[l];
         W.chunkPix0 = p0;
-        W.chunkPix = (int)std::min<long long>(chunkPix, P.nPixels - p0);
+        W.chunkPix = (int)std::min<long long>(ch.chunkPix, P.nPixels - p0);
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
-        W.cur = queue(0);
-        if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
-        else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, s, W);
-        // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
-        const int maxLevels = levels + (ctx->host.anyNoMaterial ? 2 : 0);
+        W.cur = queue(l, 0);
+        if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
+        else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
+        const hipStream_t sst = shadowOverlap ? ctx->shadowStream[l] : st;
+        WfBufs& B = ctx->wb[l];
         for (int level = 0; level < maxLevels; ++level) {
-            W.cur = queue(cur);
-            W.next = queue(cur ^ 1);
+            W.cur = queue(l, cur);
+            W.next = queue(l, cur ^ 1);
+            if (shadowOverlap) {
+                const bool odd = level & 1;
+                W.so = (float4*)(odd ? B.wsO2.p : B.wsO.p); W.sd = (float4*)(odd ? B.wsD2.p : B.wsD.p);
+                W.sc = (float4*)(odd ? B.wsC2.p : B.wsC.p); W.sid = (int*)(odd ? B.wsId2.p : B.wsId.p);
+                W.shadowSeg = cntL[l] + (odd ? 3 : 2) * kWfBlocks;
+                // shade(L) refills the queue shadow(L-2) read
+                if (level >= 2) HIP_TRY(hipStreamWaitEvent(st, ctx->evShadow[l][level - 2], 0));
+            }
             const int l0 = level == 0 ? 1 : 0;
-            if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, s, W, l0);
-            else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, s, W, l0);
-            else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, s, W, l0);
-            else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, s, W, l0);
-            if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, s, W);
-            else hipLaunchKernelGGL(k_wf_shadow<0>, gShadow, blk, 0, s, W);
+            if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
+            else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
+            else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, st, W, l0);
+            else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, st, W, l0);
+            if (shadowOverlap) {
+                HIP_TRY(hipEventRecord(ctx->evShade[l][level], st));
+                HIP_TRY(hipStreamWaitEvent(sst, ctx->evShade[l][level], 0));
+            }
+            if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, sst, W);
+            else hipLaunchKernelGGL(k_wf_shadow<0>, gShadow, blk, 0, sst, W);
+            if (shadowOverlap) HIP_TRY(hipEventRecord(ctx->evShadow[l][level], sst));
             if (level + 1 == maxLevels) break;
             cur ^= 1;
-            W.cur = queue(cur);
-            if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, s, W);
-            else hipLaunchKernelGGL(k_wf_extend<0>, gExtend, blk, 0, s, W);
+            W.cur = queue(l, cur);
+            if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W);
+            else hipLaunchKernelGGL(k_wf_extend<0>, gExtend, blk, 0, st, W);
         }
+        // the fold reads every level's records: after the last shadow launch (stream order on sst)
+        if (shadowOverlap) HIP_TRY(hipStreamWaitEvent(st, ctx->evShadow[l][maxLevels - 1], 0));
         const int pb = finish_pixels(spp);
-        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + pb - 1) / pb), blk, 0, s, W);
+        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + pb - 1) / pb), blk, 0, st, W);
     }
     HIP_TRY(hipGetLastError());
-    return PBR_OK;
+    return wf_join(ctx, s, ch.lanes);
 }
 
 // Wavefront Path: per bounce shade → shadow → probe → resolve → extend (pbr_wavefront_path.h).
 int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol) {
     const int spp = P.spp;
-    int chunkLog2 = 25;   // ≈ 290 B of queues + state per sample: 9.7 GB per chunk
-    if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
-    long long chunkPix = std::max(1LL, (1LL << chunkLog2) / spp);
-    if (chunkPix > P.nPixels) chunkPix = P.nPixels;
-    const size_t cap = (size_t)chunkPix * spp;
-    const int segCap = (int)((cap + (size_t)kWfBlocks * 256 - 1) / ((size_t)kWfBlocks * 256) * 256);
-    const size_t qcap = std::max(cap, (size_t)segCap * kWfBlocks);
-    for (int k = 0; k < 2; ++k) {
-        HIP_TRY(ctx->wqO[k].ensure(qcap * 16)); HIP_TRY(ctx->wqD[k].ensure(qcap * 16));
-        HIP_TRY(ctx->wqId[k].ensure(qcap * 4)); HIP_TRY(ctx->wqHit[k].ensure(qcap * 16));
-    }
-    HIP_TRY(ctx->wsO.ensure(qcap * 16)); HIP_TRY(ctx->wsD.ensure(qcap * 16)); HIP_TRY(ctx->wsId.ensure(qcap * 4));
-    HIP_TRY(ctx->wpO.ensure(qcap * 16)); HIP_TRY(ctx->wpD.ensure(qcap * 16)); HIP_TRY(ctx->wpId.ensure(qcap * 4));
-    HIP_TRY(ctx->wdId.ensure(qcap * 4));
-    HIP_TRY(ctx->sL.ensure(cap * 16)); HIP_TRY(ctx->sBeta.ensure(cap * 16));
-    HIP_TRY(ctx->rA.ensure(cap * 16)); HIP_TRY(ctx->rB.ensure(cap * 16)); HIP_TRY(ctx->rBeta.ensure(cap * 16));
-    HIP_TRY(ctx->rLi.ensure(cap * 16)); HIP_TRY(ctx->rFlags.ensure(cap * 4)); HIP_TRY(ctx->rLight.ensure(cap * 4));
-    HIP_TRY(ctx->wIndex.ensure(cap * 4));
-    HIP_TRY(ctx->wCnt.ensure(6 * kWfBlocks * sizeof(int)));
-    int* cnt = (int*)ctx->wCnt.p;   // segment counts: ray queues 0/1, shadow, probe, direct, Tr walk
-    WfvParams V;
-    std::memset(&V, 0, sizeof(V));
-    WfpParams& X = V.X;
-    WfParams& W = X.W;
-    if (vol) {
-        HIP_TRY(ctx->wtO.ensure(qcap * 16)); HIP_TRY(ctx->wtD.ensure(qcap * 16)); HIP_TRY(ctx->wtP.ensure(qcap * 16));
-        HIP_TRY(ctx->wtE.ensure(qcap * 16)); HIP_TRY(ctx->wtN.ensure(qcap * 16)); HIP_TRY(ctx->wtId.ensure(qcap * 4));
-        HIP_TRY(ctx->rLiA.ensure(cap * 16)); HIP_TRY(ctx->rTr.ensure(cap * 16)); HIP_TRY(ctx->rWA.ensure(cap * 4));
-        V.to = (float4*)ctx->wtO.p; V.td = (float4*)ctx->wtD.p; V.tp = (float4*)ctx->wtP.p;
-        V.te = (float4*)ctx->wtE.p; V.tn = (float4*)ctx->wtN.p; V.tid = (int*)ctx->wtId.p;
-        V.trSeg = cnt + 5 * kWfBlocks;
-        V.dLiA = (float4*)ctx->rLiA.p; V.dTr = (float4*)ctx->rTr.p; V.dWA = (float*)ctx->rWA.p;
-    }
-    W.P = P;
-    W.so = (float4*)ctx->wsO.p; W.sd = (float4*)ctx->wsD.p; W.sid = (int*)ctx->wsId.p;
-    W.shadowSeg = cnt + 2 * kWfBlocks;
-    W.segCap = segCap;
-    W.sampleIndex = (uint32_t*)ctx->wIndex.p;
-    W.cap = (int)cap;
-    X.po = (float4*)ctx->wpO.p; X.pd = (float4*)ctx->wpD.p; X.pid = (int*)ctx->wpId.p;
-    X.probeSeg = cnt + 3 * kWfBlocks;
-    X.directId = (int*)ctx->wdId.p;
-    X.directSeg = cnt + 4 * kWfBlocks;
-    X.stL = (float4*)ctx->sL.p; X.stBeta = (float4*)ctx->sBeta.p;
-    X.dA = (float4*)ctx->rA.p; X.dB = (float4*)ctx->rB.p; X.dBeta = (float4*)ctx->rBeta.p; X.dLi = (float4*)ctx->rLi.p;
-    X.dFlags = (int*)ctx->rFlags.p; X.dLight = (int*)ctx->rLight.p;
-    HIP_TRY(hipMemsetAsync(X.dFlags, 0, cap * 4, s));
-    // Path: 5 camera dims + per bounce 1 + 2 + 2 (light) + 2 (BSDF) + 1 (RR)
-    W.P.smp.ldsDims = std::min(kLdsDims, 5 + 8 * std::max(1, P.maxDepth) + 2);
-    if (const char* e = getenv("PBR_HALTON_LDS")) if (e[0] == '0') W.P.smp.ldsDims = 0;
+    const WfChunks ch = wf_chunks(P);   // ≈ 290 B of queues + state per sample: 9.7 GB per 2^25 chunk
+    const size_t cap = ch.cap, qcap = ch.qcap;
     int lobes = 0;
     for (const MatTemplate& m : ctx->host.materials)
         for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
     const bool simple = (lobes & ~kSimpleLobes) == 0;
     const char* eMats = getenv("PBR_MATS_LDS");
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
-    auto queue = [&](int k) {
+    WfvParams VL[kWfLanes];
+    int* cntL[kWfLanes];
+    for (int l = 0; l < ch.lanes; ++l) {
+        WfBufs& B = ctx->wb[l];
+        for (int k = 0; k < 2; ++k) {
+            HIP_TRY(B.wqO[k].ensure(qcap * 16)); HIP_TRY(B.wqD[k].ensure(qcap * 16));
+            HIP_TRY(B.wqId[k].ensure(qcap * 4)); HIP_TRY(B.wqHit[k].ensure(qcap * 16));
+        }
+        HIP_TRY(B.wsO.ensure(qcap * 16)); HIP_TRY(B.wsD.ensure(qcap * 16)); HIP_TRY(B.wsId.ensure(qcap * 4));
+        HIP_TRY(B.wpO.ensure(qcap * 16)); HIP_TRY(B.wpD.ensure(qcap * 16)); HIP_TRY(B.wpId.ensure(qcap * 4));
+        HIP_TRY(B.wdId.ensure(qcap * 4));
+        HIP_TRY(B.sL.ensure(cap * 16)); HIP_TRY(B.sBeta.ensure(cap * 16));
+        HIP_TRY(B.rA.ensure(cap * 16)); HIP_TRY(B.rB.ensure(cap * 16)); HIP_TRY(B.rBeta.ensure(cap * 16));
+        HIP_TRY(B.rLi.ensure(cap * 16)); HIP_TRY(B.rFlags.ensure(cap * 4)); HIP_TRY(B.rLight.ensure(cap * 4));
+        HIP_TRY(B.wIndex.ensure(cap * 4));
+        HIP_TRY(B.wCnt.ensure(6 * kWfBlocks * sizeof(int)));
+        int* cnt = cntL[l] = (int*)B.wCnt.p;   // segment counts: ray queues 0/1, shadow, probe, direct, Tr walk
+        WfvParams& V = VL[l];
+        std::memset(&V, 0, sizeof(V));
+        WfpParams& X = V.X;
+        WfParams& W = X.W;
+        if (vol) {
+            HIP_TRY(B.wtO.ensure(qcap * 16)); HIP_TRY(B.wtD.ensure(qcap * 16)); HIP_TRY(B.wtP.ensure(qcap * 16));
+            HIP_TRY(B.wtE.ensure(qcap * 16)); HIP_TRY(B.wtN.ensure(qcap * 16)); HIP_TRY(B.wtId.ensure(qcap * 4));
+            HIP_TRY(B.rLiA.ensure(cap * 16)); HIP_TRY(B.rTr.ensure(cap * 16)); HIP_TRY(B.rWA.ensure(cap * 4));
+            V.to = (float4*)B.wtO.p; V.td = (float4*)B.wtD.p; V.tp = (float4*)B.wtP.p;
+            V.te = (float4*)B.wtE.p; V.tn = (float4*)B.wtN.p; V.tid = (int*)B.wtId.p;
+            V.trSeg = cnt + 5 * kWfBlocks;
+            V.dLiA = (float4*)B.rLiA.p; V.dTr = (float4*)B.rTr.p; V.dWA = (float*)B.rWA.p;
+        }
+        W.P = P;
+        W.so = (float4*)B.wsO.p; W.sd = (float4*)B.wsD.p; W.sid = (int*)B.wsId.p;
+        W.shadowSeg = cnt + 2 * kWfBlocks;
+        W.segCap = ch.segCap;
+        W.sampleIndex = (uint32_t*)B.wIndex.p;
+        W.cap = (int)cap;
+        X.po = (float4*)B.wpO.p; X.pd = (float4*)B.wpD.p; X.pid = (int*)B.wpId.p;
+        X.probeSeg = cnt + 3 * kWfBlocks;
+        X.directId = (int*)B.wdId.p;
+        X.directSeg = cnt + 4 * kWfBlocks;
+        X.stL = (float4*)B.sL.p; X.stBeta = (float4*)B.sBeta.p;
+        X.dA = (float4*)B.rA.p; X.dB = (float4*)B.rB.p; X.dBeta = (float4*)B.rBeta.p; X.dLi = (float4*)B.rLi.p;
+        X.dFlags = (int*)B.rFlags.p; X.dLight = (int*)B.rLight.p;
+        HIP_TRY(hipMemsetAsync(X.dFlags, 0, cap * 4, s));
+        // Path: 5 camera dims + per bounce 1 + 2 + 2 (light) + 2 (BSDF) + 1 (RR)
+        W.P.smp.ldsDims = std::min(kLdsDims, 5 + 8 * std::max(1, P.maxDepth) + 2);
+        if (const char* e = getenv("PBR_HALTON_LDS")) if (e[0] == '0') W.P.smp.ldsDims = 0;
+    }
+    auto queue = [&](int l, int k) {
+        WfBufs& B = ctx->wb[l];
         WfQueue q;
-        q.o = (float4*)ctx->wqO[k].p; q.d = (float4*)ctx->wqD[k].p; q.id = (int*)ctx->wqId[k].p; q.hit = (float4*)ctx->wqHit[k].p;
-        q.segCount = cnt + k * kWfBlocks;
+        q.o = (float4*)B.wqO[k].p; q.d = (float4*)B.wqD[k].p; q.id = (int*)B.wqId[k].p; q.hit = (float4*)B.wqHit[k].p;
+        q.segCount = cntL[l] + k * kWfBlocks;
         return q;
     };
-    auto resident = [&](const void* fn) {
-        int perCU = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, fn, 256, 0) != hipSuccess || perCU <= 0) perCU = 4;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
-        return dim3((unsigned)(perCU * cus));
-    };
     const dim3 blk(256), gshade(kWfBlocks);
-    const dim3 gShadow = resident((const void*)k_wfp_shadow<kShortStack>), gProbe = resident((const void*)k_wfp_probe<kShortStack>);
-    const dim3 gExtend = resident((const void*)k_wf_extend<kShortStack>), gResolve = resident((const void*)k_wfp_resolve);
+    const dim3 gShadow = resident_grid(ctx, (const void*)k_wfp_shadow<kShortStack>);
+    const dim3 gProbe = resident_grid(ctx, (const void*)k_wfp_probe<kShortStack>);
+    const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack>);
+    const dim3 gResolve = resident_grid(ctx, (const void*)k_wfp_resolve);
     const int maxLevels = std::max(1, P.maxDepth) + 1 + (ctx->host.anyNoMaterial ? 8 : 0);
-    for (long long p0 = 0; p0 < P.nPixels; p0 += chunkPix) {
+    if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
+    int chunk = 0;
+    for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
+        const int l = chunk % ch.lanes;
+        const hipStream_t st = l ? ctx->side : s;
+        WfvParams& V = VL[l];
+        WfpParams& X = V.X;
+        WfParams& W = X.W;
         W.chunkPix0 = p0;
-        W.chunkPix = (int)std::min<long long>(chunkPix, P.nPixels - p0);
+        W.chunkPix = (int)std::min<long long>(ch.chunkPix, P.nPixels - p0);
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
-        W.cur = queue(0);
-        hipLaunchKernelGGL(k_wfp_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, s, X);
+        W.cur = queue(l, 0);
+        hipLaunchKernelGGL(k_wfp_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, X);
         for (int level = 0; level < maxLevels; ++level) {
-            W.cur = queue(cur);
-            W.next = queue(cur ^ 1);
+            W.cur = queue(l, cur);
+            W.next = queue(l, cur ^ 1);
             const int l0 = level == 0 ? 1 : 0;
             if (vol) {
-                if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, s, V, l0);
-                else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, s, V, l0);
-                else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, s, V, l0);
-                else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, s, V, l0);
-                hipLaunchKernelGGL(k_wfv_tr<kShortStack>, gShadow, blk, 0, s, V);
-                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, s, X);
-                hipLaunchKernelGGL(k_wfv_resolve, gResolve, blk, 0, s, V);
+                if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0);
+                else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, st, V, l0);
+                else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0);
+                else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0);
+                hipLaunchKernelGGL(k_wfv_tr<kShortStack>, gShadow, blk, 0, st, V);
+                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, st, X);
+                hipLaunchKernelGGL(k_wfv_resolve, gResolve, blk, 0, st, V);
             } else {
-                if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, s, X, l0);
-                else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, s, X, l0);
-                else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, s, X, l0);
-                else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, s, X, l0);
-                hipLaunchKernelGGL(k_wfp_shadow<kShortStack>, gShadow, blk, 0, s, X);
-                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, s, X);
-                hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, s, X);
+                if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
+                else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0);
+                else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, st, X, l0);
+                else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, st, X, l0);
+                hipLaunchKernelGGL(k_wfp_shadow<kShortStack>, gShadow, blk, 0, st, X);
+                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, st, X);
+                hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, st, X);
             }
             if (level + 1 == maxLevels) break;
             cur ^= 1;
-            W.cur = queue(cur);
-            hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, s, W);
+            W.cur = queue(l, cur);
+            hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W);
         }
         const int pb = finish_pixels(spp);
-        hipLaunchKernelGGL(k_wfp_finish, dim3((W.chunkPix + pb - 1) / pb), blk, 0, s, X);
+        hipLaunchKernelGGL(k_wfp_finish, dim3((W.chunkPix + pb - 1) / pb), blk, 0, st, X);
     }
     HIP_TRY(hipGetLastError());
-    return PBR_OK;
+    return wf_join(ctx, s, ch.lanes);
 }
 
 }  // namespace
@@ -1019,6 +1123,18 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)drain(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    for (int l = 0; l < kWfLanes; ++l) {
+        if (ctx->shadowStream[l]) (void)hipStreamSynchronize(ctx->shadowStream[l]);
+        for (int k = 0; k < kWfMaxDepth + 2; ++k) {
+            if (ctx->evShade[l][k]) (void)hipEventDestroy(ctx->evShade[l][k]);
+            if (ctx->evShadow[l][k]) (void)hipEventDestroy(ctx->evShadow[l][k]);
+        }
+        if (ctx->shadowStream[l]) (void)hipStreamDestroy(ctx->shadowStream[l]);
+    }
+    if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
+    if (ctx->evJoin) (void)hipEventDestroy(ctx->evJoin);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     hipStream_t s = ctx->stream;

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--lib", default=None, help="an experimental build of libpbr_hip.so")
     ap.add_argument("--shard", default=None, help="R/N: render only rank R's tiles of an N-GPU job "
                                                    "(per-rank frame time of the sharded bench)")
+    ap.add_argument("--tile", type=int, default=64, help="tile edge of the --shard partition")
     ap.add_argument("variants", nargs="*", default=[""])
     a = ap.parse_args()
     if a.lib:
@@ -35,7 +36,7 @@ def main():
     npx = W * H
     if a.shard:
         rk, n = (int(x) for x in a.shard.split("/"))
-        tiles = tiles_for_rank(W, H, rk, n)
+        tiles = tiles_for_rank(W, H, rk, n, a.tile)
         rd = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
                                 rd.sampler, tiles=tiles)
         npx = sum((t[2] - t[0]) * (t[3] - t[1]) for t in tiles)
@@ -64,7 +65,7 @@ def main():
         if ref is None:
             ref = out
         m = float(np.median(ms))
-        tag = f" shard {a.shard} ({npx} px)" if a.shard else ""
+        tag = f" shard {a.shard} tile {a.tile} ({npx} px)" if a.shard else ""
         print(f"{a.config}{tag} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  "
               f"{npx * spp / m / 1e3:8.1f} Msamples/s  {same}", flush=True)
         for k, old in saved.items():
