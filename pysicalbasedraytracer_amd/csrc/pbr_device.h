@@ -223,6 +223,96 @@ constexpr int kShortStack = PBR_SHORT_STACK_DEPTH;
 __shared__ int s_trav_ref[kShortStack * 256];
 __shared__ float s_trav_t[kShortStack * 256];
 
+// The binary traversal below over the quad layout of build_quad_nodes: one node fetch covers two
+// binary levels, halving the chain of dependent node loads per ray.  Visit order stays BVHAccel's:
+// at binary node N with near child A (dirIsNeg[axN] order) the reference visits A's near and far
+// children, then B's, each gated by its box test against the tMax current at that point.  The four
+// slots are ordered the same way from the direction signs of (axN, axA, axB); the first one whose
+// slab passes with tEnter < tMax is visited now (the reference visits it after A's test, which
+// the nested boxes make pass — a slot box lies inside its parent's, and the slab test is monotone
+// in the box) and the passing slots after it are pushed far-last, each re-tested against tMax
+// when popped — the moment the reference would test it.  Slots that fail now would fail later
+// (tMax only shrinks), so primitive tests run in exactly the reference's order (F8 ties).
+#ifndef PBR_QUAD_TRAVERSAL
+#define PBR_QUAD_TRAVERSAL 1
+#endif
+constexpr bool kQuadTraversal = PBR_QUAD_TRAVERSAL != 0;
+template <bool ANY, int SHORT>
+__device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, bool n0, bool n1, bool n2) {
+    int stackRef[64 - SHORT];
+    float stackT[64 - SHORT];
+    int* lref = nullptr;
+    float* lt = nullptr;
+    if constexpr (SHORT > 0) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
+    auto push = [&](int ref, float t, int sp) {
+        if (SHORT && sp < SHORT) { lref[sp * 256] = ref; lt[sp * 256] = t; }
+        else { stackRef[sp - SHORT] = ref; stackT[sp - SHORT] = t; }
+    };
+    auto neg = [&](int axis) { return axis == 0 ? n0 : (axis == 1 ? n1 : n2); };
+    int cur = S.quadRootRef, sp = 0;
+    bool found = false;
+    while (true) {
+        if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
+            int slot = cur & 0x7fffffff;
+            while (true) {
+                const float4* tv = S.triVerts + 3 * (size_t)slot;
+                float4 v0 = tv[0], v1 = tv[1], v2 = tv[2];
+                int flags = __float_as_int(v0.w);
+                float t, b0 = 0, b1 = 0, b2 = 0;
+                bool hit = (flags & PRIM_SPHERE)
+                               ? sphere_test(S.spheres[__float_as_int(v0.x)], r, &t)
+                               : tri_test(mk(v0.x, v0.y, v0.z), mk(v1.x, v1.y, v1.z), mk(v2.x, v2.y, v2.z), r, &t, &b0, &b1, &b2);
+                if (hit) {
+                    if (ANY) return true;
+                    r.tMax = t;   // GeometricPrimitive::Intersect (Primitive.cpp:26)
+                    h->slot = slot; h->b0 = b0; h->b1 = b1; h->b2 = b2;
+                    found = true;
+                }
+                if (flags & PRIM_LEAF_END) break;
+                ++slot;
+            }
+        } else {
+            const float4* w = S.quad + 8 * (size_t)cur;
+            float4 LX = w[0], LY = w[1], LZ = w[2], HX = w[3], HY = w[4], HZ = w[5], R = w[6], M = w[7];
+            const int meta = __float_as_int(M.x);
+            float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+            bool k0 = node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t0) & ((meta >> 8) & 1);
+            bool k1 = node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t1) & ((meta >> 9) & 1);
+            bool k2 = node_slab(mk(LX.z, LY.z, LZ.z), mk(HX.z, HY.z, HZ.z), r, inv, n0, n1, n2, &t2) & ((meta >> 10) & 1);
+            bool k3 = node_slab(mk(LX.w, LY.w, LZ.w), mk(HX.w, HY.w, HZ.w), r, inv, n0, n1, n2, &t3) & ((meta >> 11) & 1);
+            int r0 = __float_as_int(R.x), r1 = __float_as_int(R.y), r2 = __float_as_int(R.z), r3 = __float_as_int(R.w);
+            auto swp = [](bool c, auto& a, auto& b) { auto x = c ? b : a; b = c ? a : b; a = x; };
+            const bool sA = neg((meta >> 2) & 3), sB = neg((meta >> 4) & 3), sN = neg(meta & 3);
+            swp(sA, k0, k1); swp(sA, t0, t1); swp(sA, r0, r1);
+            swp(sB, k2, k3); swp(sB, t2, t3); swp(sB, r2, r3);
+            swp(sN, k0, k2); swp(sN, t0, t2); swp(sN, r0, r2);
+            swp(sN, k1, k3); swp(sN, t1, t3); swp(sN, r1, r3);
+            const float tM = r.tMax;
+            const bool p0 = k0 && t0 < tM, p1 = k1 && t1 < tM, p2 = k2 && t2 < tM, p3 = k3 && t3 < tM;
+            if (p0 | p1 | p2 | p3) {
+                if (sp > 64 - 3) break;   // never reached: SAH trees here stay < 30 binary levels
+                const int first = p0 ? 0 : (p1 ? 1 : (p2 ? 2 : 3));
+                if (p3 && first < 3) push(r3, t3, sp++);
+                if (p2 && first < 2) push(r2, t2, sp++);
+                if (p1 && first < 1) push(r1, t1, sp++);
+                cur = first == 0 ? r0 : (first == 1 ? r1 : (first == 2 ? r2 : r3));
+                continue;
+            }
+        }
+        bool more = false;   // pop until an entry passes its box test against the current tMax
+        while (sp > 0) {
+            --sp;
+            int rr;
+            float tt;
+            if (SHORT && sp < SHORT) { rr = lref[sp * 256]; tt = lt[sp * 256]; }
+            else { rr = stackRef[sp - SHORT]; tt = stackT[sp - SHORT]; }
+            if (tt < r.tMax) { cur = rr; more = true; break; }
+        }
+        if (!more) break;
+    }
+    return found;
+}
+
 // BVHAccel::Intersect / IntersectP (BVHAccel.cpp:285-366) over the wide layout of
 // build_wide_nodes.  The reference pops a node and tests its box against the current ray.tMax;
 // since only the last comparison of that test reads ray.tMax (Geometry.h:1438-1468), the slab part
@@ -247,6 +337,7 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
         if (STATS) c->nodes++;
         if (!node_hit(a, b, r, inv, n0, n1, n2)) return false;
     }
+    if constexpr (!STATS && kQuadTraversal) return traverse_quad<ANY, SHORT>(S, r, h, inv, n0, n1, n2);
     int stackRef[64 - SHORT];
     float stackT[64 - SHORT];
     int* lref = nullptr;

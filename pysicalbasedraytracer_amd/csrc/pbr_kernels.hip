@@ -630,7 +630,7 @@ struct pbr_hip_ctx {
     bool haveScene = false;
     HostScene host;
     HaltonTables halton;
-    DevBuf dNodes, dWide, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
+    DevBuf dNodes, dWide, dQuad, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dSobol, dSobolPix;          // active Sobol matrices, pixel tables
     std::vector<uint32_t> sobolBuiltin;
@@ -678,6 +678,8 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     S.nodes = (const float4*)ctx->dNodes.p;
     S.wide = (const float4*)ctx->dWide.p;
     S.rootRef = h.rootRef;
+    S.quad = (const float4*)ctx->dQuad.p;
+    S.quadRootRef = h.quadRootRef;
     S.triVerts = (const float4*)ctx->dTri.p;
     S.primInfo = (const int4*)ctx->dInfo.p;
     S.triUV = h.triUV.empty() ? nullptr : (const float2*)ctx->dUV.p;
@@ -1158,6 +1160,7 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     const HostScene& h = ctx->host;
     HIP_TRY(ctx->dNodes.upload(h.nodes, ctx->stream));
     HIP_TRY(ctx->dWide.upload(h.wide, ctx->stream));
+    HIP_TRY(ctx->dQuad.upload(h.quad, ctx->stream));
     HIP_TRY(ctx->dTri.upload(h.triVerts, ctx->stream));
     HIP_TRY(ctx->dInfo.upload(h.primInfo, ctx->stream));
     HIP_TRY(ctx->dUV.upload(h.triUV, ctx->stream));

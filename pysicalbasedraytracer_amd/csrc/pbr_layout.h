@@ -60,6 +60,8 @@ struct DeviceScene {
     const float4* nodes;
     const float4* wide;            // 4 float4 per interior node: child boxes, child refs, axis
     int rootRef;
+    const float4* quad;            // 8 float4 per quad node (two binary levels, pbr_scene.cpp build_quad_nodes)
+    int quadRootRef;
     const float4* triVerts;
     const int4* primInfo;
     const float2* triUV;

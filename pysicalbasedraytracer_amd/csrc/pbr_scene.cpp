@@ -54,6 +54,72 @@ struct PrimRef { int shape, tri; };
 
 void fail(const std::string& why) { throw std::invalid_argument(why); }
 
+// The same tree collapsed two levels at a time for the closest/any-hit traversal (pbr_device.h
+// traverse_quad): a quad node stands for binary interior node N and holds the boxes of N's
+// grandchildren — or of a child itself where that child is a leaf — in the slots
+// [A.near-side, A.far-side, B.near-side, B.far-side] (A = N's first child, B = its second), plus
+// the split axes of N, A and B, so the traversal recovers BVHAccel's near-first order from the
+// ray's direction signs.  Layout, 8 float4 (128 B, one L2 line) per node:
+//   [0..5] lo.x, lo.y, lo.z, hi.x, hi.y, hi.z of the four slots (SoA)
+//   [6]    slot references: quad-node index, or kLeafRef | first primitive slot
+//   [7]    .x = axN | axA << 2 | axB << 4 | validMask << 8 (slot 1 / 3 is empty when A / B is a leaf)
+// The child boxes are nested inside their parent's, so a slot that passes its slab test implies
+// the skipped parent test passes too; primitive tests keep the reference's order (see traverse_quad).
+template <class Ref>
+void build_quad_nodes(HostScene* S, Ref&& binRef) {
+    const std::vector<LinearBVHNode>& L = S->nodes;
+    S->quad.clear();
+    S->quadRootRef = binRef(0);
+    if (L.empty() || L[0].nPrimitives > 0) return;
+    std::vector<int32_t> qid(L.size(), -1);
+    int nQuad = 0;
+    // quad nodes exist for the root and every interior grandchild of a quad node (preorder)
+    std::vector<int> todo{0};
+    std::vector<int> order;
+    while (!todo.empty()) {
+        int i = todo.back();
+        todo.pop_back();
+        qid[i] = nQuad++;
+        order.push_back(i);
+        int kids[2] = {i + 1, L[i].offset};
+        for (int k = 1; k >= 0; --k) {
+            int c = kids[k];
+            if (L[c].nPrimitives > 0) continue;
+            int g[2] = {c + 1, L[c].offset};
+            for (int m = 1; m >= 0; --m)
+                if (L[g[m]].nPrimitives == 0) todo.push_back(g[m]);
+        }
+    }
+    auto ref = [&](int i) -> int32_t { return L[i].nPrimitives > 0 ? binRef(i) : qid[i]; };
+    S->quad.assign((size_t)nQuad * 32, 0.f);
+    for (int i : order) {
+        float* w = &S->quad[(size_t)qid[i] * 32];
+        int kids[2] = {i + 1, L[i].offset};
+        int32_t refs[4] = {0, 0, 0, 0};
+        int axes[2] = {0, 0}, mask = 0;
+        for (int k = 0; k < 2; ++k) {
+            int c = kids[k];
+            int slots[2] = {-1, -1};
+            if (L[c].nPrimitives > 0) slots[0] = c;
+            else { slots[0] = c + 1; slots[1] = L[c].offset; axes[k] = L[c].axis; }
+            for (int m = 0; m < 2; ++m) {
+                int s = 2 * k + m, n = slots[m];
+                if (n < 0) {   // empty slot: an inverted box, never tested (validMask)
+                    for (int a = 0; a < 3; ++a) { w[4 * a + s] = 1.f; w[12 + 4 * a + s] = -1.f; }
+                    continue;
+                }
+                for (int a = 0; a < 3; ++a) { w[4 * a + s] = L[n].pMin[a]; w[12 + 4 * a + s] = L[n].pMax[a]; }
+                refs[s] = ref(n);
+                mask |= 1 << s;
+            }
+        }
+        std::memcpy(&w[24], refs, 16);
+        int32_t meta = (int32_t)L[i].axis | axes[0] << 2 | axes[1] << 4 | mask << 8;
+        std::memcpy(&w[28], &meta, 4);
+    }
+    S->quadRootRef = qid[0];
+}
+
 // The same tree re-laid out for traversal: each interior node carries both children's boxes (so a
 // child is box-tested from its parent, before its own record is fetched) and child references
 // (interior rank, or kLeafRef | first primitive slot).  The last primitive of every leaf gets
@@ -96,6 +162,7 @@ void build_wide_nodes(HostScene* S) {
         std::memcpy(&w[14], &ax, 4);
     }
     S->rootRef = ref(0);
+    build_quad_nodes(S, ref);
 }
 
 // Bucketed SAH builder writing LinearBVHNodes in depth-first preorder.

@@ -38,6 +38,8 @@ struct HostScene {
     bool anyNoMaterial = false;             // some primitive has material == nullptr
     std::vector<float> wide;                // 16 floats per interior node (build_wide_nodes)
     int32_t rootRef = 0;
+    std::vector<float> quad;                // 32 floats per quad node (build_quad_nodes)
+    int32_t quadRootRef = 0;
 };
 
 // Throws std::invalid_argument on a malformed descriptor.

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--shard", default=None, help="R/N: render only rank R's tiles of an N-GPU job "
                                                    "(per-rank frame time of the sharded bench)")
     ap.add_argument("--tile", type=int, default=64, help="tile edge of the --shard partition")
+    ap.add_argument("--ref-file", default=None, help=".npy frame to compare against (written if absent), "
+                                                     "so experimental builds can be checked against each other")
     ap.add_argument("variants", nargs="*", default=[""])
     a = ap.parse_args()
     if a.lib:
@@ -47,6 +49,8 @@ def main():
     rgb = torch.empty((npx, 3), dtype=torch.float32, device=dev)
     rgba = torch.empty((npx, 4), dtype=torch.uint8, device=dev)
     ref = None
+    if a.ref_file and os.path.exists(a.ref_file):
+        ref = np.load(a.ref_file)
     for v in a.variants:
         env = dict(kv.split("=") for kv in v.split(",") if kv)
         saved = {k: os.environ.get(k) for k in env}
@@ -64,6 +68,8 @@ def main():
                                           else "DIFFERENT max|d|=%g" % np.abs(out - ref).max())
         if ref is None:
             ref = out
+            if a.ref_file:
+                np.save(a.ref_file, out)
         m = float(np.median(ms))
         tag = f" shard {a.shard} tile {a.tile} ({npx} px)" if a.shard else ""
         print(f"{a.config}{tag} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  "
