@@ -314,6 +314,20 @@ class SkyBoxLight : public Light {   // Light/SkyBoxLight.h
     std::vector<float> data;
 };
 
+class InfiniteAreaLight : public Light {   // Light/InfiniteAreaLight.h
+  public:
+    // Loads texmap the way stbi_loadf does: rows flipped only if a SkyBoxLight has already set
+    // stb's global stbi_set_flip_vertically_on_load(true) (SkyBoxLight.cpp:20); "" → constant power.
+    InfiniteAreaLight(const Transform& LightToWorld, const Spectrum& power, int nSamples, const std::string& texmap);
+    // In-memory variant: data = width*height*components floats in stbi_loadf's row order (empty → constant).
+    InfiniteAreaLight(const Transform& LightToWorld, const Spectrum& power, int nSamples, int width, int height,
+                      int components, std::vector<float> data);
+    bool IsInfinite() const override { return true; }
+    const Spectrum L;
+    int imageWidth = 0, imageHeight = 0, nrComponents = 0;
+    std::vector<float> data;
+};
+
 // ---------------------------------------------------------------------------- Core/Primitive.h
 class Primitive {
   public:

@@ -59,7 +59,10 @@ enum pbr_material_type {
 enum pbr_light_type {
     PBR_LIGHT_POINT = 0,        /* Light/PointLight.cpp */
     PBR_LIGHT_DIFFUSE_AREA = 1, /* Light/DiffuseLight.cpp */
-    PBR_LIGHT_SKYBOX = 2        /* Light/SkyBoxLight.cpp */
+    PBR_LIGHT_SKYBOX = 2,       /* Light/SkyBoxLight.cpp */
+    PBR_LIGHT_INFINITE_AREA = 3 /* Light/InfiniteAreaLight.cpp: light_to_world, Le = the `power`
+                                 * scale, n_samples, env_* = the image as stbi_loadf returned it
+                                 * (NULL → a 1x1 map of Le); worldRadius from the scene bounds */
 };
 enum pbr_integrator_type {
     PBR_INTEGRATOR_WHITTED = 0, /* Integrator/WhittedIntegrator.cpp:11-65 */

@@ -38,6 +38,7 @@ inline float t_log(float x) { return (float)std::log((double)x); }
 inline float t_pow(float x, float y) { return (float)std::pow((double)x, (double)y); }
 inline float t_atan2(float y, float x) { return (float)std::atan2((double)y, (double)x); }
 inline float t_asin(float x) { return (float)std::asin((double)x); }
+inline float t_acos(float x) { return (float)std::acos((double)x); }
 
 // std::min / std::max / Clamp semantics (NaN-sensitive order), Core/PBR.h:183-191
 inline float fmin_(float a, float b) { return (b < a) ? b : a; }

@@ -3,6 +3,7 @@
 // file:line it follows. See pbr_oracle.h for the pinning story and the documented deviations.
 #include "pbr_oracle.h"
 #include "orc_core.h"
+#include "orc_envmap.h"
 
 #include <chrono>
 #include <memory>
@@ -62,6 +63,10 @@ struct Light {
     int w = 0, h = 0, comps = 0;
     std::vector<float> data;
     int medIn = -1, medOut = -1;
+    // InfiniteAreaLight (Light/InfiniteAreaLight.h:11-45); built by Preprocess once the BVH exists
+    Xform l2w, w2l;
+    std::shared_ptr<MIPMapS> Lmap;
+    std::shared_ptr<Distribution2D> distribution;
 };
 struct Medium { Spec sigma_a, sigma_s, sigma_t; float g; };
 struct MaterialO { pbr_material_desc d; float ua, va, ra; };   // pre-remapped roughness
@@ -985,7 +990,19 @@ static Spec SkyValue(const Light& l, float u, float v) {   // SkyBoxLight.cpp:27
     Spec Lv(l.data[offset + 0], l.data[offset + 1], l.data[offset + 2]);
     return HDRtoLDR(Lv, 0.3f);
 }
+// InfiniteAreaLight (Light/InfiniteAreaLight.cpp)
+static float SphericalTheta(V3 v) { return t_acos(Clampf(v.z, -1, 1)); }   // Geometry.h:1517-1519
+static float SphericalPhi(V3 v) {                                           // Geometry.h:1521-1524
+    float p = t_atan2(v.y, v.x);
+    return (p < 0) ? (p + 2 * Pi) : p;
+}
+static Spec InfiniteLe(const Light& l, const Ray& ray) {   // InfiniteAreaLight.cpp:70-75
+    V3 w = Normalize(l.w2l.vector(ray.d));
+    P2 st(SphericalPhi(w) * Inv2Pi, SphericalTheta(w) * InvPi);
+    return l.Lmap->Lookup(st, 0.f);
+}
 static Spec LightLe(const Light& l, const Ray& ray) {
+    if (l.type == PBR_LIGHT_INFINITE_AREA) return InfiniteLe(l, ray);
     if (l.type == PBR_LIGHT_SKYBOX) {   // SkyBoxLight.cpp:59-77
         V3 dn = Normalize(ray.d);
         float u, v;
@@ -1037,6 +1054,19 @@ static Spec SampleLi(const Scene& s, const Light& l, const Interaction& ref, P2 
         vis->p0 = ref; vis->p1 = intr;
         return AreaL(l, intr, -*wi);
     }
+    if (l.type == PBR_LIGHT_INFINITE_AREA) {   // InfiniteAreaLight.cpp:78-100
+        float mapPdf;
+        P2 uv = l.distribution->SampleContinuous2(u, &mapPdf);
+        if (mapPdf == 0) { *pdf = 0; return Spec(0.f); }
+        float theta = uv.y * Pi, phi = uv.x * 2 * Pi;
+        float cosTheta = t_cos(theta), sinTheta = t_sin(theta);
+        float sinPhi = t_sin(phi), cosPhi = t_cos(phi);
+        *wi = l.l2w.vector(V3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
+        *pdf = mapPdf / (2 * Pi * Pi * sinTheta);
+        if (sinTheta == 0) *pdf = 0;
+        vis->p0 = ref; vis->p1 = Interaction(); vis->p1.p = ref.p + *wi * (2 * l.worldRadius);
+        return l.Lmap->Lookup(uv, 0.f);
+    }
     // SkyBoxLight::Sample_Li (SkyBoxLight.cpp:43-56)
     *wi = UniformSampleSphere(u);
     *pdf = 1.f / (4 * Pi);
@@ -1047,6 +1077,13 @@ static Spec SampleLi(const Scene& s, const Light& l, const Interaction& ref, P2 
     return SkyValue(l, ul, vl);
 }
 static float PdfLi(const Scene& s, const Light& l, const Interaction& ref, V3 wi) {
+    if (l.type == PBR_LIGHT_INFINITE_AREA) {   // InfiniteAreaLight.cpp:103-110
+        V3 w = l.w2l.vector(wi);
+        float theta = SphericalTheta(w), phi = SphericalPhi(w);
+        float sinTheta = t_sin(theta);
+        if (sinTheta == 0) return 0;
+        return l.distribution->Pdf(P2(phi * Inv2Pi, theta * InvPi)) / (2 * Pi * Pi * sinTheta);
+    }
     if (l.type != PBR_LIGHT_DIFFUSE_AREA) return 0;   // point: 0; skybox: 0 (SkyBoxLight.h:29)
     // Shape::Pdf (Shape.cpp:31-42): intersect the light's own shape only
     const Prim& pr = s.prims[s.primOfOriginal[l.prim]];
@@ -1400,6 +1437,51 @@ struct Camera {
 };
 
 // ---------------------------------------------------------------- scene assembly from the C desc
+// InfiniteAreaLight constructor (InfiniteAreaLight.cpp:7-61) and Preprocess (InfiniteAreaLight.h:15-17)
+static void InfinitePreprocess(const Scene& s, Light* l) {
+    int w = 1, h = 1;
+    std::vector<Spec> texels;
+    if (!l->data.empty()) {
+        w = l->w; h = l->h;
+        texels.resize((size_t)w * h);
+        for (int j = 0; j < h; j++)
+            for (int i = 0; i < w; i++) {
+                Spec r;
+                for (int k = 0; k < 3; ++k) {
+                    r[k] = l->data[((size_t)i + (size_t)j * w) * l->comps + k];
+                    r[k] = l->Lemit[k] * r[k];
+                }
+                texels[i + (size_t)j * w] = r;
+            }
+    } else {
+        texels.assign(1, l->Lemit);   // no texmap: the 1x1 map of L (the reference frees an uninitialised pointer first)
+    }
+    l->Lmap = std::make_shared<MIPMapS>(w, h, texels.data());
+    int width = l->Lmap->Width(), height = l->Lmap->Height();
+    std::vector<float> img((size_t)width * height);
+    for (int v = 0; v < height; v++) {
+        float vp = (v + .5f) / (float)height;
+        float sinTheta = t_sin(Pi * (v + .5f) / height);
+        for (int u = 0; u < width; ++u) {
+            float up = (u + .5f) / (float)width;
+            img[u + (size_t)v * width] = l->Lmap->Lookup(P2(up, vp), 0.f).y();
+            img[u + (size_t)v * width] *= sinTheta;
+        }
+    }
+    l->distribution = std::make_shared<Distribution2D>(img.data(), width, height);
+    // scene.WorldBound().BoundingSphere(&worldCenter, &worldRadius) (Geometry.h:1250-1254)
+    Bounds3 wb;
+    if (!s.nodes.empty()) {
+        wb.pMin = V3(s.nodes[0].pMin[0], s.nodes[0].pMin[1], s.nodes[0].pMin[2]);
+        wb.pMax = V3(s.nodes[0].pMax[0], s.nodes[0].pMax[1], s.nodes[0].pMax[2]);
+    }
+    V3 c = (wb.pMin + wb.pMax) * 0.5f;   // Point3::operator/(2): multiply by the reciprocal
+    bool inside = c.x >= wb.pMin.x && c.x <= wb.pMax.x && c.y >= wb.pMin.y && c.y <= wb.pMax.y && c.z >= wb.pMin.z &&
+                  c.z <= wb.pMax.z;
+    l->worldCenter = c;
+    l->worldRadius = inside ? Length(c - wb.pMax) : 0;
+}
+
 static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
     if (!d || d->abi_version != PBR_HIP_ABI_VERSION) throw std::runtime_error("bad scene desc");
     std::unique_ptr<Scene> s(new Scene);
@@ -1475,6 +1557,15 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
             l.Lemit = S3(ld.Le);
             l.twoSided = ld.two_sided != 0;
             l.prim = firstPrimOfShape[ld.shape] + ld.triangle;
+        } else if (ld.type == PBR_LIGHT_INFINITE_AREA) {
+            l.l2w = l2w;
+            l.w2l = Xform(l2w.mInv, l2w.m);   // Inverse(LightToWorld) swaps m and mInv
+            l.Lemit = S3(ld.Le);              // the constructor's `power` scale
+            if (ld.env_data && ld.env_width > 0 && ld.env_height > 0) {
+                l.w = ld.env_width; l.h = ld.env_height; l.comps = ld.env_components;
+                l.data.assign(ld.env_data, ld.env_data + (size_t)l.w * l.h * l.comps);
+            }
+            s->infinite.push_back(i);
         } else {
             l.worldCenter = V3(ld.world_center[0], ld.world_center[1], ld.world_center[2]);
             l.worldRadius = ld.world_radius;
@@ -1489,6 +1580,8 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
     BuildBVH(*s, prims, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1);
     for (Light& l : s->lights)
         if (l.type == PBR_LIGHT_DIFFUSE_AREA) l.area = TriangleArea(*s, s->prims[s->primOfOriginal[l.prim]]);
+    for (Light& l : s->lights)
+        if (l.type == PBR_LIGHT_INFINITE_AREA) InfinitePreprocess(*s, &l);
     return s;
 }
 
@@ -1501,6 +1594,8 @@ static Distribution1D MakeLightDistrib(const Scene& s, int strategy) {   // Ligh
             const Light& l = s.lights[i];
             Spec P(0.f);
             if (l.type == PBR_LIGHT_POINT) P = 4 * Pi * l.I;
+            else if (l.type == PBR_LIGHT_INFINITE_AREA)   // InfiniteAreaLight.cpp:63-67
+                P = (4 * Pi) * Pi * l.worldRadius * l.worldRadius * l.Lmap->Lookup(P2(.5f, .5f), .5f);
             else if (l.type == PBR_LIGHT_DIFFUSE_AREA) P = (float)(l.twoSided ? 2 : 1) * l.Lemit * l.area * Pi;
             f[i] = P.y();
         }

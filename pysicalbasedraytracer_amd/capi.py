@@ -19,7 +19,7 @@ PBR_E_NODEVICE = -5
 
 SHAPE_TRIANGLE_MESH, SHAPE_SPHERE = 0, 1
 MAT_NONE, MAT_MATTE, MAT_MIRROR, MAT_GLASS, MAT_METAL, MAT_PLASTIC = range(6)
-LIGHT_POINT, LIGHT_DIFFUSE_AREA, LIGHT_SKYBOX = 0, 1, 2
+LIGHT_POINT, LIGHT_DIFFUSE_AREA, LIGHT_SKYBOX, LIGHT_INFINITE_AREA = 0, 1, 2, 3
 INTEGRATOR_WHITTED, INTEGRATOR_PATH, INTEGRATOR_VOLPATH = 0, 1, 2
 SAMPLER_HALTON, SAMPLER_SOBOL = 0, 1
 LIGHTS_UNIFORM, LIGHTS_POWER = 0, 1

@@ -798,7 +798,64 @@ __device__ __forceinline__ rgb sky_value(const DeviceScene& S, const DLight& l, 
     float4 t = S.env[w + h * l.envW];   // HDRtoLDR already applied at upload
     return sp3(t.x, t.y, t.z);
 }
+// ---- InfiniteAreaLight (Light/InfiniteAreaLight.cpp:63-110) over the tables of pbr_infinite.cpp
+// MIPMap::Lookup(st, 0) = triangle(0, st): bilinear on level 0, ImageWrap::Repeat (MIPMap.h:240-252)
+__device__ __forceinline__ rgb inf_lookup(const InfDev& E, float s0f, float t0f) {
+    float s = s0f * E.w - 0.5f, t = t0f * E.h - 0.5f;
+    float fs = floorf(s), ft = floorf(t);
+    int s0 = (int)fs, t0 = (int)ft;
+    float ds = s - s0, dt = t - t0;
+    auto wrap = [](int a, int b) { int r = a - (a / b) * b; return r < 0 ? r + b : r; };   // Mod (PBR.h:194-197)
+    int sa = wrap(s0, E.w), sb = wrap(s0 + 1, E.w), ta = wrap(t0, E.h), tb = wrap(t0 + 1, E.h);
+    float4 a = E.tex[(size_t)ta * E.w + sa], b = E.tex[(size_t)tb * E.w + sa];
+    float4 c = E.tex[(size_t)ta * E.w + sb], d = E.tex[(size_t)tb * E.w + sb];
+    return ((1 - ds) * (1 - dt)) * sp3(a.x, a.y, a.z) + ((1 - ds) * dt) * sp3(b.x, b.y, b.z) +
+           (ds * (1 - dt)) * sp3(c.x, c.y, c.z) + (ds * dt) * sp3(d.x, d.y, d.z);
+}
+PBR_HD float spherical_theta(f3 v) { return t_acos(clampf(v.z, -1, 1)); }   // Geometry.h:1517-1519
+PBR_HD float spherical_phi(f3 v) {                                           // Geometry.h:1521-1524
+    float p = t_atan2(v.y, v.x);
+    return (p < 0) ? (p + 2 * kPi) : p;
+}
+// FindInterval (PBR.h:168-181) over a cdf of `size` entries
+__device__ __forceinline__ int find_interval(const float* cdf, int size, float u) {
+    int first = 0, len_ = size;
+    while (len_ > 0) {
+        int half = len_ >> 1, middle = first + half;
+        if (cdf[middle] <= u) { first = middle + 1; len_ -= half + 1; }
+        else len_ = half;
+    }
+    return clampi(first - 1, 0, size - 2);
+}
+// Distribution1D::SampleContinuous (Sampling.h:117-131)
+__device__ __forceinline__ float sample_continuous(const float* func, const float* cdf, int n, float funcInt, float u,
+                                                   float* pdf, int* off) {
+    int offset = find_interval(cdf, n + 1, u);
+    *off = offset;
+    float du = u - cdf[offset];
+    if ((cdf[offset + 1] - cdf[offset]) > 0) du /= (cdf[offset + 1] - cdf[offset]);
+    *pdf = (funcInt > 0) ? func[offset] / funcInt : 0;
+    return (offset + du) / n;
+}
+__device__ __forceinline__ rgb inf_Le(const DeviceScene& S, const Ray& r) {   // InfiniteAreaLight.cpp:70-75
+    f3 w = normalize(xf_vector(S.inf.w2l, r.d));
+    return inf_lookup(S.inf, spherical_phi(w) * kInv2Pi, spherical_theta(w) * kInvPi);
+}
+// Pdf_Li (InfiniteAreaLight.cpp:103-110) with Distribution2D::Pdf (Sampling.h:159-166)
+__device__ __forceinline__ float inf_pdf_li(const DeviceScene& S, f3 w) {
+    const InfDev& E = S.inf;
+    f3 wi = xf_vector(E.w2l, w);
+    float theta = spherical_theta(wi), phi = spherical_phi(wi);
+    float sinTheta = t_sin(theta);
+    if (sinTheta == 0) return 0;
+    float p0 = phi * kInv2Pi, p1 = theta * kInvPi;
+    int iu = clampi((int)(p0 * E.w), 0, E.w - 1);
+    int iv = clampi((int)(p1 * E.h), 0, E.h - 1);
+    return E.condFunc[(size_t)iv * E.w + iu] / E.margInt / (2 * kPi * kPi * sinTheta);
+}
+
 __device__ __forceinline__ rgb light_Le(const DeviceScene& S, const DLight& l, const Ray& r) {
+    if (l.type == LT_INF) return inf_Le(S, r);
     if (l.type == LT_SKY) {
         f3 dn = normalize(r.d);
         float u, v;
@@ -819,6 +876,27 @@ __device__ __forceinline__ void tri_verts(const DeviceScene& S, int slot, f3* p0
     const float4* tv = S.triVerts + 3 * (size_t)slot;
     float4 a = tv[0], b = tv[1], c = tv[2];
     *p0 = mk(a.x, a.y, a.z); *p1 = mk(b.x, b.y, b.z); *p2 = mk(c.x, c.y, c.z);
+}
+// InfiniteAreaLight::Sample_Li (InfiniteAreaLight.cpp:78-100) with Distribution2D::SampleContinuous
+// (Sampling.h:146-156)
+__device__ rgb inf_sample_li(const DeviceScene& S, const DLight& l, const Isect& ref, float u0, float u1, f3* wi,
+                             float* pdf, VisPt* v) {
+    const InfDev& E = S.inf;
+    float pdf0, pdf1;
+    int row, col;
+    float d1 = sample_continuous(E.margFunc, E.margCdf, E.h, E.margInt, u1, &pdf1, &row);
+    float d0 = sample_continuous(E.condFunc + (size_t)row * E.w, E.condCdf + (size_t)row * (E.w + 1), E.w,
+                                 E.margFunc[row], u0, &pdf0, &col);
+    float mapPdf = pdf0 * pdf1;
+    if (mapPdf == 0) { *pdf = 0; return sp(0.f); }
+    float theta = d1 * kPi, phi = d0 * 2 * kPi;
+    float cosTheta = t_cos(theta), sinTheta = t_sin(theta);
+    float sinPhi = t_sin(phi), cosPhi = t_cos(phi);
+    *wi = xf_vector(E.l2w, mk(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
+    *pdf = mapPdf / (2 * kPi * kPi * sinTheta);
+    if (sinTheta == 0) *pdf = 0;
+    v->p = ref.p + *wi * (2 * l.worldRadius); v->pError = mk(0, 0, 0); v->n = mk(0, 0, 0); v->medIn = -1; v->medOut = -1;
+    return inf_lookup(E, d0, d1);
 }
 __device__ rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref, float u0, float u1, f3* wi, float* pdf, VisPt* v) {
     if (l.type == LT_POINT) {   // PointLight.cpp:5-15
@@ -854,6 +932,7 @@ __device__ rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref
         v->p = ip; v->pError = ipErr; v->n = in; v->medIn = -1; v->medOut = -1;
         return area_L(l, in, -*wi);
     }
+    if (l.type == LT_INF) return inf_sample_li(S, l, ref, u0, u1, wi, pdf, v);
     // SkyBoxLight::Sample_Li (SkyBoxLight.cpp:43-56)
     *wi = uniform_sphere(u0, u1);
     *pdf = 1.f / (4 * kPi);
@@ -865,6 +944,7 @@ __device__ rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref
 }
 // Shape::Pdf through the light's own triangle (Shape.cpp:31-42); 0 for point and skybox lights
 __device__ float pdf_li(const DeviceScene& S, const DLight& l, const Isect& ref, f3 wi) {
+    if (l.type == LT_INF) return inf_pdf_li(S, wi);
     if (l.type != LT_AREA) return 0;
     Ray ray = spawn_ray(ref, wi);
     f3 p0, p1, p2;

@@ -630,6 +630,7 @@ struct pbr_hip_ctx {
     bool haveScene = false;
     HostScene host;
     HaltonTables halton;
+    DevBuf dInfTex, dInfCF, dInfCC, dInfMF, dInfMC;
     DevBuf dNodes, dWide, dQuad, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dSobol, dSobolPix;          // active Sobol matrices, pixel tables
@@ -699,6 +700,18 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     S.lightFuncInt = ctx->funcInt;
     S.media = (const float*)ctx->dMedia.p;
     S.nMedia = (int)h.media.size() / 10;
+    if (h.inf.light >= 0) {
+        S.inf.tex = (const float4*)ctx->dInfTex.p;
+        S.inf.condFunc = (const float*)ctx->dInfCF.p;
+        S.inf.condCdf = (const float*)ctx->dInfCC.p;
+        S.inf.margFunc = (const float*)ctx->dInfMF.p;
+        S.inf.margCdf = (const float*)ctx->dInfMC.p;
+        S.inf.margInt = h.inf.margInt;
+        S.inf.w = h.inf.w;
+        S.inf.h = h.inf.h;
+        std::memcpy(S.inf.l2w, h.inf.l2w, sizeof(S.inf.l2w));
+        std::memcpy(S.inf.w2l, h.inf.w2l, sizeof(S.inf.w2l));
+    }
     return S;
 }
 
@@ -1169,6 +1182,11 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     HIP_TRY(ctx->dLights.upload(h.lights, ctx->stream));
     HIP_TRY(ctx->dEnv.upload(h.env, ctx->stream));
     HIP_TRY(ctx->dMedia.upload(h.media, ctx->stream));
+    HIP_TRY(ctx->dInfTex.upload(h.inf.tex, ctx->stream));
+    HIP_TRY(ctx->dInfCF.upload(h.inf.condFunc, ctx->stream));
+    HIP_TRY(ctx->dInfCC.upload(h.inf.condCdf, ctx->stream));
+    HIP_TRY(ctx->dInfMF.upload(h.inf.margFunc, ctx->stream));
+    HIP_TRY(ctx->dInfMC.upload(h.inf.margCdf, ctx->stream));
     HIP_TRY(ctx->dPrimIds.upload(h.primIds, ctx->stream));
     int rc = upload_light_distribution(ctx, PBR_LIGHTS_UNIFORM);
     if (rc) return rc;

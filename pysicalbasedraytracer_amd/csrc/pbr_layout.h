@@ -40,7 +40,7 @@ struct MatTemplate {              // what Material::ComputeScatteringFunctions a
     Lobe lobes[2];
 };
 
-enum LightType { LT_POINT = 0, LT_AREA = 1, LT_SKY = 2 };
+enum LightType { LT_POINT = 0, LT_AREA = 1, LT_SKY = 2, LT_INF = 3 };
 struct DLight {
     int type;
     int primSlot;                 // area light: BVH-ordered primitive slot of its triangle
@@ -55,6 +55,18 @@ struct DLight {
 };
 
 struct SphereRec { float o2w[16]; float w2o[16]; float radius; int flip; int pad[2]; };
+
+// InfiniteAreaLight (Light/InfiniteAreaLight.cpp): level-0 MIPMap texels and its Distribution2D
+struct InfDev {
+    const float4* tex;             // w*h texels (RGB), powers of two
+    const float* condFunc;         // h rows of w
+    const float* condCdf;          // h rows of w + 1
+    const float* margFunc;         // h (= each row's funcInt)
+    const float* margCdf;          // h + 1
+    float margInt;
+    int w, h;
+    float l2w[12], w2l[12];        // LightToWorld / WorldToLight, top three rows
+};
 
 struct DeviceScene {
     const float4* nodes;
@@ -80,6 +92,7 @@ struct DeviceScene {
     // media
     const float* media;            // per medium: sigma_a[3] sigma_s[3] sigma_t[3] g → 10 floats
     int nMedia;
+    InfDev inf;
 };
 
 struct DeviceSampler {

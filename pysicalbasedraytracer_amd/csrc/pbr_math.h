@@ -48,6 +48,7 @@ PBR_TRANS float t_log(float x) { return (float)log((double)x); }
 PBR_TRANS float t_pow(float x, float y) { return (float)pow((double)x, (double)y); }
 PBR_TRANS float t_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 PBR_TRANS float t_asin(float x) { return (float)asin((double)x); }
+PBR_TRANS float t_acos(float x) { return (float)acos((double)x); }
 
 // std::min/std::max/Clamp with the reference's NaN behaviour
 PBR_HD float mn(float a, float b) { return (b < a) ? b : a; }

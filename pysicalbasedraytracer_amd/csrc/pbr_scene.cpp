@@ -594,6 +594,19 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
             S->envLight = li;
             S->infinite.push_back(li);
             S->lightPower.push_back(0.f);
+        } else if (ld.type == PBR_LIGHT_INFINITE_AREA) {
+            if (S->inf.light >= 0) fail("only one InfiniteAreaLight is supported");
+            // Preprocess sees scene.WorldBound() = the BVH root's bounds (empty Bounds3f → radius 0)
+            const float big = std::numeric_limits<float>::max(), low = std::numeric_limits<float>::lowest();
+            float lo[3] = {big, big, big}, hi[3] = {low, low, low};
+            if (!S->nodes.empty())
+                for (int k = 0; k < 3; ++k) { lo[k] = S->nodes[0].pMin[k]; hi[k] = S->nodes[0].pMax[k]; }
+            float P[3];
+            build_infinite_light(ld, lo, hi, &S->inf, P);
+            S->inf.light = li;
+            L.worldRadius = S->inf.worldRadius;
+            S->infinite.push_back(li);
+            S->lightPower.push_back(0.212671f * P[0] + 0.715160f * P[1] + 0.072169f * P[2]);
         } else {
             fail("unknown light type");
         }

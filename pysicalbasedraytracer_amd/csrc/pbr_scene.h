@@ -19,6 +19,17 @@ struct LinearBVHNode {            // BVHAccel.cpp:46-55, 32 bytes
 };
 static_assert(sizeof(LinearBVHNode) == 32, "LinearBVHNode is 32 bytes");
 
+struct InfiniteHost {
+    int light = -1;                         // index in lights, -1 = none
+    int w = 0, h = 0;                       // level-0 resolution (powers of two)
+    std::vector<float> tex;                 // 4 floats per texel, RGB + pad
+    std::vector<float> condFunc, condCdf;   // h rows of w / w + 1
+    std::vector<float> margFunc, margCdf;   // h / h + 1
+    float margInt = 0;
+    float l2w[16], w2l[16];
+    float worldRadius = 0;
+};
+
 struct HostScene {
     std::vector<LinearBVHNode> nodes;
     std::vector<int32_t> primIds;           // ordered slot → index in the prims vector
@@ -40,8 +51,13 @@ struct HostScene {
     int32_t rootRef = 0;
     std::vector<float> quad;                // 32 floats per quad node (build_quad_nodes)
     int32_t quadRootRef = 0;
+    InfiniteHost inf;                       // the InfiniteAreaLight, if any (pbr_infinite.cpp)
 };
 
+// InfiniteAreaLight tables (Light/InfiniteAreaLight.cpp:7-61): the level-0 MIPMap image (resampled
+// to powers of two as Texture/MIPMap.h:86-150 does) and the Distribution2D over its luminance.
+void build_infinite_light(const pbr_light_desc& ld, const float worldMin[3], const float worldMax[3],
+                          InfiniteHost* out, float power[3]);
 // Throws std::invalid_argument on a malformed descriptor.
 void build_host_scene(const pbr_scene_desc* desc, HostScene* out);
 

@@ -255,7 +255,9 @@ PlyMesh LoadPLY(const std::string& path) {
 namespace {
 // Radiance RGBE → float exactly as stbi_loadf (stbi__hdr_load / stbi__hdr_convert), rows flipped
 // as stbi_set_flip_vertically_on_load(true) does (SkyBoxLight.cpp:19-24).
-bool load_hdr(const char* file, int* w, int* h, int* comp, std::vector<float>* data) {
+// stb's global stbi_set_flip_vertically_on_load flag: SkyBoxLight::loadImage sets it (and it stays set)
+bool g_stbiFlip = false;
+bool load_hdr(const char* file, int* w, int* h, int* comp, std::vector<float>* data, bool flip) {
     std::ifstream f(file, std::ios::binary);
     if (!f) return false;
     std::string line;
@@ -309,7 +311,7 @@ bool load_hdr(const char* file, int* w, int* h, int* comp, std::vector<float>* d
     if (flat && (W < 8 || W >= 32768) && !rd(rgbe.data(), rgbe.size())) return false;
     data->assign((size_t)W * H * 3, 0.f);
     for (int y = 0; y < H; ++y) {
-        int dy = H - 1 - y;   // vertical flip
+        int dy = flip ? H - 1 - y : y;   // vertical flip
         for (int x = 0; x < W; ++x) {
             const unsigned char* in = &rgbe[((size_t)y * W + x) * 4];
             float* o = &(*data)[((size_t)dy * W + x) * 3];
@@ -337,7 +339,21 @@ SkyBoxLight::SkyBoxLight(const Transform& LightToWorld, const Point3f& worldCent
 bool SkyBoxLight::loadImage(const char* imageFile) {
     imageWidth = imageHeight = nrComponents = 0;
     data.clear();
-    return imageFile && load_hdr(imageFile, &imageWidth, &imageHeight, &nrComponents, &data);
+    g_stbiFlip = true;   // stbi_set_flip_vertically_on_load(true)
+    return imageFile && load_hdr(imageFile, &imageWidth, &imageHeight, &nrComponents, &data, true);
+}
+InfiniteAreaLight::InfiniteAreaLight(const Transform& LightToWorld, const Spectrum& power, int nSamples, const std::string& texmap)
+    : Light(LightToWorld, MediumInterface(), nSamples), L(power) {
+    if (!texmap.empty() && !load_hdr(texmap.c_str(), &imageWidth, &imageHeight, &nrComponents, &data, g_stbiFlip)) {
+        imageWidth = imageHeight = nrComponents = 0;
+        data.clear();
+    }
+}
+InfiniteAreaLight::InfiniteAreaLight(const Transform& LightToWorld, const Spectrum& power, int nSamples, int width,
+                                     int height, int components, std::vector<float> d)
+    : Light(LightToWorld, MediumInterface(), nSamples), L(power), imageWidth(width), imageHeight(height),
+      nrComponents(components), data(std::move(d)) {
+    if ((size_t)width * height * components != data.size()) throw std::invalid_argument("InfiniteAreaLight: data size mismatch");
 }
 
 // ============================================================================ aggregate, scene, camera, sampler
@@ -382,6 +398,7 @@ struct FlatScene {
     std::vector<std::vector<int32_t>> indexRuns;
     std::vector<std::shared_ptr<TriangleMesh>> meshes;   // keep P/N/UV alive
     std::vector<std::shared_ptr<SkyBoxLight>> skies;     // keep env data alive
+    std::vector<std::shared_ptr<InfiniteAreaLight>> infs;
     std::map<const Medium*, int> mediumIndex;
 };
 
@@ -588,6 +605,18 @@ std::shared_ptr<FlatScene> FlattenScene(const Scene& scene, const Medium* camera
             L.n_samples = sk->nSamples;
             L.medium_inside = L.medium_outside = -1;
             F->skies.push_back(std::static_pointer_cast<SkyBoxLight>(scene.lights[li]));
+        } else if (auto* il = dynamic_cast<const InfiniteAreaLight*>(l)) {
+            std::memset(&L, 0, sizeof(L));
+            L.type = PBR_LIGHT_INFINITE_AREA;
+            fill_transform(il->LightToWorld, &L.light_to_world);
+            put(L.Le, il->L);
+            L.env_width = il->imageWidth;
+            L.env_height = il->imageHeight;
+            L.env_components = il->nrComponents;
+            L.env_data = il->data.empty() ? nullptr : il->data.data();
+            L.n_samples = il->nSamples;
+            L.medium_inside = L.medium_outside = -1;
+            F->infs.push_back(std::static_pointer_cast<InfiniteAreaLight>(scene.lights[li]));
         } else if (dynamic_cast<const DiffuseAreaLight*>(l)) {
             if (!boundArea[li]) throw std::invalid_argument("DiffuseAreaLight whose shape is not a scene triangle");
         } else {

@@ -42,6 +42,29 @@ def scale(sx, sy, sz):
     return m, mi
 
 
+def _rotate(axis, theta):
+    """RotateX/Y/Z (Core/Transform.cpp): sin/cos of Radians(theta) in float (correctly rounded,
+    pbr_math.h convention), mInv = Transpose(m)."""
+    rad = f32(f32(f32(math.pi) / f32(180)) * f32(theta))   # Radians (PBR.h)
+    st, ct = f32(math.sin(float(rad))), f32(math.cos(float(rad)))
+    m = np.eye(4, dtype=f32)
+    i, j = {"x": (1, 2), "y": (2, 0), "z": (0, 1)}[axis]
+    m[i, i], m[i, j], m[j, i], m[j, j] = ct, -st, st, ct
+    return m, np.ascontiguousarray(m.T)
+
+
+def rotate_x(theta):
+    return _rotate("x", theta)
+
+
+def rotate_y(theta):
+    return _rotate("y", theta)
+
+
+def rotate_z(theta):
+    return _rotate("z", theta)
+
+
 def _mul(a, b):
     r = np.zeros((4, 4), dtype=f32)
     for i in range(4):
@@ -353,6 +376,20 @@ class Scene:
         l.env_height, l.env_width, l.env_components = env.shape
         l.env_data = capi.fptr(env)
         self._keep.append(env)
+        self.lights.append(l)
+        return len(self.lights) - 1
+
+    def infinite_light(self, env=None, L=(1.0, 1.0, 1.0), xform=None, n_samples=1):
+        """InfiniteAreaLight(LightToWorld, power L, nSamples, texmap) (Light/InfiniteAreaLight.cpp:7-61):
+        env = the image as stbi_loadf returned it (rows × cols × comps float), None → a constant L."""
+        l = capi.LightDesc(type=capi.LIGHT_INFINITE_AREA, n_samples=n_samples, medium_inside=-1, medium_outside=-1)
+        l.light_to_world = _xf(xform or identity())
+        l.Le[:] = [float(c) for c in L]
+        if env is not None:
+            env = np.ascontiguousarray(env, dtype=f32)
+            l.env_height, l.env_width, l.env_components = env.shape
+            l.env_data = capi.fptr(env)
+            self._keep.append(env)
         self.lights.append(l)
         return len(self.lights) - 1
 
