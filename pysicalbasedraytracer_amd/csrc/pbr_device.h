@@ -837,13 +837,15 @@ __device__ __forceinline__ float sample_continuous(const float* func, const floa
     *pdf = (funcInt > 0) ? func[offset] / funcInt : 0;
     return (offset + du) / n;
 }
-__device__ __forceinline__ rgb inf_Le(const DeviceScene& S, const Ray& r) {   // InfiniteAreaLight.cpp:70-75
-    f3 w = normalize(xf_vector(S.inf.w2l, r.d));
-    return inf_lookup(S.inf, spherical_phi(w) * kInv2Pi, spherical_theta(w) * kInvPi);
+// The InfiniteAreaLight functions are out of line and read the light's record from device memory,
+// so scenes without one pay neither registers nor kernel-argument SGPRs for them.
+__device__ __noinline__ rgb inf_Le(const InfDev* E, f3 d) {   // InfiniteAreaLight.cpp:70-75
+    f3 w = normalize(xf_vector(E->w2l, d));
+    return inf_lookup(*E, spherical_phi(w) * kInv2Pi, spherical_theta(w) * kInvPi);
 }
 // Pdf_Li (InfiniteAreaLight.cpp:103-110) with Distribution2D::Pdf (Sampling.h:159-166)
-__device__ __forceinline__ float inf_pdf_li(const DeviceScene& S, f3 w) {
-    const InfDev& E = S.inf;
+__device__ __noinline__ float inf_pdf_li(const InfDev* Ep, f3 w) {
+    const InfDev& E = *Ep;
     f3 wi = xf_vector(E.w2l, w);
     float theta = spherical_theta(wi), phi = spherical_phi(wi);
     float sinTheta = t_sin(theta);
@@ -855,7 +857,7 @@ __device__ __forceinline__ float inf_pdf_li(const DeviceScene& S, f3 w) {
 }
 
 __device__ __forceinline__ rgb light_Le(const DeviceScene& S, const DLight& l, const Ray& r) {
-    if (l.type == LT_INF) return inf_Le(S, r);
+    if (l.type == LT_INF) return inf_Le(S.inf, r.d);
     if (l.type == LT_SKY) {
         f3 dn = normalize(r.d);
         float u, v;
@@ -879,9 +881,9 @@ __device__ __forceinline__ void tri_verts(const DeviceScene& S, int slot, f3* p0
 }
 // InfiniteAreaLight::Sample_Li (InfiniteAreaLight.cpp:78-100) with Distribution2D::SampleContinuous
 // (Sampling.h:146-156)
-__device__ rgb inf_sample_li(const DeviceScene& S, const DLight& l, const Isect& ref, float u0, float u1, f3* wi,
-                             float* pdf, VisPt* v) {
-    const InfDev& E = S.inf;
+__device__ __noinline__ rgb inf_sample_li(const InfDev* Ep, float worldRadius, f3 refP, float u0, float u1, f3* wi,
+                                          float* pdf, VisPt* v) {
+    const InfDev& E = *Ep;
     float pdf0, pdf1;
     int row, col;
     float d1 = sample_continuous(E.margFunc, E.margCdf, E.h, E.margInt, u1, &pdf1, &row);
@@ -895,7 +897,7 @@ __device__ rgb inf_sample_li(const DeviceScene& S, const DLight& l, const Isect&
     *wi = xf_vector(E.l2w, mk(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
     *pdf = mapPdf / (2 * kPi * kPi * sinTheta);
     if (sinTheta == 0) *pdf = 0;
-    v->p = ref.p + *wi * (2 * l.worldRadius); v->pError = mk(0, 0, 0); v->n = mk(0, 0, 0); v->medIn = -1; v->medOut = -1;
+    v->p = refP + *wi * (2 * worldRadius); v->pError = mk(0, 0, 0); v->n = mk(0, 0, 0); v->medIn = -1; v->medOut = -1;
     return inf_lookup(E, d0, d1);
 }
 __device__ rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref, float u0, float u1, f3* wi, float* pdf, VisPt* v) {
@@ -932,7 +934,7 @@ __device__ rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref
         v->p = ip; v->pError = ipErr; v->n = in; v->medIn = -1; v->medOut = -1;
         return area_L(l, in, -*wi);
     }
-    if (l.type == LT_INF) return inf_sample_li(S, l, ref, u0, u1, wi, pdf, v);
+    if (l.type == LT_INF) return inf_sample_li(S.inf, l.worldRadius, ref.p, u0, u1, wi, pdf, v);
     // SkyBoxLight::Sample_Li (SkyBoxLight.cpp:43-56)
     *wi = uniform_sphere(u0, u1);
     *pdf = 1.f / (4 * kPi);
@@ -944,7 +946,7 @@ __device__ rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref
 }
 // Shape::Pdf through the light's own triangle (Shape.cpp:31-42); 0 for point and skybox lights
 __device__ float pdf_li(const DeviceScene& S, const DLight& l, const Isect& ref, f3 wi) {
-    if (l.type == LT_INF) return inf_pdf_li(S, wi);
+    if (l.type == LT_INF) return inf_pdf_li(S.inf, wi);
     if (l.type != LT_AREA) return 0;
     Ray ray = spawn_ray(ref, wi);
     f3 p0, p1, p2;

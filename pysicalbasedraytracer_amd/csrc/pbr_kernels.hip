@@ -152,6 +152,21 @@ struct KParams {
     unsigned long long* stats; // rays, nodes, prims, shading
 };
 
+// GetCameraSample (Sampler.cpp:10-21) + GenerateRay: pFilm = dims 0,1; time = dim 2 (no motion
+// blur: never read); pLens = dims 3,4, read only by a camera with an aperture (lensRadius > 0), so
+// a pinhole camera skips their scrambled radical inverses and only advances the dimension to 5.
+__device__ __forceinline__ Ray camera_sample_ray(const KParams& P, SState& st, int x, int y) {
+    float u0, u1, l0 = 0.f, l1 = 0.f;
+    get2d(P.smp, st, &u0, &u1);
+    if (P.cam.lensRadius > 0) {
+        get1d(P.smp, st);
+        get2d(P.smp, st, &l0, &l1);
+    } else {
+        st.dim = 5;
+    }
+    return camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
+}
+
 // ---------------------------------------------------------------- direct lighting (Integrator.cpp:46-177)
 template <bool STATS>
 __device__ bool unoccluded(const DeviceScene& S, const Isect& p0, const VisPt& p1, Counters* c) {   // Light.cpp:19-22
@@ -520,11 +535,7 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
             st.px = x;
             st.py = y;
             // GetCameraSample (Sampler.cpp:10-21): pFilm, time, pLens
-            float u0, u1, l0, l1;
-            get2d(P.smp, st, &u0, &u1);
-            get1d(P.smp, st);
-            get2d(P.smp, st, &l0, &l1);
-            Ray r = camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
+            Ray r = camera_sample_ray(P, st, x, y);
             if (INTEGRATOR == PBR_INTEGRATOR_WHITTED) L = whitted_li<STATS>(P, r, st, &cnt);
             else if (INTEGRATOR == PBR_INTEGRATOR_PATH) L = path_li<STATS>(P, r, st, &cnt);
             else L = volpath_li<STATS>(P, r, st, &cnt);
@@ -630,7 +641,7 @@ struct pbr_hip_ctx {
     bool haveScene = false;
     HostScene host;
     HaltonTables halton;
-    DevBuf dInfTex, dInfCF, dInfCC, dInfMF, dInfMC;
+    DevBuf dInfTex, dInfCF, dInfCC, dInfMF, dInfMC, dInfRec;
     DevBuf dNodes, dWide, dQuad, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dSobol, dSobolPix;          // active Sobol matrices, pixel tables
@@ -700,18 +711,7 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     S.lightFuncInt = ctx->funcInt;
     S.media = (const float*)ctx->dMedia.p;
     S.nMedia = (int)h.media.size() / 10;
-    if (h.inf.light >= 0) {
-        S.inf.tex = (const float4*)ctx->dInfTex.p;
-        S.inf.condFunc = (const float*)ctx->dInfCF.p;
-        S.inf.condCdf = (const float*)ctx->dInfCC.p;
-        S.inf.margFunc = (const float*)ctx->dInfMF.p;
-        S.inf.margCdf = (const float*)ctx->dInfMC.p;
-        S.inf.margInt = h.inf.margInt;
-        S.inf.w = h.inf.w;
-        S.inf.h = h.inf.h;
-        std::memcpy(S.inf.l2w, h.inf.l2w, sizeof(S.inf.l2w));
-        std::memcpy(S.inf.w2l, h.inf.w2l, sizeof(S.inf.w2l));
-    }
+    S.inf = h.inf.light >= 0 ? (const InfDev*)ctx->dInfRec.p : nullptr;
     return S;
 }
 
@@ -1187,6 +1187,22 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     HIP_TRY(ctx->dInfCC.upload(h.inf.condCdf, ctx->stream));
     HIP_TRY(ctx->dInfMF.upload(h.inf.margFunc, ctx->stream));
     HIP_TRY(ctx->dInfMC.upload(h.inf.margCdf, ctx->stream));
+    {   // the InfiniteAreaLight record the device functions read (pbr_layout.h InfDev)
+        std::vector<InfDev> rec(1);
+        std::memset(rec.data(), 0, sizeof(InfDev));
+        rec[0].tex = (const float4*)ctx->dInfTex.p;
+        rec[0].condFunc = (const float*)ctx->dInfCF.p;
+        rec[0].condCdf = (const float*)ctx->dInfCC.p;
+        rec[0].margFunc = (const float*)ctx->dInfMF.p;
+        rec[0].margCdf = (const float*)ctx->dInfMC.p;
+        rec[0].margInt = h.inf.margInt;
+        rec[0].w = h.inf.w;
+        rec[0].h = h.inf.h;
+        std::memcpy(rec[0].l2w, h.inf.l2w, sizeof(rec[0].l2w));
+        std::memcpy(rec[0].w2l, h.inf.w2l, sizeof(rec[0].w2l));
+        HIP_TRY(ctx->dInfRec.upload(rec, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));   // rec is a host temporary
+    }
     HIP_TRY(ctx->dPrimIds.upload(h.primIds, ctx->stream));
     int rc = upload_light_distribution(ctx, PBR_LIGHTS_UNIFORM);
     if (rc) return rc;

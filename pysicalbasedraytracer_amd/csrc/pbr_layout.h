@@ -92,7 +92,7 @@ struct DeviceScene {
     // media
     const float* media;            // per medium: sigma_a[3] sigma_s[3] sigma_t[3] g → 10 floats
     int nMedia;
-    InfDev inf;
+    const InfDev* inf;             // the InfiniteAreaLight's tables (device memory), or null
 };
 
 struct DeviceSampler {

@@ -108,11 +108,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams
     st.dim = 0;
     st.px = x;
     st.py = y;
-    float u0, u1, l0, l1;
-    get2d(P.smp, st, &u0, &u1);
-    get1d(P.smp, st);
-    get2d(P.smp, st, &l0, &l1);
-    Ray r = camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
+    Ray r = camera_sample_ray(P, st, x, y);
     HitRec h;
     Counters c;
     bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
