@@ -3,8 +3,9 @@
 dominant kernel and the CPU restatement timed beside it.
 
 One step = one full frame.  With --gpus N (launched by torch.distributed.run, one rank per GPU)
-the frame's 64×64 tiles are dealt round-robin over ranks and rank 0 gathers the per-tile float RGB
-spans over RCCL — total work is fixed, so scaling is strong.
+the frame's 64×64 tiles are dealt round-robin over ranks and rank 0 gathers the per-tile RGBA8
+FrameBuffer spans over RCCL — total work is fixed, so scaling is strong.  The gather of frame k
+runs on a communication stream while frame k+1 renders into the other of two output buffers.
 """
 import argparse
 import json
@@ -98,25 +99,46 @@ def main():
     # a real stream (torch's default one has handle 0, which the C-ABI reads as "context stream")
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    rgb = torch.empty((npx, 3), dtype=torch.float32, device=dev)
-    rgba = torch.empty((npx, 4), dtype=torch.uint8, device=dev)
-    # multi-GPU: rank 0 gathers the packed tile spans over RCCL and scatters them into the frame
-    exchange = FrameGather(W, H, world, dev) if world > 1 else None
+    # multi-GPU: rank 0 gathers the packed RGBA8 tile spans (the FrameBuffer the reference's Render
+    # fills) over RCCL and scatters them into the frame; double-buffered outputs let the gather of
+    # frame k (communication stream) overlap the render of frame k+1 (render stream)
+    nbuf = 2 if world > 1 else 1
+    rgbs = [torch.empty((npx, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    rgbas = [torch.empty((npx, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    exchange = FrameGather(W, H, world, dev, channels=4, dtype=torch.uint8) if world > 1 else None
+    comm = torch.cuda.Stream(dev) if world > 1 else None
+    released = [None] * nbuf   # event: the gather that read buffer b has finished
+    frame_no = [0]
 
-    def step():
+    def render(ev0=None, ev1=None):
+        b = frame_no[0] % nbuf
+        frame_no[0] += 1
+        if released[b] is not None:
+            stream.wait_event(released[b])
+        if ev0 is not None:
+            ev0.record(stream)
         # asynchronous: the frame is enqueued on `stream` and the next one queues behind it
-        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
+        r.render_device(rdr, rgbs[b].data_ptr(), rgbas[b].data_ptr(), stream=stream.cuda_stream, sync=False)
+        if ev1 is not None:
+            ev1.record(stream)
         if exchange is not None:
-            exchange(rgb, rank)
+            rendered = torch.cuda.Event()
+            rendered.record(stream)
+            comm.wait_event(rendered)
+            with torch.cuda.stream(comm):
+                exchange(rgbas[b], rank)
+                done = torch.cuda.Event()
+                done.record(comm)
+            released[b] = done
 
     # roofline counters: one instrumented, untimed pass on the same workload
-    st = r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, stats=True)
+    st = r.render_device(rdr, rgbs[0].data_ptr(), rgbas[0].data_ptr(), stream=stream.cuda_stream, stats=True)
     torch.cuda.synchronize(dev)
     samples_rank = npx * spp
     alg_bytes = B_NODE * st.node_visits + B_PRIM * st.prim_tests + B_RAY * st.rays + B_SHADE * st.shading_events
 
     for _ in range(args.warmup):
-        step()
+        render()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -125,11 +147,7 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for ev0, ev1 in evs:
-        ev0.record(stream)
-        r.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
-        ev1.record(stream)
-        if exchange is not None:
-            exchange(rgb, rank)
+        render(ev0, ev1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -161,11 +179,16 @@ def main():
             "config": {"workload": f"{args.config}: {W}x{H}, {spp} spp, "
                                    f"{['Whitted', 'Path', 'VolPath'][rd.integrator]} d{rd.max_depth}",
                        "scene": scene.info.get("dragon", ""), "triangles": scene.info.get("triangles"),
-                       "parallelism": f"tiles64x64 round-robin over {world} GPU(s), RCCL gather",
+                       "parallelism": f"tiles64x64 round-robin over {world} GPU(s), RCCL gather of RGBA8 spans",
                        "frame_ms": round(ms_per_step, 3), "scene_upload_s": round(upload_s, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
+                         # measured HBM bytes over the same frame time: what HBM actually moved
+                         # (the algorithmic bytes include BVH/mesh fetches that L2 and the
+                         # Infinity Cache serve, which is how `frac` can exceed 1)
+                         "traffic_gbs": None if traffic is None else round(traffic / (k_ms * 1e-3) / 1e9, 1),
+                         "traffic_frac": None if traffic is None else round(traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "kernel": ["wavefront frame: k_wf_camera_extend, (k_wf_shade, k_wf_shadow, k_wf_extend) per "
                                     "level, k_wf_finish, per 2^25-sample chunk",
                                     "wavefront frame: k_wfp_camera_extend, (k_wfp_shade, k_wfp_shadow, k_wfp_probe, "

@@ -141,14 +141,17 @@ def span_pixels(width, height, rank, world, tile=64):
 
 
 class FrameGather:
-    """Multi-GPU exchange.  Every rank holds its tiles' packed float-RGB span (a
-    torch tensor [npx, 3] on its device, or on the CPU under gloo).  One `gather` brings the spans
-    to rank 0 (RCCL over xGMI under the nccl backend), padded to the largest span, and rank 0
-    scatters them into a row-major [height*width, 3] frame on its own device (index_copy_ with
-    per-rank pixel indices computed once)."""
+    """Multi-GPU exchange.  Every rank holds its tiles' packed span — float linear
+    RGB [npx, 3] (the F7 float buffer) or the RGBA8 FrameBuffer bytes [npx, 4] uint8 (what the
+    reference's Render writes, Integrator.cpp:327-344) — as a torch tensor on its device, or on
+    the CPU under gloo.  One `gather` brings the spans to rank 0 (RCCL over xGMI under the nccl
+    backend), padded to the largest span, and rank 0 scatters them into a row-major
+    [height*width, channels] frame on its own device (index_copy_ with per-rank pixel indices
+    computed once)."""
 
-    def __init__(self, width, height, world, device, tile=64):
+    def __init__(self, width, height, world, device, tile=64, channels=3, dtype=None):
         import torch
+        dtype = torch.float32 if dtype is None else dtype
         self.world = world
         self.npx = [span_pixels(width, height, r, world, tile) for r in range(world)]
         self.max_px = max(self.npx)
@@ -157,9 +160,9 @@ class FrameGather:
             idx = [y * width + x for (x0, y0, x1, y1) in tiles_for_rank(width, height, r, world, tile)
                    for y in range(y0, y1) for x in range(x0, x1)]
             self.index.append(torch.tensor(idx, dtype=torch.long, device=device))
-        self.send = torch.zeros((self.max_px, 3), dtype=torch.float32, device=device)
+        self.send = torch.zeros((self.max_px, channels), dtype=dtype, device=device)
         self.recv = [torch.empty_like(self.send) for _ in range(world)]
-        self.frame = torch.zeros((height * width, 3), dtype=torch.float32, device=device)
+        self.frame = torch.zeros((height * width, channels), dtype=dtype, device=device)
 
     def __call__(self, span, rank, group=None):
         import torch.distributed as dist
@@ -173,7 +176,8 @@ class FrameGather:
 
 
 def gather_frame(span, width, height, rank, world, group=None, tile=64):
-    """One-shot FrameGather: the assembled [height, width, 3] numpy frame on rank 0, None elsewhere."""
-    g = FrameGather(width, height, world, span.device, tile)
+    """One-shot FrameGather: the assembled [height, width, channels] numpy frame on rank 0, None elsewhere."""
+    ch = span.shape[1]
+    g = FrameGather(width, height, world, span.device, tile, channels=ch, dtype=span.dtype)
     f = g(span, rank, group)
-    return None if f is None else f.cpu().numpy().reshape(height, width, 3)
+    return None if f is None else f.cpu().numpy().reshape(height, width, ch)

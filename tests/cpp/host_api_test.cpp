@@ -100,6 +100,21 @@ void build_area(Built& b, int W, int H, bool medium) {
     b.cam = std::shared_ptr<Camera>(CreatePerspectiveCamera(W, H, Inverse(lookat), nullptr));
 }
 
+// The reference's main.cpp light (main.cpp:377-381): InfiniteAreaLight(RotateX(-90) * RotateY(-0) *
+// RotateZ(-50), power 1, nSamples 10, texmap) — here an in-memory 60x30 sky (not a power of two,
+// so the MIPMap resamples it) added to a built scene.
+void add_infinite(Built& b) {
+    std::vector<float> img(60 * 30 * 3);
+    for (int y = 0; y < 30; ++y)
+        for (int x = 0; x < 60; ++x)
+            for (int c = 0; c < 3; ++c)
+                img[(y * 60 + x) * 3 + c] = 0.2f + 0.6f * (float)y / 30.f + (c == 2 ? 0.3f : 0.f) + ((x == 17 && y == 22) ? 50.f : 0.f);
+    Transform l2w = RotateX(-90) * RotateY(-0) * RotateZ(-50);
+    std::vector<std::shared_ptr<Light>> lights = b.scene->lights;
+    lights.push_back(std::make_shared<InfiniteAreaLight>(l2w, Spectrum(1.f), 10, 60, 30, 3, img));
+    b.scene = std::make_unique<Scene>(b.scene->GetAggregate(), lights);
+}
+
 // The same camera/render settings as SamplerIntegrator::Render builds, for the oracle.
 pbr_render_desc oracle_desc(const Built& b, const FlatScene& flat, int integrator, int spp, int depth, float rr) {
     auto* cam = dynamic_cast<const PerspectiveCamera*>(b.cam.get());
@@ -171,6 +186,12 @@ int run_cpu() {
     expect(d2->n_shapes == 3 && d2->shapes[0].n_triangles == 4 && d2->shapes[2].area_light_first == 0 && d2->n_media == 1 &&
                d2->shapes[0].medium_inside == 0 && d2->lights[1].triangle == 1,
            "area-light scene flattens to mesh runs with bound lights and a medium");
+    add_infinite(a);
+    auto flat3 = FlattenScene(*a.scene, nullptr);
+    const pbr_scene_desc* d3 = SceneDesc(*flat3);
+    expect(d3->n_lights == 3 && d3->lights[2].type == PBR_LIGHT_INFINITE_AREA && d3->lights[2].env_width == 60 &&
+               d3->lights[2].env_data != nullptr && a.scene->infiniteLights.size() == 1,
+           "InfiniteAreaLight flattens with its image and is an infinite light");
     // Render must fail loudly without a device (no CPU fallback)
     FrameBuffer fb;
     fb.InitBuffer(32, 32, 4);
@@ -224,6 +245,17 @@ int run_gpu() {
         auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
         auto v = std::make_shared<VolPathIntegrator>(10, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 1.f, "uniform", &fb);
         compare("VolPath homogeneous medium", b, v, fb, PBR_INTEGRATOR_VOLPATH, spp, 10, 1.f);
+    }
+    {   // main.cpp's own configuration: VolPath d10 "uniform" + the rotated InfiniteAreaLight
+        Built b;
+        const int W = 40, H = 32, spp = 8;
+        build_area(b, W, H, true);
+        add_infinite(b);
+        FrameBuffer fb;
+        fb.InitBuffer(W, H, 4);
+        auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        auto v = std::make_shared<VolPathIntegrator>(10, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 1.f, "uniform", &fb);
+        compare("VolPath medium + InfiniteAreaLight", b, v, fb, PBR_INTEGRATOR_VOLPATH, spp, 10, 1.f);
     }
     return failures ? 1 : 0;
 }

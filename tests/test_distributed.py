@@ -29,10 +29,13 @@ def _worker(rank, world, port, out_path):
     W, H = rd.camera.width, rd.camera.height
     tiles = tiles_for_rank(W, H, rank, world)
     rdr = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, tiles=tiles)
-    rgb, _, _ = oracle_lib.render(scene, rdr, threads=2)
+    rgb, rgba, _ = oracle_lib.render(scene, rdr, threads=2)
     frame = gather_frame(torch.from_numpy(rgb), W, H, rank, world)
+    # the RGBA8 FrameBuffer spans (what bench.py gathers over RCCL)
+    frame8 = gather_frame(torch.from_numpy(np.ascontiguousarray(rgba.reshape(-1, 4))), W, H, rank, world)
     if rank == 0:
         np.save(out_path, frame)
+        np.save(out_path + ".u8.npy", frame8)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -44,8 +47,9 @@ def test_two_rank_tile_gather_reassembles_frame(tmp_path):
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     frame = np.load(out)
     scene, rd = scenes.config_c1(150, 100, 2)
-    full, _, _ = oracle_lib.render(scene, rd, threads=2)
+    full, full8, _ = oracle_lib.render(scene, rd, threads=2)
     assert np.array_equal(frame.reshape(-1, 3).view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(np.load(out + ".u8.npy").reshape(-1, 4), full8.reshape(-1, 4))
     # both ranks own work and no tile is dealt twice
     t0, t1 = tiles_for_rank(150, 100, 0, 2), tiles_for_rank(150, 100, 1, 2)
     assert t0 and t1 and not set(t0) & set(t1)
