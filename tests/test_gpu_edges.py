@@ -1,0 +1,122 @@
+"""Edge cases of the device path against the oracle (SURVEY §8(c) fixture list, items 3 and 7-8):
+exact edge/vertex hits that take the watertight test's double-precision fallback
+(Triangle.cpp:102-113) and its t == tMax ties (F8), empty and light-less scenes, degenerate frame
+and tile shapes, non-power-of-two spp, and the full-size C3/C5 frames checked through
+size-independent properties plus spot pixels."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from pysicalbasedraytracer_amd import HipRenderer, capi, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    r = HipRenderer(0)
+    yield r
+    r.close()
+
+
+def grid_mesh(n=6, z=0.0):
+    """n×n unit squares in the z plane, two triangles each, vertices on integer coordinates."""
+    xs = np.arange(n + 1, dtype=np.float32)
+    P = np.array([(x, y, z) for y in xs for x in xs], np.float32)
+    I = []
+    for j in range(n):
+        for i in range(n):
+            a, b, c, d = j * (n + 1) + i, j * (n + 1) + i + 1, (j + 1) * (n + 1) + i, (j + 1) * (n + 1) + i + 1
+            I += [(a, b, d), (a, d, c)]
+    return P, np.array(I, np.int32)
+
+
+def test_edge_and_vertex_hits_bit_exact(hip):
+    """Axis-aligned rays through shared edges, diagonals and vertices make an edge function exactly
+    zero (the double fallback) and hit two triangles at the same t (later primitive wins)."""
+    s = scenes.Scene()
+    m = s.matte((0.5, 0.5, 0.5))
+    P, I = grid_mesh(6)
+    s.mesh(P, I, m)
+    s.mesh(P + np.float32([0.0, 0.0, -1.0]), I, m)   # a second sheet: ties across meshes behind
+    hip.upload(s)
+    pts = np.array([(x, y) for x in np.arange(0, 6.01, 0.5) for y in np.arange(0, 6.01, 0.5)], np.float32)
+    rays = []
+    for x, y in pts:
+        rays.append((x, y, 2.0, 0.0, 0.0, -1.0, np.inf))        # straight down
+        rays.append((x, y, 2.0, 0.25, -0.5, -1.0, np.inf))      # oblique
+        rays.append((x, y, -3.0, 0.0, 0.0, 1.0, 4.0))           # from below, tMax at the top sheet
+    rays = np.array(rays, np.float32)
+    for any_hit in (False, True):
+        g = hip.intersect(rays, any_hit)
+        c = O.intersect(s, rays, any_hit)
+        assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+    assert (c[:, 0] > 0).sum() > len(rays) // 2
+
+
+def test_scene_without_geometry_and_without_lights(hip):
+    """No primitives (an empty BVH): every camera ray escapes — the F4 grey 0.8 per light under
+    Whitted, black without lights; Path sees only infinite lights."""
+    cam = scenes.camera(8, 6, (0, 0, 3), (0, 0, 0))
+    s = scenes.Scene()
+    s.point_light((0.0, 2.0, 0.0), (5.0, 5.0, 5.0))
+    hip.upload(s)
+    g, g8, _ = hip.render(scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 2, 5))
+    c, c8, _ = O.render(s, scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 2, 5))
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)) and np.allclose(g, 0.8)
+    s2 = scenes.Scene()
+    s2.sphere((0.0, 0.0, 0.0), 1.0, s2.matte((0.5, 0.5, 0.5)))
+    hip.upload(s2)
+    for integ in (capi.INTEGRATOR_WHITTED, capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH):
+        rd = scenes.render_desc(cam, integ, 2, 5)
+        g, _, _ = hip.render(rd)
+        c, _, _ = O.render(s2, rd)
+        assert np.array_equal(g.view(np.uint32), c.view(np.uint32)) and not g.any()
+
+
+@pytest.mark.parametrize("w,h,spp", [(1, 1, 1), (7, 3, 3), (65, 1, 5), (1, 130, 2)])
+def test_degenerate_frames_and_odd_spp(hip, w, h, spp):
+    s, _ = scenes.config_c1(w, h, spp)
+    cam = scenes.camera(w, h, (0.0, 0.0, 5.0), (0.0, 0.0, 0.0))
+    hip.upload(s)
+    for integ in (capi.INTEGRATOR_WHITTED, capi.INTEGRATOR_PATH):
+        rd = scenes.render_desc(cam, integ, spp, 5)
+        g, g8, st = hip.render(rd)
+        c, c8, _ = O.render(s, rd)
+        assert np.abs(g - c).max() <= 1e-3 and np.abs(g8.astype(int) - c8.astype(int)).max() <= 1
+        assert st.samples == w * h * spp
+
+
+def test_ragged_tiles_and_single_pixel_tiles(hip):
+    """Tiles that do not divide the frame, single pixels and a 1-row strip, in arbitrary order."""
+    s, rd = scenes.config_c2(100, 37, 2, mesh=scenes.dragon_standin(n=32) + ("s",),
+                             sky=np.ones((8, 16, 3), np.float32))
+    tiles = [(64, 32, 100, 37), (0, 0, 1, 1), (99, 36, 100, 37), (3, 10, 97, 11), (0, 0, 64, 32)]
+    rdt = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, tiles=tiles)
+    hip.upload(s)
+    g, g8, st = hip.render(rdt)
+    c, c8, _ = O.render(s, rdt)
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32)) and np.array_equal(g8, c8)
+    assert st.samples == sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles) * 2
+
+
+@pytest.mark.parametrize("config", ["C3", "C5"])
+def test_full_size_path_volpath_properties(hip, config):
+    """BASELINE sizes of C3 (1080p, 256 spp, Path, Sobol) and C5 (1080p, 512 spp, VolPath):
+    finite, non-negative, deterministic frames; 24 spot pixels within the L∞ tolerance of the
+    oracle (same sampler indices: the pixels are rendered as one-pixel tiles on the CPU)."""
+    s, rd = scenes.CONFIGS[config]()
+    W, H = rd.camera.width, rd.camera.height
+    hip.upload(s)
+    g, g8, st = hip.render(rd)
+    assert g.shape == (W * H, 3) and np.isfinite(g).all() and (g >= 0).all()
+    assert st.samples == W * H * rd.spp
+    rng = np.random.default_rng(7)
+    picks = rng.integers(0, W * H, 24)
+    tiles = [(int(p % W), int(p // W), int(p % W) + 1, int(p // W) + 1) for p in picks]
+    rdt = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                             rd.sampler, tiles=tiles)
+    c, c8, _ = O.render(s, rdt)
+    assert np.abs(g[picks] - c).max() <= 1e-3
+    again, _, _ = hip.render(rdt)
+    assert np.array_equal(again.view(np.uint32), g[picks].view(np.uint32))
