@@ -37,16 +37,29 @@ __host__ __device__ __forceinline__ HaltonParams hparams(const DeviceSampler& s)
     return h;
 }
 
-// The low Halton dimensions a bounce loop samples over and over, staged in LDS by the kernels that
-// ask for it (LDS = true): one scrambled radical inverse is a chain of dependent digit-permutation
-// lookups, and ds_read latency is a fraction of an L1/L2 round trip.
+// The low sampler dimensions a bounce loop samples over and over, staged in LDS by the kernels
+// that ask for it (LDS = true).  Halton: one scrambled radical inverse is a chain of dependent
+// digit-permutation lookups, and ds_read latency is a fraction of an L1/L2 round trip.  Sobol: the
+// nibble tables of the first kLdsSobolDims dimensions (below).  One LDS array serves both.
 constexpr int kLdsDims = 64;
 constexpr int kLdsPermEntries = 8893;              // Σ of the first 64 primes
-__shared__ uint16_t s_halton_perm[kLdsPermEntries];
+constexpr int kSobolNib = 128;                     // words per dimension: 8 nibble positions × 16
+constexpr int kLdsSobolDims = 34;                  // 34 × 512 B fit the Halton permutation array
+static_assert(kLdsSobolDims * kSobolNib * 4 <= kLdsPermEntries * 2, "Sobol LDS tables share the Halton array");
+__shared__ __align__(16) uint16_t s_halton_perm[kLdsPermEntries];
 __shared__ uint4 s_halton_tab[kLdsDims];           // prime, floor(2^32/prime), primeSums
 
+__device__ __forceinline__ int sobol_lds_dims(const DeviceSampler& s) {
+    return min(min(s.ldsDims, kLdsSobolDims), s.nSobolDims);
+}
 // Whole workgroup; call before the first LDS sample and follow with __syncthreads().
 __device__ void stage_halton_lds(const DeviceSampler& s) {
+    if (s.type == PBR_SAMPLER_SOBOL) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_halton_perm);
+        const int n = sobol_lds_dims(s) * kSobolNib;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = s.sobol[i];
+        return;
+    }
     const int nd = s.ldsDims;
     for (int i = threadIdx.x; i < nd; i += blockDim.x)
         s_halton_tab[i] = make_uint4(s.primes[i], s.recips[i], s.primeSums[i], 0u);
@@ -56,13 +69,21 @@ __device__ void stage_halton_lds(const DeviceSampler& s) {
 
 // pbrt-v3 SobolSampler::SampleDimension (Sobol.cpp) over SobolSampleFloat (LowDiscrepancy.h):
 // XOR of the generator columns of the set index bits, v·2^-32 narrowed, dims 0/1 remapped into
-// the pixel.  Dimensions beyond the matrices read 0 (pbrt aborts there).
+// the pixel.  Dimensions beyond the matrices read 0 (pbrt aborts there).  The XOR over the 32
+// index bits is regrouped by nibble (XOR is associative and commutative, so v is unchanged):
+// T[8k + n] = XOR of columns 4k..4k+3 selected by n (prepare_sobol), eight independent lookups
+// instead of a loop of up to 32 dependent column loads.
+__device__ __forceinline__ uint32_t sobol_nibbles(const uint32_t* T, uint32_t index) {
+    return T[index & 15u] ^ T[16 + ((index >> 4) & 15u)] ^ T[32 + ((index >> 8) & 15u)] ^ T[48 + ((index >> 12) & 15u)] ^
+           T[64 + ((index >> 16) & 15u)] ^ T[80 + ((index >> 20) & 15u)] ^ T[96 + ((index >> 24) & 15u)] ^
+           T[112 + (index >> 28)];
+}
+template <bool LDS = false>
 __device__ __forceinline__ float sobol_dimension(const DeviceSampler& s, uint32_t index, int dim, int px, int py) {
     if (dim >= s.nSobolDims) return 0.f;
-    const uint32_t* M = s.sobol + (size_t)dim * kSobolMatrixSize;
-    uint32_t v = 0;
-    for (int c = 0; index != 0; index >>= 1, ++c)
-        if (index & 1u) v ^= M[c];
+    uint32_t v;
+    if (LDS && dim < sobol_lds_dims(s)) v = sobol_nibbles(reinterpret_cast<const uint32_t*>(s_halton_perm) + dim * kSobolNib, index);
+    else v = sobol_nibbles(s.sobol + (size_t)dim * kSobolNib, index);
     float f = mn((float)v * 2.3283064365386963e-10f, kOneMinusEpsilon);
     if (dim <= 1) {
         f = f * (float)s.sobolRes;   // + sampleBounds.pMin[dim] == 0
@@ -91,7 +112,7 @@ __device__ __forceinline__ uint32_t sample_index(const DeviceSampler& smp, int x
 
 template <bool LDS = false>
 __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int dim, int px = 0, int py = 0) {
-    if (s.type == PBR_SAMPLER_SOBOL) return sobol_dimension(s, index, dim, px, py);
+    if (s.type == PBR_SAMPLER_SOBOL) return sobol_dimension<LDS>(s, index, dim, px, py);
     // HaltonSampler::SampleDimension (Halton.cpp:83-92)
     if (dim == 0) return radical_inverse_2(index >> s.baseExp0);
     if (dim == 1) return radical_inverse_b(3u, 0x55555555u, div_prime(index, (uint32_t)s.baseScale1, 0xffffffffu / (uint32_t)s.baseScale1));
@@ -741,8 +762,17 @@ int prepare_sobol(pbr_hip_ctx* ctx, const uint32_t* user, int userDims, int w, i
     if (dims < 2) return set_err(ctx, PBR_E_INVALID, "Sobol needs at least 2 dimensions of matrices");
     if (src != ctx->sobolSrc || dims != ctx->sobolSrcDims) {
         if (int rc = drain(ctx)) return rc;
-        HIP_TRY(ctx->dSobol.ensure((size_t)dims * kSobolMatrixSize * 4));
-        HIP_TRY(hipMemcpyAsync(ctx->dSobol.p, src, (size_t)dims * kSobolMatrixSize * 4, hipMemcpyHostToDevice, ctx->stream));
+        // nibble tables of the first 32 columns (the device index is 32-bit, sobol_nibbles)
+        std::vector<uint32_t> nib((size_t)dims * kSobolNib, 0u);
+        for (int d = 0; d < dims; ++d)
+            for (int k = 0; k < 8; ++k)
+                for (int n = 0; n < 16; ++n) {
+                    uint32_t v = 0;
+                    for (int b = 0; b < 4; ++b)
+                        if ((n >> b) & 1) v ^= src[(size_t)d * kSobolMatrixSize + 4 * k + b];
+                    nib[(size_t)d * kSobolNib + 16 * k + n] = v;
+                }
+        HIP_TRY(ctx->dSobol.upload(nib, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         ctx->sobolSrc = src;
         ctx->sobolSrcDims = dims;
