@@ -646,6 +646,7 @@ struct DevBuf {
 struct WfBufs {
     DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
     DevBuf wsO2, wsD2, wsC2, wsId2;   // Whitted: second shadow queue (levels alternate)
+    DevBuf wRecC, wRecV;              // multi-light Whitted: per-light contributions, visibility
     // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
     DevBuf wpO, wpD, wpId, wdId, sL, sBeta, rA, rB, rBeta, rLi, rFlags, rLight;
     DevBuf wtO, wtD, wtP, wtE, wtN, wtId, rLiA, rTr, rWA;   // VolPath transmittance walk
@@ -826,9 +827,9 @@ struct WfChunks {
     int segCap = 0;   // capacity of one queue segment
     size_t qcap = 0;  // queue entries
 };
-WfChunks wf_chunks(const KParams& P) {
+WfChunks wf_chunks(const KParams& P, int maxLog2 = 25) {
     WfChunks c;
-    int chunkLog2 = 25;
+    int chunkLog2 = maxLog2;
     if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
     c.lanes = kWfLanes;
     if (const char* e = getenv("PBR_LANES")) c.lanes = std::min(kWfLanes, std::max(1, atoi(e)));
@@ -874,9 +875,17 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const int spp = P.spp;
     // samples per chunk: queue + record memory ≈ 370 B per sample at depth 5 (12 GB at 2^25);
     // measured on C2 (one lane): 2^23 29.4 ms, 2^24 28.1, 2^25 26.6, 2^27 (whole frame) 26.6
-    const WfChunks ch = wf_chunks(P);
-    const size_t cap = ch.cap, qcap = ch.qcap;
     const int levels = P.maxDepth < 1 ? 1 : P.maxDepth;
+    // multi-light scenes (k_wf_shade_ml): per (level, light) records of 17 B per sample and up to
+    // nL shadow rays per shading event; the chunk shrinks so those stay near 6 GB per lane
+    const int nL = (int)ctx->host.lights.size();
+    const bool ml = nL != 1;
+    int maxLog2 = 25;
+    while (ml && nL > 0 && maxLog2 > 20 && (double)levels * nL * 17.0 * (double)(1LL << maxLog2) > 6e9) --maxLog2;
+    const WfChunks ch = wf_chunks(P, maxLog2);
+    const size_t cap = ch.cap, qcap = ch.qcap;
+    const int lightsPerShade = ml ? std::max(1, nL) : 1;
+    const size_t sqcap = qcap * (size_t)lightsPerShade;   // shadow-queue entries
     int lobes = 0;
     for (const MatTemplate& m : ctx->host.materials)
         for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
@@ -902,14 +911,15 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             HIP_TRY(B.wqO[k].ensure(qcap * 16)); HIP_TRY(B.wqD[k].ensure(qcap * 16));
             HIP_TRY(B.wqId[k].ensure(qcap * 4)); HIP_TRY(B.wqHit[k].ensure(qcap * 16));
         }
-        HIP_TRY(B.wsO.ensure(qcap * 16)); HIP_TRY(B.wsD.ensure(qcap * 16));
-        HIP_TRY(B.wsC.ensure(qcap * 16)); HIP_TRY(B.wsId.ensure(qcap * 4));
+        HIP_TRY(B.wsO.ensure(sqcap * 16)); HIP_TRY(B.wsD.ensure(sqcap * 16));
+        HIP_TRY(B.wsC.ensure(qcap * 16)); HIP_TRY(B.wsId.ensure(sqcap * 4));
+        if (ml) { HIP_TRY(B.wRecC.ensure(cap * 16 * levels * nL)); HIP_TRY(B.wRecV.ensure(cap * levels * nL)); }
         HIP_TRY(B.wRecA.ensure(cap * 16 * levels)); HIP_TRY(B.wRecF.ensure(cap * 16 * levels));
         HIP_TRY(B.wRecP.ensure(cap * 4 * levels)); HIP_TRY(B.wDepth.ensure(cap * 4));
         HIP_TRY(B.wIndex.ensure(cap * 4));
         if (shadowOverlap) {
-            HIP_TRY(B.wsO2.ensure(qcap * 16)); HIP_TRY(B.wsD2.ensure(qcap * 16));
-            HIP_TRY(B.wsC2.ensure(qcap * 16)); HIP_TRY(B.wsId2.ensure(qcap * 4));
+            HIP_TRY(B.wsO2.ensure(sqcap * 16)); HIP_TRY(B.wsD2.ensure(sqcap * 16));
+            HIP_TRY(B.wsC2.ensure(qcap * 16)); HIP_TRY(B.wsId2.ensure(sqcap * 4));
             if (!ctx->shadowStream[l]) {
                 HIP_TRY(hipStreamCreateWithFlags(&ctx->shadowStream[l], hipStreamNonBlocking));
                 for (int k = 0; k < kWfMaxDepth + 2; ++k) {
@@ -926,12 +936,16 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         W.so = (float4*)B.wsO.p; W.sd = (float4*)B.wsD.p; W.sc = (float4*)B.wsC.p; W.sid = (int*)B.wsId.p;
         W.shadowSeg = cnt + 2 * kWfBlocks;
         W.segCap = ch.segCap;
+        W.shadowSegCap = ch.segCap * lightsPerShade;
+        W.nLightsML = ml ? nL : 0;
+        W.recC = ml ? (float4*)B.wRecC.p : nullptr;
+        W.recV = ml ? (uint8_t*)B.wRecV.p : nullptr;
         W.recA = (float4*)B.wRecA.p; W.recF = (float4*)B.wRecF.p; W.recP = (float*)B.wRecP.p;
         W.depthOf = (int*)B.wDepth.p;
         W.sampleIndex = (uint32_t*)B.wIndex.p;
         W.initRecords = ctx->host.anyNoMaterial ? 1 : 0;
-        // Halton dims one sample reaches: 5 camera + 4 per level (light 2D, SpecularReflect 2D)
-        W.P.smp.ldsDims = std::min(kLdsDims, 5 + 4 * levels + 2);
+        // Halton dims one sample reaches: 5 camera + per level 2 per light + 2 (SpecularReflect)
+        W.P.smp.ldsDims = std::min(kLdsDims, 5 + (2 * lightsPerShade + 2) * levels + 2);
         W.cap = (int)cap;
     }
     auto queue = [&](int l, int k) {
@@ -947,6 +961,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const char* ePers = getenv("PBR_RESIDENT_GRID");
     const bool pers = !(ePers && ePers[0] == '0');
     const dim3 gShadow = pers ? resident_grid(ctx, shortStack ? (const void*)k_wf_shadow<kShortStack> : (const void*)k_wf_shadow<0>) : gstride;
+    const dim3 gShadowML = pers ? resident_grid(ctx, (const void*)k_wf_shadow_ml<kShortStack>) : gstride;
     const dim3 gExtend = pers ? resident_grid(ctx, shortStack ? (const void*)k_wf_extend<kShortStack> : (const void*)k_wf_extend<0>) : gstride;
     if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
     int chunk = 0;
@@ -975,7 +990,12 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 if (level >= 2) HIP_TRY(hipStreamWaitEvent(st, ctx->evShadow[l][level - 2], 0));
             }
             const int l0 = level == 0 ? 1 : 0;
-            if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
+            if (ml) {
+                if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
+                else if (simple) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
+                else if (matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, true>), gstride, blk, 0, st, W, l0);
+                else hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, false>), gstride, blk, 0, st, W, l0);
+            } else if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
             else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, st, W, l0);
             else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, st, W, l0);
@@ -983,7 +1003,8 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 HIP_TRY(hipEventRecord(ctx->evShade[l][level], st));
                 HIP_TRY(hipStreamWaitEvent(sst, ctx->evShade[l][level], 0));
             }
-            if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, sst, W);
+            if (ml) hipLaunchKernelGGL(k_wf_shadow_ml<kShortStack>, gShadowML, blk, 0, sst, W);
+            else if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, sst, W);
             else hipLaunchKernelGGL(k_wf_shadow<0>, gShadow, blk, 0, sst, W);
             if (shadowOverlap) HIP_TRY(hipEventRecord(ctx->evShadow[l][level], sst));
             if (level + 1 == maxLevels) break;
@@ -1046,6 +1067,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         W.so = (float4*)B.wsO.p; W.sd = (float4*)B.wsD.p; W.sid = (int*)B.wsId.p;
         W.shadowSeg = cnt + 2 * kWfBlocks;
         W.segCap = ch.segCap;
+        W.shadowSegCap = ch.segCap;
         W.sampleIndex = (uint32_t*)B.wIndex.p;
         W.cap = (int)cap;
         X.po = (float4*)B.wpO.p; X.pd = (float4*)B.wpD.p; X.pid = (int*)B.wpId.p;
@@ -1344,7 +1366,7 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (blocks > 0) {
         bool st = d->collect_stats != 0;
         const char* wfEnv = getenv("PBR_WAVEFRONT");
-        bool wavefront = d->integrator == PBR_INTEGRATOR_WHITTED && !st && ctx->host.lights.size() == 1 &&
+        bool wavefront = d->integrator == PBR_INTEGRATOR_WHITTED && !st && ctx->host.lights.size() <= (size_t)kWfMaxLightsML &&
                          d->max_depth <= kWfMaxDepth && !(wfEnv && wfEnv[0] == '0');
         bool wavefrontPath = (d->integrator == PBR_INTEGRATOR_PATH || d->integrator == PBR_INTEGRATOR_VOLPATH) && !st &&
                              d->max_depth <= 120 && ctx->host.media.size() / 10 < 255 && !(wfEnv && wfEnv[0] == '0');

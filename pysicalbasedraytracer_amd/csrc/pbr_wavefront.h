@@ -48,6 +48,12 @@ struct WfParams {
     uint32_t* sampleIndex; // Halton global index of each sample (GlobalSampler::SetSampleNumber)
     int cap;               // record stride (>= nSamples)
     int initRecords;       // some primitive has no material (Whitted's pass-through branch)
+    int shadowSegCap;      // capacity of one shadow-queue segment (segCap × lights per shade)
+    // multi-light Whitted (k_wf_shade_ml): per (level, light, sample) the light's contribution and
+    // whether its shadow ray got through, [(depth * nLightsML + light) * cap + id]
+    float4* recC;
+    uint8_t* recV;
+    int nLightsML;         // 0: the single-light schedule
 };
 
 // LDS counter; the wave's lanes must be converged
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;   // <= segCap / 256: a segment holds all pushes
-    const int base = blockIdx.x * W.segCap;
+    const int base = blockIdx.x * W.segCap, sbase = blockIdx.x * W.shadowSegCap;
     for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
         const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
         const bool active = i < n;
@@ -276,7 +282,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                 }
             }
         }
-        int si = base + wave_push(&s_push[0], pushShadow);
+        int si = sbase + wave_push(&s_push[0], pushShadow);
         if (pushShadow) {   // the visibility result lands in the level that emitted the ray
             W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
             W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(emitDepth));
@@ -299,7 +305,7 @@ template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int q = seg_pos(W.segCap, i);
+        const int q = seg_pos(W.shadowSegCap, i);
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
@@ -321,6 +327,177 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
 // (conflict-free), then one thread per (pixel, channel) adds that pixel's samples in sample order
 // — the reference's colObj += Li order; Spectrum addition is per channel — and one thread per
 // pixel runs the film.
+// One level of WhittedIntegrator::Li for scenes with 2..kWfMaxLightsML lights.  The light loop
+// (WhittedIntegrator.cpp:39-54) runs for every lane of the wave — lanes with nothing to shade just
+// consume no sampler dimensions — so each light's shadow rays are pushed with one ballot; a light
+// whose shadow ray is pushed leaves its contribution in recC and recV = 0, which k_wf_shadow_ml
+// turns to 1 when the ray gets through.  Everything else is k_wf_shade.
+constexpr int kWfMaxLightsML = 8;
+template <int LOBES, bool MATS_LDS, int OCC = (LOBES & ~kSimpleLobes) ? 2 : 3>
+__global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0) {
+    const KParams& P = W.P;
+    const DeviceScene& S = P.S;
+    stage_halton_lds(P.smp);
+    const MatTemplate* mats = S.materials;
+    if constexpr (MATS_LDS) {
+        constexpr int words = (int)(sizeof(MatTemplate) / 4);
+        const int n = 2 * S.nMaterials * words;
+        const uint32_t* src = (const uint32_t*)S.materials;
+        uint32_t* dst = (uint32_t*)s_mats;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+        mats = s_mats;
+    }
+    __shared__ int s_push[2];   // shadow, next
+    if (threadIdx.x < 2) s_push[threadIdx.x] = 0;
+    __syncthreads();
+    const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
+    const int stride = gridDim.x * blockDim.x;
+    const int nIter = (n + stride - 1) / stride;
+    const int base = blockIdx.x * W.segCap, sbase = blockIdx.x * W.shadowSegCap;
+    const int nL = W.nLightsML;
+    for (int it = 0; it < nIter; ++it) {
+        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const bool active = i < n;
+        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
+        bool pushNext = false, shading = false, nonSpecular = false;
+        int id = 0, depth = 0, dim = 0;
+        Ray ray, cont;
+        Isect isect;
+        BSDF bsdf;
+        rgb L = sp(0.f);
+        SState st;
+        st.index = 0; st.dim = 0; st.px = st.py = 0;
+        if (active) {
+            float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
+            id = level0 ? q : W.cur.id[q];
+            int dd = __float_as_int(d.w);
+            dim = dd & 0xffff;
+            depth = dd >> 16;
+            ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+            int slot = __float_as_int(hr.x);
+            if (slot < 0) {   // miss: Σ over all lights of Le (F4); no direct light at this level
+                for (int k = 0; k < S.nLights; ++k) L = L + light_Le(S, S.lights[k], ray);
+                W.recA[(size_t)depth * W.cap + id] = make_float4(L.r, L.g, L.b, 0.f);
+                for (int k = 0; k < nL; ++k) W.recV[((size_t)depth * nL + k) * W.cap + id] = 0;
+                W.depthOf[id] = depth;
+            } else {
+                int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
+                if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
+                else triangle_si(S, slot, ray, hr.y, hr.z, hr.w, flags, &isect);
+                isect.slot = slot;
+                isect.medIn = isect.medOut = -1;
+                if (!make_bsdf(S, mats, isect, false, &bsdf)) {
+                    cont = spawn_ray(isect, ray.d);        // Li(isect.SpawnRay(ray.d), depth)
+                    pushNext = true;
+                } else {
+                    shading = true;
+                    L = sp(0.f) + si_Le(S, isect, isect.wo);
+                    st.index = W.sampleIndex[id];
+                    st.dim = dim;
+                    nonSpecular = num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0;
+                }
+            }
+        }
+        for (int k = 0; k < nL; ++k) {   // uniform trip count: one ballot per light
+            bool push = false;
+            Ray shadow;
+            if (shading) {
+                float a, b;
+                get2d<true>(P.smp, st, &a, &b);
+                const size_t ci = ((size_t)depth * nL + k) * W.cap + id;
+                W.recV[ci] = 0;
+                if (nonSpecular) {   // f ≡ 0 for a purely specular BSDF: nothing would be added
+                    f3 wi;
+                    float pdf;
+                    VisPt vis;
+                    rgb Li = sample_li(S, S.lights[k], isect, a, b, &wi, &pdf, &vis);
+                    if (!(black(Li) || pdf == 0)) {
+                        rgb f = bsdf_f<LOBES>(bsdf, isect.wo, wi, BSDF_ALL);
+                        if (!black(f)) {
+                            rgb c = f * Li * absdot(wi, isect.sn) / pdf;
+                            W.recC[ci] = make_float4(c.r, c.g, c.b, 0.f);
+                            shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
+                            push = true;
+                        }
+                    }
+                }
+            }
+            const int si = sbase + wave_push(&s_push[0], push);
+            if (push) {
+                W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
+                W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(depth | (k << 8)));
+                W.sid[si] = id;
+            }
+        }
+        if (shading) {
+            const size_t ri = (size_t)depth * W.cap + id;
+            float flagsA = 0.f;
+            bool final_ = true;
+            if (depth + 1 < P.maxDepth) {   // SpecularReflect (Integrator.cpp:179-222)
+                f3 wi = mk(0, 0, 0);
+                float pdf = 0;
+                int stype = 0;
+                float a, b;
+                get2d<true>(P.smp, st, &a, &b);
+                rgb f = bsdf_sample<(1 << L_SPEC_R)>(bsdf, isect.wo, &wi, a, b, &pdf, BSDF_REFLECTION | BSDF_SPECULAR, &stype);
+                if (!black(f) && pdf > 0.f && absdot(wi, isect.sn) != 0.f && depth + 1 < kWfMaxDepth) {
+                    W.recF[ri] = make_float4(f.r, f.g, f.b, absdot(wi, isect.sn));
+                    W.recP[ri] = pdf;
+                    cont = spawn_ray(isect, wi);
+                    pushNext = true;
+                    final_ = false;
+                    depth += 1;
+                } else {
+                    flagsA = 1.f;   // L += Spectrum(0) from a failed SpecularReflect
+                }
+            }
+            W.recA[ri] = make_float4(L.r, L.g, L.b, flagsA);
+            if (final_) W.depthOf[id] = depth;
+            dim = st.dim;
+        }
+        const int ni = base + wave_push(&s_push[1], pushNext);
+        if (pushNext) {
+            W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
+            W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_dd(dim, depth)));
+            W.next.id[ni] = id;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { W.shadowSeg[blockIdx.x] = s_push[0]; W.next.segCount[blockIdx.x] = s_push[1]; }
+}
+
+// any-hit for the multi-light shadow queue: the ray's (level, light) record turns visible
+template <int SHORT>
+__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow_ml(WfParams W) {
+    const int n = seg_scan(W.shadowSeg);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int q = seg_pos(W.shadowSegCap, i);
+        float4 o = W.so[q], d = W.sd[q];
+        Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+        HitRec h;
+        Counters c;
+        if (!traverse<true, false, SHORT>(W.P.S, r, &h, &c)) {
+            const int code = __float_as_int(d.w);
+            W.recV[((size_t)(code & 0xff) * W.nLightsML + (code >> 8)) * W.cap + W.sid[q]] = 1;
+        }
+    }
+}
+
+// Le plus the direct light of one level: single-light records already hold the sum (k_wf_shadow
+// adds it); multi-light ones add each light's contribution whose shadow ray got through, in the
+// order of WhittedIntegrator's light loop (WhittedIntegrator.cpp:39-54).
+__device__ __forceinline__ rgb level_direct(const WfParams& W, int lv, int id, float4 A) {
+    rgb L = sp3(A.x, A.y, A.z);
+    for (int k = 0; k < W.nLightsML; ++k) {
+        const size_t ci = ((size_t)lv * W.nLightsML + k) * W.cap + id;
+        if (W.recV[ci]) {
+            const float4 c = W.recC[ci];
+            L = L + sp3(c.x, c.y, c.z);
+        }
+    }
+    return L;
+}
+
 constexpr int kFinishSamples = 2048;
 __host__ __device__ inline int finish_pixels(int spp) {
     int pb = kFinishSamples / spp;
@@ -345,13 +522,13 @@ __global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
             const int id = (lp0 + p) * spp + k;
             const int dpt = W.depthOf[id];
             float4 a = W.recA[(size_t)dpt * W.cap + id];
-            rgb L = sp3(a.x, a.y, a.z);
+            rgb L = level_direct(W, dpt, id, a);
             if (a.w != 0.f) L = L + sp(0.f);
             for (int lv = dpt - 1; lv >= 0; --lv) {
                 size_t ri = (size_t)lv * W.cap + id;
                 float4 A = W.recA[ri], F = W.recF[ri];
                 float pdf = W.recP[ri];
-                L = sp3(A.x, A.y, A.z) + sp3(F.x, F.y, F.z) * L * F.w / pdf;
+                L = level_direct(W, lv, id, A) + sp3(F.x, F.y, F.z) * L * F.w / pdf;
             }
             const int kk = k - s0;
             lds[(p * 3 + 0) * pitch + kk] = L.r;

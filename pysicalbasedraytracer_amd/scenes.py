@@ -512,4 +512,14 @@ def config_c5(width=1920, height=1080, spp=512, mesh=None):
     return s, render_desc(cam, capi.INTEGRATOR_VOLPATH, spp, 10, rr_threshold=1.0)
 
 
-CONFIGS = {"C1": config_c1, "C2": config_c2, "C3": config_c3, "C4": config_c4, "C5": config_c5}
+def config_c2_lights(width=1920, height=1080, spp=64, mesh=None):
+    """C2 with two extra point lights (three lights): the multi-light Whitted schedule
+    (k_wf_shade_ml).  Not a BASELINE config; used to time it against the megakernel."""
+    s, rd = config_c2(width, height, spp, mesh)
+    s.point_light((1.0, 2.0, 1.5), (6.0, 5.0, 4.0))
+    s.point_light((-1.5, 1.0, 2.0), (3.0, 3.0, 6.0))
+    return s, rd
+
+
+CONFIGS = {"C1": config_c1, "C2": config_c2, "C3": config_c3, "C4": config_c4, "C5": config_c5,
+           "C2L3": config_c2_lights}
