@@ -310,7 +310,7 @@ __device__ rgb uniform_sample_one_light(const KParams& P, const Isect& it, const
 // The recursion L_k = A_k + ((f_k · L_{k+1}) · c_k) / pdf_k is unrolled into a bounded loop; the
 // per-level terms are kept and folded back deepest-first so the float result equals the
 // recursive evaluation.
-constexpr int kMaxWhittedDepth = 8;
+constexpr int kMaxWhittedDepth = 64;   // pbr_hip_render rejects a deeper Whitted maxDepth
 template <bool STATS>
 __device__ rgb whitted_li(const KParams& P, Ray ray, SState& st, Counters* c) {
     const DeviceScene& S = P.S;
@@ -880,8 +880,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     // nL shadow rays per shading event; the chunk shrinks so those stay near 6 GB per lane
     const int nL = (int)ctx->host.lights.size();
     const bool ml = nL != 1;
+    // records per sample and level: A, F+cos, pdf (36 B) + per light 17 B; the chunk shrinks so
+    // they stay under 8 GB per lane (C2: 5 levels × 36 B × 2^25 = 6 GB)
     int maxLog2 = 25;
-    while (ml && nL > 0 && maxLog2 > 20 && (double)levels * nL * 17.0 * (double)(1LL << maxLog2) > 6e9) --maxLog2;
+    while (maxLog2 > 20 && (double)levels * (36.0 + (ml ? 17.0 * nL : 0.0)) * (double)(1LL << maxLog2) > 8e9) --maxLog2;
     const WfChunks ch = wf_chunks(P, maxLog2);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const int lightsPerShade = ml ? std::max(1, nL) : 1;
@@ -896,7 +898,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const char* eMats = getenv("PBR_MATS_LDS");
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
     // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
-    const int maxLevels = levels + (ctx->host.anyNoMaterial ? 2 : 0);
+    const int maxLevels = levels;   // no material-less primitives here (those scenes run the megakernel)
     // Shadow rays of level L run on a second stream, overlapping extend(L+1) and shade(L+1) (they
     // only read what shade(L) wrote); the shadow queue alternates between two buffers by level.
     // Default: when the frame is one chunk (no lane overlap).  Measured on C2: a 1/8 shard
@@ -1094,7 +1096,9 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     const dim3 gProbe = resident_grid(ctx, (const void*)k_wfp_probe<kShortStack>);
     const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack>);
     const dim3 gResolve = resident_grid(ctx, (const void*)k_wfp_resolve);
-    const int maxLevels = std::max(1, P.maxDepth) + 1 + (ctx->host.anyNoMaterial ? 8 : 0);
+    // material-less primitives (medium interfaces) continue a path without a bounce
+    // (PathIntegrator.cpp:70-75): up to 32 such crossings per path are followed
+    const int maxLevels = std::max(1, P.maxDepth) + 1 + (ctx->host.anyNoMaterial ? 32 : 0);
     if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
     int chunk = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
@@ -1269,6 +1273,8 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
     if (d->spp <= 0) return set_err(ctx, PBR_E_INVALID, "spp must be positive");
     if (d->max_depth < 0) return set_err(ctx, PBR_E_INVALID, "max_depth must be >= 0");
+    if (d->integrator == PBR_INTEGRATOR_WHITTED && d->max_depth > kMaxWhittedDepth)
+        return set_err(ctx, PBR_E_UNSUPPORTED, "Whitted max_depth above 64 is not supported");
     if (d->integrator < PBR_INTEGRATOR_WHITTED || d->integrator > PBR_INTEGRATOR_VOLPATH)
         return set_err(ctx, PBR_E_INVALID, "unknown integrator");
     if (d->sampler != PBR_SAMPLER_HALTON && d->sampler != PBR_SAMPLER_SOBOL) return set_err(ctx, PBR_E_INVALID, "unknown sampler");
@@ -1366,7 +1372,10 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (blocks > 0) {
         bool st = d->collect_stats != 0;
         const char* wfEnv = getenv("PBR_WAVEFRONT");
+        // Whitted through material-less primitives recurses at the same depth without bound
+        // (WhittedIntegrator.cpp:26-28): only the megakernel follows such chains to the end
         bool wavefront = d->integrator == PBR_INTEGRATOR_WHITTED && !st && ctx->host.lights.size() <= (size_t)kWfMaxLightsML &&
+                         !ctx->host.anyNoMaterial &&
                          d->max_depth <= kWfMaxDepth && !(wfEnv && wfEnv[0] == '0');
         bool wavefrontPath = (d->integrator == PBR_INTEGRATOR_PATH || d->integrator == PBR_INTEGRATOR_VOLPATH) && !st &&
                              d->max_depth <= 120 && ctx->host.media.size() / 10 < 255 && !(wfEnv && wfEnv[0] == '0');

@@ -21,7 +21,7 @@
 // by sample, so the fold reproduces the recursive evaluation bit for bit in any queue order.
 #pragma once
 
-constexpr int kWfMaxDepth = 8;
+constexpr int kWfMaxDepth = 16;   // Whitted levels of the wavefront schedule (deeper: the megakernel)
 constexpr int kWfBlocks = 2048;   // workgroups of the queue kernels = segments of a queue
 
 struct WfQueue {

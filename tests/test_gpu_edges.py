@@ -120,3 +120,45 @@ def test_full_size_path_volpath_properties(hip, config):
     assert np.abs(g[picks] - c).max() <= 1e-3
     again, _, _ = hip.render(rdt)
     assert np.array_equal(again.view(np.uint32), g[picks].view(np.uint32))
+
+
+@pytest.mark.parametrize("integrator", [capi.INTEGRATOR_WHITTED, capi.INTEGRATOR_PATH])
+def test_spp_beyond_one_finish_tile(hip, integrator):
+    """spp > 2048: the finish kernels fold and sum a pixel's samples in slices of 2048, still in
+    sample order (colObj += Li)."""
+    s, _ = scenes.config_c1(4, 3, 1)
+    cam = scenes.camera(4, 3, (0.0, 0.0, 5.0), (0.0, 0.0, 0.0))
+    rd = scenes.render_desc(cam, integrator, 4100, 5)
+    hip.upload(s)
+    g, g8, st = hip.render(rd)
+    c, c8, _ = O.render(s, rd)
+    assert st.samples == 4 * 3 * 4100
+    assert np.abs(g - c).max() <= 1e-3 and np.abs(g8.astype(int) - c8.astype(int)).max() <= 1
+
+
+def test_deep_whitted_mirror_box(hip, monkeypatch):
+    """Two facing mirrors bounce camera rays until Whitted's depth limit: the wavefront schedule
+    (up to 16 levels) and the megakernel (up to 64) agree bit for bit and with the oracle, and a
+    deeper maxDepth is refused rather than truncated."""
+    s = scenes.Scene()
+    mirror = s.mirror((0.9, 0.9, 0.9))
+    matte = s.matte((0.6, 0.3, 0.2))
+    for z, flip in ((-1.0, False), (1.5, True)):
+        P = np.array([(-3, -3, z), (3, -3, z), (3, 3, z), (-3, 3, z)], np.float32)
+        I = np.array([(0, 1, 2), (0, 2, 3)] if not flip else [(0, 2, 1), (0, 3, 2)], np.int32)
+        s.mesh(P, I, mirror)
+    s.sphere((0.0, 0.0, 0.2), 0.3, matte)
+    s.point_light((0.0, 1.0, 0.5), (4.0, 4.0, 4.0))
+    cam = scenes.camera(40, 30, (0.2, 0.1, 1.2), (0.0, 0.0, -1.0))
+    hip.upload(s)
+    for depth in (5, 12, 16, 40):
+        rd = scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 4, depth)
+        g, g8, _ = hip.render(rd)
+        c, c8, _ = O.render(s, rd)
+        assert np.abs(g - c).max() <= 1e-3 and np.abs(g8.astype(int) - c8.astype(int)).max() <= 1, depth
+        monkeypatch.setenv("PBR_WAVEFRONT", "0")
+        mk, _, _ = hip.render(rd)
+        monkeypatch.delenv("PBR_WAVEFRONT")
+        assert np.array_equal(mk.view(np.uint32), g.view(np.uint32)), depth
+    with pytest.raises(RuntimeError):
+        hip.render(scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 1, 65))
