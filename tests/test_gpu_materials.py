@@ -1,0 +1,118 @@
+"""Material and shape options the BASELINE configs do not exercise, device vs oracle
+(per-pixel L∞ ≤ 1e-3, 8-bit ≤ 1): Oren-Nayar matte (sigma > 0, Reflection.cpp:176-199), an
+anisotropic metal on a mesh with per-vertex UVs (the shading frame follows dpdu,
+Triangle.cpp:148-170), two-sided area lights (DiffuseLight.h:17-19), reversed orientation under a
+handedness-swapping transform, and a material-less medium interface crossed by Path/VolPath."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from pysicalbasedraytracer_amd import HipRenderer, capi, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    r = HipRenderer(0)
+    yield r
+    r.close()
+
+
+def check(hip, s, rd):
+    hip.upload(s)
+    g, g8, _ = hip.render(rd)
+    c, c8, _ = O.render(s, rd)
+    d = float(np.abs(g.astype(np.float64) - c).max())
+    assert np.isfinite(g).all() and d <= 1e-3, d
+    assert np.abs(g8.astype(int) - c8.astype(int)).max() <= 1
+    return g
+
+
+def uv_patch(n=12, z=-0.2):
+    """A wavy n×n patch with per-vertex UVs stretched in u (so dpdu ≠ the edge directions)."""
+    xs = np.linspace(-1.5, 1.5, n + 1, dtype=np.float32)
+    P, UV = [], []
+    for j, y in enumerate(xs):
+        for i, x in enumerate(xs):
+            P.append((x, y * 0.6 - 0.4, z + 0.15 * np.sin(2.0 * x) * np.cos(1.5 * y)))
+            UV.append((3.0 * i / n, j / n))
+    I = []
+    for j in range(n):
+        for i in range(n):
+            a, b, c, d = j * (n + 1) + i, j * (n + 1) + i + 1, (j + 1) * (n + 1) + i, (j + 1) * (n + 1) + i + 1
+            I += [(a, b, d), (a, d, c)]
+    return np.array(P, np.float32), np.array(I, np.int32), np.array(UV, np.float32)
+
+
+def lit_scene(material_fn, two_sided=False, uv=True):
+    s = scenes.Scene()
+    P, I, UV = uv_patch()
+    s.mesh(P, I, material_fn(s), uv=UV if uv else None)
+    s.sphere((0.6, 0.1, 0.3), 0.35, s.matte((0.3, 0.6, 0.3), sigma=25.0))
+    Pl, Il = scenes.quad(1.8, 0.8, flip=True)
+    s.area_light_mesh(Pl, Il, (4.0, 4.0, 4.0), s.matte((0.5, 0.5, 0.5)), n_samples=2, two_sided=two_sided)
+    s.point_light((-1.0, 1.5, 1.5), (3.0, 3.0, 3.0))
+    return s
+
+
+CAM = dict(eye=(0.0, 0.8, 2.6), look=(0.0, -0.2, 0.0))
+
+
+@pytest.mark.parametrize("integrator", [capi.INTEGRATOR_WHITTED, capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH])
+def test_oren_nayar_matte(hip, integrator):
+    s = lit_scene(lambda sc: sc.matte((0.7, 0.5, 0.3), sigma=20.0))
+    cam = scenes.camera(48, 32, CAM["eye"], CAM["look"])
+    check(hip, s, scenes.render_desc(cam, integrator, 8, 5))
+
+
+@pytest.mark.parametrize("uv", [True, False])
+def test_anisotropic_metal_uv_mesh(hip, uv):
+    s = lit_scene(lambda sc: sc.metal(urough=0.05, vrough=0.4), uv=uv)
+    cam = scenes.camera(48, 32, CAM["eye"], CAM["look"])
+    check(hip, s, scenes.render_desc(cam, capi.INTEGRATOR_PATH, 8, 6, sampler=capi.SAMPLER_SOBOL))
+
+
+def test_two_sided_area_light(hip):
+    """The light quad faces down; seen from below (two-sided) it lights the floor, and the
+    camera above sees its back emitting too."""
+    s = lit_scene(lambda sc: sc.plastic(), two_sided=True)
+    cam = scenes.camera(48, 32, (0.0, 2.6, 0.5), (0.0, -0.5, 0.0))
+    for integ in (capi.INTEGRATOR_PATH, capi.INTEGRATOR_WHITTED):
+        check(hip, s, scenes.render_desc(cam, integ, 8, 5))
+
+
+def test_reversed_orientation_mirrored_transform(hip):
+    """ReverseOrientation ^ TransformSwapsHandedness flips the geometric normal
+    (Triangle.cpp:186-190, Shape.h:35): a mirrored (scale -1) emitter mesh and a reversed sphere."""
+    s = scenes.Scene()
+    P, I, UV = uv_patch()
+    s.mesh(P, I, s.matte((0.6, 0.6, 0.6)))
+    xf = scenes.compose(scenes.translate(0.0, 1.8, 0.0), scenes.scale(-1.0, 1.0, 1.0))
+    Pl, Il = scenes.quad(0.0, 0.8, flip=True)
+    s.area_light_mesh(Pl, Il, (4.0, 4.0, 4.0), s.matte((0.5, 0.5, 0.5)), xform=xf)
+    s.sphere((0.5, 0.2, 0.3), 0.3, s.glass(urough=0.0, vrough=0.0), reverse=True)
+    cam = scenes.camera(48, 32, CAM["eye"], CAM["look"])
+    for integ in (capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH):
+        check(hip, s, scenes.render_desc(cam, integ, 8, 6))
+
+
+@pytest.mark.parametrize("integrator", [capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH])
+def test_material_less_medium_interface(hip, integrator, monkeypatch):
+    """A material-less sphere bounding a homogeneous medium (pbrt's interface idiom): rays cross it
+    without a bounce (PathIntegrator.cpp:70-75, VolPathIntegrator.cpp:77-82); the wavefront
+    schedule equals the megakernel bit for bit."""
+    s = scenes.Scene()
+    P, I, UV = uv_patch()
+    s.mesh(P, I, s.matte((0.6, 0.6, 0.6)))
+    med = s.homogeneous_medium(0.3, 1.5, 0.3)
+    s.sphere((0.0, 0.1, 0.2), 0.5, -1, medium_inside=med, medium_outside=-1)
+    s.sphere((0.0, 0.1, 0.2), 0.25, -1)                  # a second pass-through shell inside
+    Pl, Il = scenes.quad(1.8, 0.8, flip=True)
+    s.area_light_mesh(Pl, Il, (4.0, 4.0, 4.0), s.matte((0.5, 0.5, 0.5)))
+    cam = scenes.camera(48, 32, CAM["eye"], CAM["look"])
+    rd = scenes.render_desc(cam, integrator, 8, 6)
+    g = check(hip, s, rd)
+    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    mk, _, _ = hip.render(rd)
+    assert np.array_equal(mk.view(np.uint32), g.view(np.uint32))
