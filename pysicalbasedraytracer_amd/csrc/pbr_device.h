@@ -233,6 +233,19 @@ __shared__ float s_trav_t[kShortStack * 256];
 // in the box) and the passing slots after it are pushed far-last, each re-tested against tMax
 // when popped — the moment the reference would test it.  Slots that fail now would fail later
 // (tMax only shrinks), so primitive tests run in exactly the reference's order (F8 ties).
+// Wave-uniform reads through the scalar cache: a pointer into the constant address space built
+// from a readfirstlane'd index is loaded with s_load (the BVH and the mesh are read-only for the
+// whole render), so a node every active lane visits costs one scalar fetch instead of 64 lanes of
+// vector-L1 traffic.  Switch: PBR_SCALAR_LOADS (results are identical either way).
+#ifndef PBR_SCALAR_LOADS
+#define PBR_SCALAR_LOADS 1
+#endif
+constexpr bool kScalarLoads = PBR_SCALAR_LOADS != 0;
+typedef float ScalarF4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) ScalarF4* ScalarF4Ptr;
+__device__ __forceinline__ ScalarF4Ptr scalar_f4(const float4* p) { return (ScalarF4Ptr)(size_t)p; }
+__device__ __forceinline__ float4 as_f4(ScalarF4 v) { return make_float4(v.x, v.y, v.z, v.w); }
+
 #ifndef PBR_QUAD_TRAVERSAL
 #define PBR_QUAD_TRAVERSAL 1
 #endif
@@ -255,8 +268,15 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
         if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
             int slot = cur & 0x7fffffff;
             while (true) {
-                const float4* tv = S.triVerts + 3 * (size_t)slot;
-                float4 v0 = tv[0], v1 = tv[1], v2 = tv[2];
+                float4 v0, v1, v2;
+                const int uslot = __builtin_amdgcn_readfirstlane(slot);
+                if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {   // one primitive for the wave
+                    const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
+                    v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
+                } else {
+                    const float4* tv = S.triVerts + 3 * (size_t)slot;
+                    v0 = tv[0]; v1 = tv[1]; v2 = tv[2];
+                }
                 int flags = __float_as_int(v0.w);
                 float t, b0 = 0, b1 = 0, b2 = 0;
                 bool hit = (flags & PRIM_SPHERE)
@@ -272,9 +292,21 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
                 ++slot;
             }
         } else {
-            const float4* w = S.quad + 8 * (size_t)cur;
-            float4 LX = w[0], LY = w[1], LZ = w[2], HX = w[3], HY = w[4], HZ = w[5], R = w[6], M = w[7];
-            const int meta = __float_as_int(M.x);
+            float4 LX, LY, LZ, HX, HY, HZ, R;
+            int meta;
+            // Coherent waves (a pixel's samples share a wave) often have every active lane at the
+            // same node: then it is fetched once through the scalar cache.
+            const int ucur = __builtin_amdgcn_readfirstlane(cur);
+            if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
+                const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
+                LX = as_f4(w[0]); LY = as_f4(w[1]); LZ = as_f4(w[2]); HX = as_f4(w[3]); HY = as_f4(w[4]);
+                HZ = as_f4(w[5]); R = as_f4(w[6]);
+                meta = __float_as_int(w[7].x);
+            } else {
+                const float4* w = S.quad + 8 * (size_t)cur;
+                LX = w[0]; LY = w[1]; LZ = w[2]; HX = w[3]; HY = w[4]; HZ = w[5]; R = w[6];
+                meta = __float_as_int(w[7].x);
+            }
             float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
             bool k0 = node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t0) & ((meta >> 8) & 1);
             bool k1 = node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t1) & ((meta >> 9) & 1);
