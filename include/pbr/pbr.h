@@ -37,6 +37,8 @@ class FrameBuffer {
     bool bufferResize(int width = 800, int height = 600);
     bool set_uc(int w, int h, int shifting, const unsigned char& dat);
     bool set_fc(int w, int h, int shifting, const float& dat);
+    // progressive running average (FrameBuffer.h:112-126): f = dat/n + (1 - 1/n)·f, u8 = f·255
+    bool update_f_u_c(int w, int h, int shifting, int renderCount, const float& dat);
     unsigned char* getUCbuffer() { return ubuffer.data(); }
     float* getFCbuffer() { return fbuffer.data(); }   // linear RGB(A) colObj/spp (not in the reference, F7)
     int width = 0, height = 0, channals = 4;
@@ -45,6 +47,13 @@ class FrameBuffer {
     std::vector<unsigned char> ubuffer;
     std::vector<float> fbuffer;
 };
+
+// The two stb_image_write calls main.cpp makes to save the FrameBuffer (main.cpp:419-429), so it
+// compiles unchanged.  The PNG (8-bit grey / grey+alpha / RGB / RGBA for comp 1-4) is written with
+// stored deflate blocks: any PNG reader decodes the same pixels as from stb's compressed file.
+// Returns 1 on success, 0 on failure, like stb.
+void stbi_flip_vertically_on_write(int flag);
+int stbi_write_png(char const* filename, int w, int h, int comp, const void* data, int stride_in_bytes);
 
 namespace PBR {
 

@@ -2,6 +2,7 @@
 // into a pbr_scene_desc and rendered through the C-ABI (include/pbr_hip.h).
 #include "../../include/pbr/pbr.h"
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -45,6 +46,89 @@ bool FrameBuffer::set_fc(int w, int h, int shifting, const float& dat) {
     if (fbuffer.empty() || w >= width || h >= height || w < 0 || h < 0) return false;
     fbuffer[((size_t)w + (size_t)h * width) * channals + shifting] = dat;
     return true;
+}
+
+bool FrameBuffer::update_f_u_c(int w, int h, int shifting, int renderCount, const float& dat) {
+    if (fbuffer.empty() || w >= width || h >= height || w < 0 || h < 0) return false;
+    const size_t off = ((size_t)w + (size_t)h * width) * channals + shifting;
+    float weight = (1.0f / (float)renderCount);
+    fbuffer[off] = weight * dat + (1.0f - weight) * fbuffer[off];
+    ubuffer[off] = (unsigned char)(fbuffer[off] * 255);
+    return true;
+}
+
+namespace {
+int g_flip_on_write = 0;
+uint32_t png_crc(const unsigned char* p, size_t n) {
+    static uint32_t table[256];
+    static bool init = false;
+    if (!init) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+            table[i] = c;
+        }
+        init = true;
+    }
+    uint32_t c = 0xffffffffu;
+    for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xffu] ^ (c >> 8);
+    return c ^ 0xffffffffu;
+}
+void put_be32(std::vector<unsigned char>& o, uint32_t v) {
+    o.push_back((unsigned char)(v >> 24)); o.push_back((unsigned char)(v >> 16));
+    o.push_back((unsigned char)(v >> 8)); o.push_back((unsigned char)v);
+}
+void put_chunk(std::vector<unsigned char>& o, const char* type, const std::vector<unsigned char>& data) {
+    put_be32(o, (uint32_t)data.size());
+    const size_t start = o.size();
+    o.insert(o.end(), type, type + 4);
+    o.insert(o.end(), data.begin(), data.end());
+    put_be32(o, png_crc(&o[start], o.size() - start));
+}
+}  // namespace
+
+void stbi_flip_vertically_on_write(int flag) { g_flip_on_write = flag; }
+
+int stbi_write_png(char const* filename, int w, int h, int comp, const void* data, int stride_in_bytes) {
+    if (!filename || !data || w <= 0 || h <= 0 || comp < 1 || comp > 4) return 0;
+    static const unsigned char kColorType[5] = {0, 0, 4, 2, 6};   // grey, grey+alpha, RGB, RGBA
+    const size_t row = (size_t)w * comp;
+    const size_t stride = stride_in_bytes ? (size_t)stride_in_bytes : row;
+    const unsigned char* px = (const unsigned char*)data;
+    // scanlines, each behind filter byte 0 (None)
+    std::vector<unsigned char> raw;
+    raw.reserve((size_t)h * (row + 1));
+    for (int y = 0; y < h; ++y) {
+        const unsigned char* src = px + (size_t)(g_flip_on_write ? h - 1 - y : y) * stride;
+        raw.push_back(0);
+        raw.insert(raw.end(), src, src + row);
+    }
+    // zlib stream: header, stored deflate blocks of at most 65535 bytes, Adler-32
+    std::vector<unsigned char> z = {0x78, 0x01};
+    size_t pos = 0;
+    do {
+        const size_t n = std::min<size_t>(65535, raw.size() - pos);
+        z.push_back(pos + n == raw.size() ? 1 : 0);
+        z.push_back((unsigned char)(n & 0xff)); z.push_back((unsigned char)(n >> 8));
+        z.push_back((unsigned char)(~n & 0xff)); z.push_back((unsigned char)((~n >> 8) & 0xff));
+        z.insert(z.end(), raw.begin() + pos, raw.begin() + pos + n);
+        pos += n;
+    } while (pos < raw.size());
+    uint32_t a = 1, b = 0;
+    for (unsigned char c : raw) { a = (a + c) % 65521u; b = (b + a) % 65521u; }
+    put_be32(z, b << 16 | a);
+    std::vector<unsigned char> out = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    std::vector<unsigned char> ihdr;
+    put_be32(ihdr, (uint32_t)w);
+    put_be32(ihdr, (uint32_t)h);
+    ihdr.insert(ihdr.end(), {8, kColorType[comp], 0, 0, 0});   // depth, color type, deflate, filter 0, no interlace
+    put_chunk(out, "IHDR", ihdr);
+    put_chunk(out, "IDAT", z);
+    put_chunk(out, "IEND", {});
+    FILE* f = std::fopen(filename, "wb");
+    if (!f) return 0;
+    const size_t wr = std::fwrite(out.data(), 1, out.size(), f);
+    return (std::fclose(f) == 0 && wr == out.size()) ? 1 : 0;
 }
 
 namespace PBR {

@@ -260,11 +260,33 @@ int run_gpu() {
     return failures ? 1 : 0;
 }
 
+// main.cpp's output stage (main.cpp:419-429) on a patterned FrameBuffer: set_uc, a few
+// update_f_u_c averages, stbi_flip_vertically_on_write + stbi_write_png.  The raw ubuffer goes
+// to <png>.raw; tests/test_host_cpp.py decodes the PNG and compares.
+int run_png(const char* path) {
+    const int W = 37, H = 23;
+    FrameBuffer fb;
+    fb.InitBuffer(W, H, 4);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+            for (int c = 0; c < 4; ++c) fb.set_uc(x, y, c, (unsigned char)((x * 7 + y * 13 + c * 29) & 255));
+    for (int n = 1; n <= 3; ++n) fb.update_f_u_c(5, 6, 1, n, 0.25f * (float)n);   // f: .25, .375, .5 → u8 127
+    if (fb.update_f_u_c(W, 0, 0, 1, 1.f) || fb.set_uc(-1, 0, 0, 0)) { std::printf("FAIL out-of-bounds write accepted\n"); return 1; }
+    stbi_flip_vertically_on_write(1);
+    if (!stbi_write_png(path, W, H, 4, fb.getUCbuffer(), W * 4)) { std::printf("FAIL stbi_write_png\n"); return 1; }
+    FILE* f = std::fopen((std::string(path) + ".raw").c_str(), "wb");
+    if (!f) return 1;
+    std::fwrite(fb.getUCbuffer(), 1, (size_t)W * H * 4, f);
+    std::fclose(f);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     std::string mode = argc > 1 ? argv[1] : "cpu";
     try {
+        if (mode == "png") return run_png(argc > 2 ? argv[2] : "host_api_test.png");
         int rc = mode == "gpu" ? run_gpu() : run_cpu();
         std::printf("%s: %d failure(s)\n", mode.c_str(), failures);
         return rc;
