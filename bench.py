@@ -3,7 +3,7 @@
 dominant kernel and the CPU restatement timed beside it.
 
 One step = one full frame.  With --gpus N (launched by torch.distributed.run, one rank per GPU)
-the frame's 64×64 tiles are dealt round-robin over ranks and rank 0 gathers the per-tile RGBA8
+the frame's 32×32 tiles are dealt round-robin over ranks and rank 0 gathers the per-tile RGBA8
 FrameBuffer spans over RCCL — total work is fixed, so scaling is strong.  The gather of frame k
 runs on a communication stream while frame k+1 renders into the other of two output buffers.
 """
@@ -179,7 +179,7 @@ def main():
             "config": {"workload": f"{args.config}: {W}x{H}, {spp} spp, "
                                    f"{['Whitted', 'Path', 'VolPath'][rd.integrator]} d{rd.max_depth}",
                        "scene": scene.info.get("dragon", ""), "triangles": scene.info.get("triangles"),
-                       "parallelism": f"tiles64x64 round-robin over {world} GPU(s), RCCL gather of RGBA8 spans",
+                       "parallelism": f"tiles32x32 round-robin over {world} GPU(s), RCCL gather of RGBA8 spans",
                        "frame_ms": round(ms_per_step, 3), "scene_upload_s": round(upload_s, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -113,13 +113,18 @@ class HipRenderer:
         return out
 
 
-def tile_grid(width, height, tile=64):
+# Edge of the multi-GPU tiles.  Per-rank frame of an 8-GPU C2 job (slowest of 8 ranks, one GPU,
+# tools/shard_sweep.sh): 64 → 3.14 ms, 32 → 3.07, 16 → 3.02; 32 keeps the tile list short.
+TILE = 32
+
+
+def tile_grid(width, height, tile=TILE):
     """64×64 pixel tiles in row-major order."""
     return [(x, y, min(x + tile, width), min(y + tile, height))
             for y in range(0, height, tile) for x in range(0, width, tile)]
 
 
-def tiles_for_rank(width, height, rank, world, tile=64):
+def tiles_for_rank(width, height, rank, world, tile=TILE):
     """Round-robin tile ownership `tileId mod nGPU` so heavy regions spread over ranks."""
     return [t for i, t in enumerate(tile_grid(width, height, tile)) if i % world == rank]
 
@@ -135,7 +140,7 @@ def assemble(width, height, tiles, packed, channels):
     return frame
 
 
-def span_pixels(width, height, rank, world, tile=64):
+def span_pixels(width, height, rank, world, tile=TILE):
     """Pixels in rank's packed span (the sum of its tiles' areas)."""
     return sum((t[2] - t[0]) * (t[3] - t[1]) for t in tiles_for_rank(width, height, rank, world, tile))
 
@@ -149,7 +154,7 @@ class FrameGather:
     [height*width, channels] frame on its own device (index_copy_ with per-rank pixel indices
     computed once)."""
 
-    def __init__(self, width, height, world, device, tile=64, channels=3, dtype=None):
+    def __init__(self, width, height, world, device, tile=TILE, channels=3, dtype=None):
         import torch
         dtype = torch.float32 if dtype is None else dtype
         self.world = world
@@ -175,7 +180,7 @@ class FrameGather:
         return self.frame
 
 
-def gather_frame(span, width, height, rank, world, group=None, tile=64):
+def gather_frame(span, width, height, rank, world, group=None, tile=TILE):
     """One-shot FrameGather: the assembled [height, width, channels] numpy frame on rank 0, None elsewhere."""
     ch = span.shape[1]
     g = FrameGather(width, height, world, span.device, tile, channels=ch, dtype=span.dtype)

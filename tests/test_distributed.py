@@ -1,4 +1,4 @@
-"""Multi-GPU path on the CPU: world size 2 over gloo.  Each rank renders its round-robin 64×64
+"""Multi-GPU path on the CPU: world size 2 over gloo.  Each rank renders its round-robin 32×32
 tiles (here with the oracle, standing in for the device) and `gather_frame` — the same exchange
 bench.py runs over RCCL — must reassemble the single-process frame bit for bit."""
 import os

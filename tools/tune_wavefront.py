@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--lib", default=None, help="an experimental build of libpbr_hip.so")
     ap.add_argument("--shard", default=None, help="R/N: render only rank R's tiles of an N-GPU job "
                                                    "(per-rank frame time of the sharded bench)")
-    ap.add_argument("--tile", type=int, default=64, help="tile edge of the --shard partition")
+    ap.add_argument("--tile", type=int, default=32, help="tile edge of the --shard partition")
     ap.add_argument("--ref-file", default=None, help=".npy frame to compare against (written if absent), "
                                                      "so experimental builds can be checked against each other")
     ap.add_argument("variants", nargs="*", default=[""])
