@@ -1027,7 +1027,9 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
 // Wavefront Path: per bounce shade → shadow → probe → resolve → extend (pbr_wavefront_path.h).
 int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol) {
     const int spp = P.spp;
-    const WfChunks ch = wf_chunks(P);   // ≈ 290 B of queues + state per sample: 9.7 GB per 2^25 chunk
+    // ≈ 290 B of queues + state per sample: 19.5 GB per 2^26 chunk and lane.  Measured (bit-identical):
+    // C3 2^25 349.4 ms, 2^26 336.1, 2^27 340.4; C5 2^25 1979 ms, 2^26 1939, 2^27 1919
+    const WfChunks ch = wf_chunks(P, 26);
     const size_t cap = ch.cap, qcap = ch.qcap;
     int lobes = 0;
     for (const MatTemplate& m : ctx->host.materials)
