@@ -315,10 +315,16 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
             int r0 = __float_as_int(R.x), r1 = __float_as_int(R.y), r2 = __float_as_int(R.z), r3 = __float_as_int(R.w);
             auto swp = [](bool c, auto& a, auto& b) { auto x = c ? b : a; b = c ? a : b; a = x; };
             const bool sA = neg((meta >> 2) & 3), sB = neg((meta >> 4) & 3), sN = neg(meta & 3);
-            swp(sA, k0, k1); swp(sA, t0, t1); swp(sA, r0, r1);
-            swp(sB, k2, k3); swp(sB, t2, t3); swp(sB, r2, r3);
-            swp(sN, k0, k2); swp(sN, t0, t2); swp(sN, r0, r2);
-            swp(sN, k1, k3); swp(sN, t1, t3); swp(sN, r1, r3);
+            // Any-hit (IntersectP) keeps the slots in build order instead.  Its answer does not
+            // depend on the visit order: ray.tMax never shrinks, so every box test and the set of
+            // reachable leaves are order-free, and the result is whether any primitive there is
+            // hit.  Build order reaches occluders of C2's shadow rays sooner (C2 19.95 → 18.55 ms).
+            if constexpr (!ANY) {
+                swp(sA, k0, k1); swp(sA, t0, t1); swp(sA, r0, r1);
+                swp(sB, k2, k3); swp(sB, t2, t3); swp(sB, r2, r3);
+                swp(sN, k0, k2); swp(sN, t0, t2); swp(sN, r0, r2);
+                swp(sN, k1, k3); swp(sN, t1, t3); swp(sN, r1, r3);
+            }
             const float tM = r.tMax;
             const bool p0 = k0 && t0 < tM, p1 = k1 && t1 < tM, p2 = k2 && t2 < tM, p3 = k3 && t3 < tM;
             if (p0 | p1 | p2 | p3) {
