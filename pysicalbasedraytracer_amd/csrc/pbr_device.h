@@ -257,9 +257,11 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
     int* lref = nullptr;
     float* lt = nullptr;
     if constexpr (SHORT > 0) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
+    // any-hit: ray.tMax never shrinks, so a pushed slot (tEnter < tMax) always passes its re-test
+    // on the way out and only the reference is kept
     auto push = [&](int ref, float t, int sp) {
-        if (SHORT && sp < SHORT) { lref[sp * 256] = ref; lt[sp * 256] = t; }
-        else { stackRef[sp - SHORT] = ref; stackT[sp - SHORT] = t; }
+        if (SHORT && sp < SHORT) { lref[sp * 256] = ref; if (!ANY) lt[sp * 256] = t; }
+        else { stackRef[sp - SHORT] = ref; if (!ANY) stackT[sp - SHORT] = t; }
     };
     auto neg = [&](int axis) { return axis == 0 ? n0 : (axis == 1 ? n1 : n2); };
     int cur = S.quadRootRef, sp = 0;
@@ -342,6 +344,7 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
             --sp;
             int rr;
             float tt;
+            if (ANY) { cur = (SHORT && sp < SHORT) ? lref[sp * 256] : stackRef[sp - SHORT]; more = true; break; }
             if (SHORT && sp < SHORT) { rr = lref[sp * 256]; tt = lt[sp * 256]; }
             else { rr = stackRef[sp - SHORT]; tt = stackT[sp - SHORT]; }
             if (tt < r.tMax) { cur = rr; more = true; break; }
