@@ -1482,6 +1482,11 @@ static void InfinitePreprocess(const Scene& s, Light* l) {
     l->worldRadius = inside ? Length(c - wb.pMax) : 0;
 }
 
+// material index of a primitive: a PBR_MAT_NONE material means material == nullptr (-1)
+static int mat_index(const pbr_scene_desc* d, int m) {
+    return (m >= 0 && m < d->n_materials && d->materials[m].type == PBR_MAT_NONE) ? -1 : m;
+}
+
 static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
     if (!d || d->abi_version != PBR_HIP_ABI_VERSION) throw std::runtime_error("bad scene desc");
     std::unique_ptr<Scene> s(new Scene);
@@ -1508,7 +1513,7 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
             m.reverse = sd.reverse_orientation != 0;
             m.swaps = o2w.SwapsHandedness();
             for (int t = 0; t < sd.n_triangles; ++t)
-                prims.push_back(Prim{i, t, sd.material, sd.area_light_first >= 0 ? sd.area_light_first + t : -1,
+                prims.push_back(Prim{i, t, mat_index(d, sd.material), sd.area_light_first >= 0 ? sd.area_light_first + t : -1,
                                      sd.medium_inside, sd.medium_outside});
         } else {
             SphereS& sp = s->spheres[i];
@@ -1518,7 +1523,7 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
             sp.reverse = sd.reverse_orientation != 0;
             sp.swaps = o2w.SwapsHandedness();
             if (sd.area_light_first >= 0) throw std::runtime_error("sphere area lights are not supported");
-            prims.push_back(Prim{i, -1, sd.material, -1, sd.medium_inside, sd.medium_outside});
+            prims.push_back(Prim{i, -1, mat_index(d, sd.material), -1, sd.medium_inside, sd.medium_outside});
         }
     }
     for (int i = 0; i < d->n_materials; ++i) {

@@ -1059,6 +1059,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         WfpParams& X = V.X;
         WfParams& W = X.W;
         if (vol) {
+            V.anyHitTr = ctx->host.anyNoMaterial ? 0 : 1;
             HIP_TRY(B.wtO.ensure(qcap * 16)); HIP_TRY(B.wtD.ensure(qcap * 16)); HIP_TRY(B.wtP.ensure(qcap * 16));
             HIP_TRY(B.wtE.ensure(qcap * 16)); HIP_TRY(B.wtN.ensure(qcap * 16)); HIP_TRY(B.wtId.ensure(qcap * 4));
             HIP_TRY(B.rLiA.ensure(cap * 16)); HIP_TRY(B.rTr.ensure(cap * 16)); HIP_TRY(B.rWA.ensure(cap * 4));

@@ -519,7 +519,8 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
         tv[3] = bitsf((uint32_t)flags);   // the traversal reads the primitive flags from v0.w
         int32_t* pi = &S->primInfo[(size_t)slot * 4];
         pi[0] = flags;
-        pi[1] = sd.material;
+        // a PBR_MAT_NONE material is material == nullptr (a medium boundary): stored as -1 like no index
+        pi[1] = (sd.material >= 0 && sd.material < d->n_materials && d->materials[sd.material].type == PBR_MAT_NONE) ? -1 : sd.material;
         pi[2] = (p.tri >= 0 && sd.area_light_first >= 0) ? sd.area_light_first + p.tri : -1;
         if (sd.medium_inside >= d->n_media || sd.medium_outside >= d->n_media) fail("medium index out of range");
         pi[3] = (int32_t)(((uint32_t)(sd.medium_inside & 0xffff)) | ((uint32_t)(sd.medium_outside & 0xffff) << 16));

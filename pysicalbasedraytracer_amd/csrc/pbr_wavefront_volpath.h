@@ -19,6 +19,7 @@ struct WfvParams {
     float4* dLiA;          // light sample Li.rgb, lightPdf
     float4* dTr;           // transmittance to the light sample
     float* dWA;            // MIS weight of the light sample
+    int anyHitTr;          // every primitive has a material: the walk is one any-hit query
 };
 
 __device__ __forceinline__ int pack_vol(int dim, int bounces, bool specular, int medium) {
@@ -305,6 +306,17 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfv_tr(WfvParams V) {
         const f3 p1 = mk(tp.x, tp.y, tp.z), e1 = mk(te.x, te.y, te.z), n1 = mk(tn.x, tn.y, tn.z);
         Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, __float_as_int(d.w));
         rgb Tr = sp(1.f);
+        if (V.anyHitTr) {
+            // Every surface has a material, so the walk's first hit, if any, returns 0 and a miss
+            // multiplies the medium's Tr over the unchanged ray: whether anything is hit is all that
+            // matters, and IntersectP answers that (same boolean, same ray on a miss).
+            HitRec h;
+            Counters c;
+            if (traverse<true, false, SHORT>(S, ray, &h, &c)) Tr = sp(0.0f);
+            else if (ray.medium >= 0) Tr = Tr * medium_tr(S, ray.medium, ray);
+            V.dTr[V.tid[q]] = make_float4(Tr.r, Tr.g, Tr.b, 0.f);
+            continue;
+        }
         for (int guard = 0; guard < 256; ++guard) {
             HitRec h;
             Counters c;
