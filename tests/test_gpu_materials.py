@@ -116,3 +116,28 @@ def test_material_less_medium_interface(hip, integrator, monkeypatch):
     monkeypatch.setenv("PBR_WAVEFRONT", "0")
     mk, _, _ = hip.render(rd)
     assert np.array_equal(mk.view(np.uint32), g.view(np.uint32))
+
+
+def test_none_material_is_no_material(hip):
+    """A PBR_MAT_NONE material is `material == nullptr` (include/pbr_hip.h): primitives that use it
+    are pass-through medium boundaries, on the device and in the oracle, exactly like index -1
+    (VolPath's Tr walk crosses them instead of being blocked, VisibilityTester::Tr, Light.cpp:31-47)."""
+    def scene(none_index):
+        s = scenes.Scene()
+        P, I, UV = uv_patch()
+        s.mesh(P, I, s.matte((0.6, 0.6, 0.6)))
+        med = s.homogeneous_medium(0.3, 1.5, 0.3)
+        mat = -1
+        if none_index:
+            s.materials.append(capi.MaterialDesc(type=capi.MAT_NONE))
+            mat = len(s.materials) - 1
+        s.sphere((0.0, 0.1, 0.2), 0.5, mat, medium_inside=med, medium_outside=-1)
+        Pl, Il = scenes.quad(1.8, 0.8, flip=True)
+        s.area_light_mesh(Pl, Il, (4.0, 4.0, 4.0), s.matte((0.5, 0.5, 0.5)))
+        return s
+    cam = scenes.camera(48, 32, CAM["eye"], CAM["look"])
+    rd = scenes.render_desc(cam, capi.INTEGRATOR_VOLPATH, 8, 6)
+    g_none = check(hip, scene(True), rd)
+    hip.upload(scene(False))
+    g_idx, _, _ = hip.render(rd)
+    assert np.array_equal(g_none.view(np.uint32), g_idx.view(np.uint32))
