@@ -199,6 +199,9 @@ def main():
                          "bytes_per_sample": round(alg_bytes / samples_rank, 1),
                          "model": "per sample: 32*node_tests + 48*prim_tests + 96*rays + 64*shading_events "
                                   "(SURVEY 8(d)); counts from an instrumented pass over this frame",
+                         "note": "frac counts every BVH-node and triangle fetch as HBM bytes (the SURVEY 8(d) "
+                                 "model), but the 10 MB BVH + mesh are served by L2, the Infinity Cache and the "
+                                 "scalar cache, so frac can exceed 1; traffic_frac is the measured HBM fraction",
                          "build": build_info},
         }
         if world == 1 and not args.no_cpu_baseline:
