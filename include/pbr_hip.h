@@ -19,10 +19,20 @@
  *                           drives {Whitted,Path,VolPath}Integrator::Li per sample
  *   pbr_hip_destroy       — scene/integrator destructors
  *   pbr_hip_last_error    — (none; the reference fails silently)
+ *   pbr_hip_sync          — (none; the reference's Render returns when the frame is done): waits
+ *                           for asynchronous frames and reports a deferred failure
  *
  * Errors: every call returns 0 on success, a negative PBR_E_* code otherwise; the message is
  * kept per context and returned by pbr_hip_last_error.  Calls on one context are not thread-safe;
  * different contexts (one per device) are independent.
+ *
+ * Unbounded walks: the reference follows chains of material-less surfaces (medium boundaries)
+ * without limit (WhittedIntegrator.cpp:26-28, PathIntegrator.cpp:70-75, Light.cpp:31-47).  The
+ * device follows them too, up to safety bounds far beyond any sane scene — 1024 crossings in one
+ * Whitted Li or Path/VolPath path, 256 interfaces on one transmittance walk — and a frame in which
+ * a walk reaches a bound fails with PBR_E_UNSUPPORTED (synchronous renders: that call;
+ * asynchronous ones: the next pbr_hip_render or pbr_hip_sync on the context) instead of returning
+ * a truncated image.
  */
 #ifndef PBR_HIP_H
 #define PBR_HIP_H
@@ -189,11 +199,11 @@ typedef struct pbr_render_desc {
     int collect_stats;          /* 1: also count BVH node visits / triangle tests (slower) */
     /* PBR_SAMPLER_SOBOL (pbrt-v3 SobolSampler; the reference ships only its tables, F3):
      * generator matrices in the layout of the reference's SobolMatrices32 (Sampler/SobolMatrices.h:
-     * 42-47: [dims][52] uint32 columns).  NULL → built-in matrices: dimensions 0 and 1 are the
-     * canonical ones (identical to SobolMatrices32's), dimensions >= 2 are Sobol' matrices from
-     * primitive polynomials in degree order with unit initial direction numbers — pass the
-     * reference's own SobolMatrices32 for its sequence.  spp is rounded up to a power of two
-     * (GlobalSampler(RoundUpPow2(spp))). */
+     * 42-47: [dims][52] uint32 columns).  NULL → the built-in matrices, which are the
+     * reference's SobolMatrices32 (all 1024 dimensions, regenerated from the Joe-Kuo direction
+     * numbers the table was built from; hash-checked against it).  spp is rounded up to a power of
+     * two (GlobalSampler(RoundUpPow2(spp))).  Sample indices are 64-bit as pbrt-v3's: up to 2^52
+     * (2·log2(resolution) + log2(spp) <= 52). */
     const uint32_t* sobol_matrices;
     int sobol_dims;
 } pbr_render_desc;
@@ -218,6 +228,9 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* desc,
                    float* rgb_out, uint8_t* rgba_out, pbr_render_stats* stats);
 int pbr_hip_destroy(pbr_hip_ctx* ctx);
 const char* pbr_hip_last_error(const pbr_hip_ctx* ctx);
+/* Waits for the context's asynchronous frames; returns PBR_E_UNSUPPORTED if one of them stopped at
+ * a safety bound (see above). */
+int pbr_hip_sync(pbr_hip_ctx* ctx);
 
 /* ---- introspection used by the parity tests (no reference counterpart) ---- */
 /* Flattened BVH after upload: 32-B LinearBVHNode records (BVHAccel.cpp:46-55) and the ordered
@@ -233,7 +246,8 @@ int pbr_hip_intersect(pbr_hip_ctx* ctx, int n, const float* rays, float* out, in
 /* Device build info: ABI version, gfx arch string. */
 int pbr_hip_abi_version(void);
 const char* pbr_hip_build_info(void);
-/* The built-in Sobol' generator matrices (SobolMatrices32 layout, dims × 52 uint32); host only. */
+/* The built-in Sobol' generator matrices (SobolMatrices32 layout, dims × 52 uint32, dims <= 1024):
+ * the reference's SobolMatrices32; host only. */
 int pbr_hip_sobol_matrices(int dims, uint32_t* out);
 
 #ifdef __cplusplus

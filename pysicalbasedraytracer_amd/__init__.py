@@ -32,6 +32,10 @@ class HipRenderer:
         if rc != capi.PBR_OK:
             raise PbrError(f"{what} failed ({rc}): {self.lib.pbr_hip_last_error(self.ctx).decode()}")
 
+    def sync(self):
+        """Wait for asynchronous frames; raises if one stopped at a safety bound (pbr_hip_sync)."""
+        self._check(self.lib.pbr_hip_sync(self.ctx), "sync")
+
     def close(self):
         if self.ctx:
             self.lib.pbr_hip_destroy(self.ctx)

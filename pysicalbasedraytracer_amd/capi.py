@@ -171,6 +171,7 @@ EXPORTS = {
                                  C.POINTER(RenderStats)]),
     "pbr_hip_destroy": (C.c_int, [C.c_void_p]),
     "pbr_hip_last_error": (C.c_char_p, [C.c_void_p]),
+    "pbr_hip_sync": (C.c_int, [C.c_void_p]),
     "pbr_hip_get_bvh": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int32),
                                   C.POINTER(C.c_int)]),
     "pbr_hip_sampler_values": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -187,6 +188,9 @@ PACKAGE_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PACKAGE_DIR, "libpbr_hip.so")
 
 _lib = None
+
+
+OPTIONAL_FOR_AB = ("pbr_hip_sync",)
 
 
 def load_library(path: str | None = None) -> C.CDLL:
@@ -206,6 +210,8 @@ def load_library(path: str | None = None) -> C.CDLL:
         pass
     lib = C.CDLL(p)
     for name, (res, args) in EXPORTS.items():
+        if path is not None and name in OPTIONAL_FOR_AB and not hasattr(lib, name):
+            continue   # an older experimental build (A/B timing runs) may predate this entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

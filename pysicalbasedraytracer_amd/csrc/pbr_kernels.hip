@@ -27,8 +27,13 @@ using namespace pbr;
 namespace {
 
 // ---------------------------------------------------------------- sampler (Sampler/Sampler.cpp)
-// index: the GlobalSampler's intervalSampleIndex; px, py: the current pixel (Sobol dims 0/1 remap)
-struct SState { uint32_t index; int dim; int px, py; };
+// index: the low 32 bits of the GlobalSampler's intervalSampleIndex (pbrt-v3 int64_t; Halton's stays
+// below 2^32); px, py: the current pixel (Sobol dims 0/1 remap); sid: any number ≡ the sample
+// number mod spp (the sample number, or the wavefront's per-chunk sample id, pixel-major), from
+// which a Sobol index's bits >= 32 follow — (frame << 2m) | j has frame << 2m >> 32 above bit 31 —
+// so they need no register or queue storage of their own
+struct SState { uint32_t index; int dim; int px, py; int sid; };
+struct SIndex { uint32_t lo, hi; };
 
 __host__ __device__ __forceinline__ HaltonParams hparams(const DeviceSampler& s) {
     HaltonParams h;
@@ -44,6 +49,7 @@ __host__ __device__ __forceinline__ HaltonParams hparams(const DeviceSampler& s)
 constexpr int kLdsDims = 64;
 constexpr int kLdsPermEntries = 8893;              // Σ of the first 64 primes
 constexpr int kSobolNib = 128;                     // words per dimension: 8 nibble positions × 16
+constexpr int kSobolNibHi = 80;                    // index bits 32..51: 5 nibble positions × 16
 constexpr int kLdsSobolDims = 34;                  // 34 × 512 B fit the Halton permutation array
 static_assert(kLdsSobolDims * kSobolNib * 4 <= kLdsPermEntries * 2, "Sobol LDS tables share the Halton array");
 __shared__ __align__(16) uint16_t s_halton_perm[kLdsPermEntries];
@@ -78,12 +84,22 @@ __device__ __forceinline__ uint32_t sobol_nibbles(const uint32_t* T, uint32_t in
            T[64 + ((index >> 16) & 15u)] ^ T[80 + ((index >> 20) & 15u)] ^ T[96 + ((index >> 24) & 15u)] ^
            T[112 + (index >> 28)];
 }
+// index bits 32..51 (columns 32..51 of the 52-column matrices): five more nibble tables, read from
+// global memory only when a sample's index needs them
+__device__ __noinline__ uint32_t sobol_nibbles_hi(const uint32_t* T, uint32_t hi) {
+    return T[hi & 15u] ^ T[16 + ((hi >> 4) & 15u)] ^ T[32 + ((hi >> 8) & 15u)] ^ T[48 + ((hi >> 12) & 15u)] ^
+           T[64 + ((hi >> 16) & 15u)];
+}
 template <bool LDS = false>
-__device__ __forceinline__ float sobol_dimension(const DeviceSampler& s, uint32_t index, int dim, int px, int py) {
+__device__ __forceinline__ float sobol_dimension(const DeviceSampler& s, uint32_t index, int sid, int dim, int px, int py) {
     if (dim >= s.nSobolDims) return 0.f;
     uint32_t v;
     if (LDS && dim < sobol_lds_dims(s)) v = sobol_nibbles(reinterpret_cast<const uint32_t*>(s_halton_perm) + dim * kSobolNib, index);
     else v = sobol_nibbles(s.sobol + (size_t)dim * kSobolNib, index);
+    if (s.wideIndex) {   // index bits 32..51: the frame's bits above 31 - 2m (spp is a power of two)
+        const uint32_t hi = ((uint32_t)sid & (uint32_t)(s.spp - 1)) >> s.hiShift;
+        if (hi) v ^= sobol_nibbles_hi(s.sobolHi + (size_t)dim * kSobolNibHi, hi);
+    }
     float f = mn((float)v * 2.3283064365386963e-10f, kOneMinusEpsilon);
     if (dim <= 1) {
         f = f * (float)s.sobolRes;   // + sampleBounds.pMin[dim] == 0
@@ -91,10 +107,11 @@ __device__ __forceinline__ float sobol_dimension(const DeviceSampler& s, uint32_
     }
     return f;
 }
-// SobolIntervalToIndex (LowDiscrepancy.h) via the GF(2) tables of sobol_pixel_tables
-__device__ __forceinline__ uint32_t sobol_index(const DeviceSampler& s, int px, int py, uint32_t frame) {
+// SobolIntervalToIndex (LowDiscrepancy.h) via the GF(2) tables of sobol_pixel_tables; the index is
+// (frame << 2m) | j, 64-bit as pbrt-v3's (bits >= 32 come from the frame alone)
+__device__ __forceinline__ SIndex sobol_index(const DeviceSampler& s, int px, int py, uint32_t frame) {
     const int m = s.sobolLog2Res;
-    if (m == 0) return 0;   // pbrt-v3 returns 0 here (a 1×1 raster repeats sample 0)
+    if (m == 0) return SIndex{0u, 0u};   // pbrt-v3 returns 0 here (a 1×1 raster repeats sample 0)
     const uint32_t* T = s.sobolPix;
     uint32_t delta = 0;
     for (int k = 0; (frame >> k) != 0u; ++k)
@@ -102,17 +119,18 @@ __device__ __forceinline__ uint32_t sobol_index(const DeviceSampler& s, int px, 
     uint32_t b = (((uint32_t)px << m) | (uint32_t)py) ^ delta, j = 0;
     for (int r = 0; b != 0; b >>= 1, ++r)
         if (b & 1u) j ^= T[r];
-    return (frame << (2 * m)) | j;
+    const uint64_t idx = ((uint64_t)frame << (2 * m)) | j;
+    return SIndex{(uint32_t)idx, (uint32_t)(idx >> 32)};
 }
 // GlobalSampler::StartPixel / SetSampleNumber: the global index of sample s of pixel (x, y)
-__device__ __forceinline__ uint32_t sample_index(const DeviceSampler& smp, int x, int y, int s) {
+__device__ __forceinline__ SIndex sample_index(const DeviceSampler& smp, int x, int y, int s) {
     if (smp.type == PBR_SAMPLER_SOBOL) return sobol_index(smp, x, y, (uint32_t)s);
-    return halton_pixel_offset(hparams(smp), x, y) + (uint32_t)s * (uint32_t)smp.stride;   // Halton.cpp:61-81
+    return SIndex{halton_pixel_offset(hparams(smp), x, y) + (uint32_t)s * (uint32_t)smp.stride, 0u};   // Halton.cpp:61-81
 }
 
 template <bool LDS = false>
-__device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int dim, int px = 0, int py = 0) {
-    if (s.type == PBR_SAMPLER_SOBOL) return sobol_dimension<LDS>(s, index, dim, px, py);
+__device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int sid, int dim, int px = 0, int py = 0) {
+    if (s.type == PBR_SAMPLER_SOBOL) return sobol_dimension<LDS>(s, index, sid, dim, px, py);
     // HaltonSampler::SampleDimension (Halton.cpp:83-92)
     if (dim == 0) return radical_inverse_2(index >> s.baseExp0);
     if (dim == 1) return radical_inverse_b(3u, 0x55555555u, div_prime(index, (uint32_t)s.baseScale1, 0xffffffffu / (uint32_t)s.baseScale1));
@@ -129,13 +147,13 @@ __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32
 // arrayStartDim == arrayEndDim == 5, so only a Get2D that would straddle dimension 5 is moved.
 template <bool LDS = false>
 __device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) {
-    return sample_dimension<LDS>(s, st.index, st.dim++, st.px, st.py);
+    return sample_dimension<LDS>(s, st.index, st.sid, st.dim++, st.px, st.py);
 }
 template <bool LDS = false>
 __device__ __forceinline__ void get2d(const DeviceSampler& s, SState& st, float* a, float* b) {
     if (st.dim == 4) st.dim = 5;
-    *a = sample_dimension<LDS>(s, st.index, st.dim, st.px, st.py);
-    *b = sample_dimension<LDS>(s, st.index, st.dim + 1, st.px, st.py);
+    *a = sample_dimension<LDS>(s, st.index, st.sid, st.dim, st.px, st.py);
+    *b = sample_dimension<LDS>(s, st.index, st.sid, st.dim + 1, st.px, st.py);
     st.dim += 2;
 }
 
@@ -199,12 +217,13 @@ template <bool STATS>
 __device__ rgb vis_tr(const DeviceScene& S, const Isect& p0, const VisPt& p1, Counters* c) {   // Light.cpp:31-47
     Ray ray = spawn_ray_to(p0, p1.p, p1.pError, p1.n);
     rgb Tr = sp(1.f);
-    for (int guard = 0; guard < 256; ++guard) {
+    for (int guard = 0;; ++guard) {
         Isect isect;
         bool hit = intersect<STATS>(S, ray, &isect, c);
         if (hit && S.primInfo[isect.slot].y >= 0) return sp(0.0f);
         if (ray.medium >= 0) Tr = Tr * medium_tr(S, ray.medium, ray);
         if (!hit) break;
+        if (guard == kMaxTrCrossings) { atomicOr(S.guard, kGuardTransmittance); break; }
         ray = spawn_ray_to(isect, p1.p, p1.pError, p1.n);
     }
     return Tr;
@@ -330,7 +349,7 @@ __device__ rgb whitted_li(const KParams& P, Ray ray, SState& st, Counters* c) {
         f3 n = isect.sn, wo = isect.wo;
         BSDF bsdf;
         if (!make_bsdf(S, S.materials, isect, false, &bsdf)) {
-            if (guard > 1024) { Llast = sp(0.f); break; }
+            if (guard > kMaxPassThrough) { atomicOr(S.guard, kGuardWhittedPassThrough); Llast = sp(0.f); break; }
             ray = spawn_ray(isect, ray.d);     // Li(isect.SpawnRay(ray.d), depth)
             continue;
         }
@@ -551,7 +570,8 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
             pixel_xy(P, pixBase + lp, &x, &y);
             // GlobalSampler::StartPixel/SetSampleNumber (Sampler.cpp:97-130)
             SState st;
-            st.index = sample_index(P.smp, x, y, s);
+            st.index = sample_index(P.smp, x, y, s).lo;
+            st.sid = s;
             st.dim = 0;
             st.px = x;
             st.py = y;
@@ -590,8 +610,8 @@ __global__ __launch_bounds__(256, OCC) void k_render(KParams P) {
 __global__ void k_sampler_values(DeviceSampler smp, HaltonParams hp, int n, const int32_t* q, float* out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint32_t idx = sample_index(smp, q[4 * i], q[4 * i + 1], q[4 * i + 2]);
-    out[i] = sample_dimension(smp, idx, q[4 * i + 3], q[4 * i], q[4 * i + 1]);
+    const SIndex idx = sample_index(smp, q[4 * i], q[4 * i + 1], q[4 * i + 2]);
+    out[i] = sample_dimension(smp, idx.lo, q[4 * i + 2], q[4 * i + 3], q[4 * i], q[4 * i + 1]);
 }
 __global__ void k_camera_rays(DeviceCamera cam, int n, const float* pf, float* out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -666,9 +686,9 @@ struct pbr_hip_ctx {
     DevBuf dInfTex, dInfCF, dInfCC, dInfMF, dInfMC, dInfRec;
     DevBuf dNodes, dWide, dQuad, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
-    DevBuf dSobol, dSobolPix;          // active Sobol matrices, pixel tables
+    DevBuf dSobol, dSobolHi, dSobolPix;  // active Sobol nibble tables (index bits 0-31, 32-51), pixel tables
     std::vector<uint32_t> sobolBuiltin;
-    const uint32_t* sobolSrc = nullptr;  // what dSobol holds (user pointer or the built-in table)
+    uint64_t sobolKey = 0;               // FNV-1a of the matrices dSobol was built from
     int sobolSrcDims = 0, sobolPixM = -1;
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
     std::vector<int32_t> tilesHost;      // what dTiles / dTileStart hold (re-uploaded on change only)
@@ -684,6 +704,8 @@ struct pbr_hip_ctx {
     hipEvent_t evShade[kWfLanes][kWfMaxDepth + 2] = {}, evShadow[kWfLanes][kWfMaxDepth + 2] = {};
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
+    DevBuf dGuard;                       // DeviceScene::guard (kGuard* bits of tripped safety bounds)
+    int* guardHost = nullptr;            // pinned copy, refreshed at the end of frames that can trip one
 };
 
 namespace {
@@ -705,6 +727,20 @@ int drain(pbr_hip_ctx* ctx) {
     return PBR_OK;
 }
 
+// A frame whose walk reached a safety bound fails instead of returning a truncated image.  Frames
+// that can trip one (scenes with material-less primitives) copy the flag to pinned memory at their
+// end; synchronous renders check it before returning, asynchronous ones at the next call.
+int check_guard(pbr_hip_ctx* ctx) {
+    const int g = ctx->guardHost ? *(volatile int*)ctx->guardHost : 0;
+    if (!g) return PBR_OK;
+    *ctx->guardHost = 0;
+    HIP_TRY(hipMemset(ctx->dGuard.p, 0, sizeof(int)));
+    std::string what;
+    if (g & kGuardWhittedPassThrough) what += "a Whitted path crossed more than 1024 material-less surfaces; ";
+    if (g & kGuardTransmittance) what += "a transmittance walk crossed more than 256 medium interfaces; ";
+    return set_err(ctx, PBR_E_UNSUPPORTED, what + "the frame is incomplete");
+}
+
 DeviceScene device_scene(pbr_hip_ctx* ctx) {
     const HostScene& h = ctx->host;
     DeviceScene S;
@@ -715,6 +751,7 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     S.quad = (const float4*)ctx->dQuad.p;
     S.quadRootRef = h.quadRootRef;
     S.triVerts = (const float4*)ctx->dTri.p;
+    S.guard = (int*)ctx->dGuard.p;
     S.primInfo = (const int4*)ctx->dInfo.p;
     S.triUV = h.triUV.empty() ? nullptr : (const float2*)ctx->dUV.p;
     S.spheres = (const SphereRec*)ctx->dSph.p;
@@ -761,21 +798,27 @@ int prepare_sobol(pbr_hip_ctx* ctx, const uint32_t* user, int userDims, int w, i
         dims = 1024;
     }
     if (dims < 2) return set_err(ctx, PBR_E_INVALID, "Sobol needs at least 2 dimensions of matrices");
-    if (src != ctx->sobolSrc || dims != ctx->sobolSrcDims) {
+    // the cached device tables are keyed on the matrices' contents, not on the caller's pointer (a
+    // reused or reallocated buffer can hold new matrices at the same address)
+    uint64_t key = 1469598103934665603ull;
+    for (size_t i = 0; i < (size_t)dims * kSobolMatrixSize; ++i) key = (key ^ src[i]) * 1099511628211ull;
+    if (key != ctx->sobolKey || dims != ctx->sobolSrcDims) {
         if (int rc = drain(ctx)) return rc;
-        // nibble tables of the first 32 columns (the device index is 32-bit, sobol_nibbles)
-        std::vector<uint32_t> nib((size_t)dims * kSobolNib, 0u);
+        // nibble tables: index bits 0..31 (sobol_nibbles) and 32..51 (sobol_nibbles_hi)
+        std::vector<uint32_t> nib((size_t)dims * kSobolNib, 0u), nibHi((size_t)dims * kSobolNibHi, 0u);
         for (int d = 0; d < dims; ++d)
-            for (int k = 0; k < 8; ++k)
+            for (int k = 0; k < 13; ++k)
                 for (int n = 0; n < 16; ++n) {
                     uint32_t v = 0;
                     for (int b = 0; b < 4; ++b)
                         if ((n >> b) & 1) v ^= src[(size_t)d * kSobolMatrixSize + 4 * k + b];
-                    nib[(size_t)d * kSobolNib + 16 * k + n] = v;
+                    if (k < 8) nib[(size_t)d * kSobolNib + 16 * k + n] = v;
+                    else nibHi[(size_t)d * kSobolNibHi + 16 * (k - 8) + n] = v;
                 }
         HIP_TRY(ctx->dSobol.upload(nib, ctx->stream));
+        HIP_TRY(ctx->dSobolHi.upload(nibHi, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
-        ctx->sobolSrc = src;
+        ctx->sobolKey = key;
         ctx->sobolSrcDims = dims;
         ctx->sobolPixM = -1;
     }
@@ -795,6 +838,7 @@ int prepare_sobol(pbr_hip_ctx* ctx, const uint32_t* user, int userDims, int w, i
         ctx->sobolPixM = m;
     }
     s->sobol = (const uint32_t*)ctx->dSobol.p;
+    s->sobolHi = (const uint32_t*)ctx->dSobolHi.p;
     s->nSobolDims = dims;
     s->sobolLog2Res = m;
     s->sobolRes = res;
@@ -1099,9 +1143,13 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     const dim3 gProbe = resident_grid(ctx, (const void*)k_wfp_probe<kShortStack>);
     const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack>);
     const dim3 gResolve = resident_grid(ctx, (const void*)k_wfp_resolve);
-    // material-less primitives (medium interfaces) continue a path without a bounce
-    // (PathIntegrator.cpp:70-75): up to 32 such crossings per path are followed
+    // Material-less primitives (medium interfaces) continue a path without a bounce
+    // (PathIntegrator.cpp:70-75), one level per crossing.  With such primitives the schedule runs
+    // 32 extra levels and then keeps going while continuation rays are queued (a host read of the
+    // queue's segment counts per extra level), so no path is cut short; a chain of more than
+    // kMaxPassThrough crossings fails the render.
     const int maxLevels = std::max(1, P.maxDepth) + 1 + (ctx->host.anyNoMaterial ? 32 : 0);
+    std::vector<int> segHost(kWfBlocks);
     if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
     int chunk = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
@@ -1116,7 +1164,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         int cur = 0;
         W.cur = queue(l, 0);
         hipLaunchKernelGGL(k_wfp_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, X);
-        for (int level = 0; level < maxLevels; ++level) {
+        for (int level = 0;; ++level) {   // ends below: at maxLevels, or when no continuation is queued
             W.cur = queue(l, cur);
             W.next = queue(l, cur ^ 1);
             const int l0 = level == 0 ? 1 : 0;
@@ -1137,7 +1185,16 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
                 hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, st, X);
                 hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, st, X);
             }
-            if (level + 1 == maxLevels) break;
+            if (level + 1 >= maxLevels) {
+                if (!ctx->host.anyNoMaterial) break;
+                HIP_TRY(hipMemcpyAsync(segHost.data(), W.next.segCount, kWfBlocks * sizeof(int), hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                long long pending = 0;
+                for (int c : segHost) pending += c;
+                if (pending == 0) break;
+                if (level + 1 >= maxLevels + kMaxPassThrough)
+                    return set_err(ctx, PBR_E_UNSUPPORTED, "a path crossed more than 1024 material-less surfaces");
+            }
             cur ^= 1;
             W.cur = queue(l, cur);
             hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W);
@@ -1160,7 +1217,7 @@ int pbr_hip_abi_version(void) { return PBR_HIP_ABI_VERSION; }
 const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 wavefront+megakernel src " PBR_SRC_HASH; }
 
 int pbr_hip_sobol_matrices(int dims, uint32_t* out) {
-    if (dims < 1 || dims > 4096 || !out) return PBR_E_INVALID;
+    if (dims < 1 || dims > kSobolMaxDims || !out) return PBR_E_INVALID;
     std::vector<uint32_t> m;
     build_sobol_matrices(dims, &m);
     std::memcpy(out, m.data(), m.size() * 4);
@@ -1182,6 +1239,10 @@ int pbr_hip_create(int device, pbr_hip_ctx** out) {
     pbr_hip_ctx* c = ctx.get();
     {
         pbr_hip_ctx* ctx = c;   // for HIP_TRY
+        HIP_TRY(hipHostMalloc((void**)&ctx->guardHost, sizeof(int), hipHostMallocDefault));
+        *ctx->guardHost = 0;
+        HIP_TRY(ctx->dGuard.ensure(sizeof(int)));
+        HIP_TRY(hipMemsetAsync(ctx->dGuard.p, 0, sizeof(int), ctx->stream));
         HIP_TRY(ctx->dPrimes.upload(ctx->halton.primes, ctx->stream));
         HIP_TRY(ctx->dRecips.upload(ctx->halton.recips, ctx->stream));
         HIP_TRY(ctx->dPrimeSums.upload(ctx->halton.primeSums, ctx->stream));
@@ -1211,6 +1272,7 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->guardHost) (void)hipHostFree(ctx->guardHost);
     hipStream_t s = ctx->stream;
     delete ctx;
     if (s) (void)hipStreamDestroy(s);
@@ -1218,6 +1280,13 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
 }
 
 const char* pbr_hip_last_error(const pbr_hip_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pbr_hip_sync(pbr_hip_ctx* ctx) {
+    if (!ctx) return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    return check_guard(ctx);
+}
 
 int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     if (!ctx) return PBR_E_INVALID;
@@ -1230,6 +1299,8 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
         return set_err(ctx, PBR_E_INVALID, e.what());
     }
     const HostScene& h = ctx->host;
+    HIP_TRY(hipMemsetAsync(ctx->dGuard.p, 0, sizeof(int), ctx->stream));
+    *ctx->guardHost = 0;
     HIP_TRY(ctx->dNodes.upload(h.nodes, ctx->stream));
     HIP_TRY(ctx->dWide.upload(h.wide, ctx->stream));
     HIP_TRY(ctx->dQuad.upload(h.quad, ctx->stream));
@@ -1274,6 +1345,7 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (!ctx) return PBR_E_INVALID;
     if (!d) return set_err(ctx, PBR_E_INVALID, "null render desc");
     if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    if (int rc = check_guard(ctx)) return rc;   // an earlier asynchronous frame stopped at a bound
     if (d->spp <= 0) return set_err(ctx, PBR_E_INVALID, "spp must be positive");
     if (d->max_depth < 0) return set_err(ctx, PBR_E_INVALID, "max_depth must be >= 0");
     if (d->integrator == PBR_INTEGRATOR_WHITTED && d->max_depth > kMaxWhittedDepth)
@@ -1289,7 +1361,8 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         spp = p2;
         int res = 1, m = 0;
         while (res < std::max(d->camera.width, d->camera.height)) { res <<= 1; ++m; }
-        if (((uint64_t)spp << (2 * m)) > (1ull << 32)) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol sample index beyond 32 bits");
+        // pbrt-v3's SobolSampleFloat reads one 52-column matrix per dimension: indices below 2^52
+        if (2 * m + 31 - __builtin_clz((unsigned)spp) > kSobolMatrixSize) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol sample index beyond 52 bits");
     } else if ((long long)spp * (long long)31104 >= (1ll << 32)) {
         return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
     }
@@ -1313,6 +1386,9 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (d->sampler == PBR_SAMPLER_SOBOL) {
         int rc = prepare_sobol(ctx, d->sobol_matrices, d->sobol_dims, d->camera.width, d->camera.height, &P.smp);
         if (rc) return rc;
+        // sample indices (frame << 2m) | j with frame < spp: bits >= 32 exist iff 2m + log2(spp) > 32
+        P.smp.wideIndex = 2 * P.smp.sobolLog2Res + 31 - __builtin_clz((unsigned)spp) > 32;
+        P.smp.hiShift = 32 - 2 * P.smp.sobolLog2Res;
     }
     P.integrator = d->integrator;
     P.maxDepth = d->max_depth;
@@ -1411,8 +1487,10 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     }
     unsigned long long hs[4] = {0, 0, 0, 0};
     if (d->collect_stats) HIP_TRY(hipMemcpyAsync(hs, ctx->dStats.p, sizeof(hs), hipMemcpyDeviceToHost, s));
+    if (ctx->host.anyNoMaterial) HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, s));
     if (!d->outputs_on_device || d->collect_stats || stats) {
         HIP_TRY(hipStreamSynchronize(s));
+        if (int rc = check_guard(ctx)) return rc;
     } else {
         ctx->inFlight = true;
         ctx->lastStream = s;
@@ -1457,6 +1535,10 @@ int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height,
     if (sampler == PBR_SAMPLER_SOBOL) {
         int rc = prepare_sobol(ctx, nullptr, 0, width, height, &s);
         if (rc) return rc;
+        // queries name their sample numbers directly (any int32): keep all of their bits
+        s.wideIndex = s.sobolLog2Res > 0;
+        s.hiShift = 32 - 2 * s.sobolLog2Res;
+        s.spp = 0;   // the mask (spp - 1) of sobol_dimension becomes all ones
     }
     HaltonParams hp = hparams(s);
     HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 16));

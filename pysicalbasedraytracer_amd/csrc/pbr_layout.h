@@ -93,7 +93,14 @@ struct DeviceScene {
     const float* media;            // per medium: sigma_a[3] sigma_s[3] sigma_t[3] g → 10 floats
     int nMedia;
     const InfDev* inf;             // the InfiniteAreaLight's tables (device memory), or null
+    int* guard;                    // set (kGuard*) when a walk stops at a safety bound; the render then fails
 };
+// Safety bounds of walks the reference runs without limit; reaching one fails the render
+// (PBR_E_UNSUPPORTED) instead of returning a silently truncated result.
+constexpr int kGuardWhittedPassThrough = 1;   // > kMaxPassThrough material-less crossings in one Whitted Li
+constexpr int kGuardTransmittance = 2;        // > kMaxTrCrossings interfaces on one VisibilityTester::Tr walk
+constexpr int kMaxPassThrough = 1024;
+constexpr int kMaxTrCrossings = 256;
 
 struct DeviceSampler {
     int type;                      // pbr_sampler_type
@@ -103,11 +110,14 @@ struct DeviceSampler {
     const uint32_t* recips;        // floor(2^32/p)
     const uint32_t* primeSums;     // [1000]
     const uint16_t* perms;         // digit permutations
-    const uint32_t* sobol;         // Sobol generator matrices (dims × 32), or null
+    const uint32_t* sobol;         // Sobol nibble tables of matrix columns 0..31 (dims × 128), or null
     int nSobolDims;
     int sobolLog2Res;              // log2 of the power-of-two resolution
     int sobolRes;
-    const uint32_t* sobolPix;      // sobol_pixel_tables: T_low^-1 columns [2m], T_high columns
+    const uint32_t* sobolPix;      // sobol_pixel_tables: T_low^-1 columns [2m], T_high columns [52 - 2m]
+    const uint32_t* sobolHi;       // nibble tables of matrix columns 32..51 (index bits >= 32)
+    int wideIndex;                 // some sample index of this render needs bits >= 32
+    int hiShift;                   // 32 - 2m: sample number >> hiShift = the index's bits >= 32
     int ldsDims;                   // Halton dimensions a kernel may stage in LDS (<= 64)
 };
 

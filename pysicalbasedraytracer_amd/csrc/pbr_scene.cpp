@@ -8,6 +8,7 @@
 // the same std::partition / std::nth_element calls on the same element order, so the layout is
 // identical.
 #include "pbr_scene.h"
+#include "pbr_sobol_jk.h"
 #include "pbr_xform.h"
 
 #include <algorithm>
@@ -729,69 +730,38 @@ void halton_params(int resX, int resY, DeviceSampler* s) {   // HaltonSampler ct
 }
 
 // ---------------------------------------------------------------- Sobol (pbrt-v3 SobolSampler)
-// Built-in generator matrices: column c of dimension d is the direction number v_{c+1} of a
-// Sobol' sequence.  Dimension 0 is van der Corput, dimension 1 the polynomial x + 1 (both equal to
-// the reference's SobolMatrices32 rows); dimensions >= 2 use the primitive polynomials of degree
-// 2, 3, ... in increasing coefficient order with all initial direction numbers m_k = 1.
-namespace {
-bool gf2_primitive(uint32_t poly, int deg) {   // poly includes the x^deg and 1 terms
-    const uint64_t order = (1ull << deg) - 1;
-    auto mulmod = [&](uint32_t a, uint32_t b) {
-        uint32_t r = 0;
-        for (int i = 0; i < deg; ++i) {
-            if (b & (1u << i)) r ^= a;
-            a <<= 1;
-            if (a & (1u << deg)) a ^= poly;
-        }
-        return r;
-    };
-    auto powx = [&](uint64_t e) {
-        uint32_t r = 1, b = 2 % (1u << deg);
-        if (deg == 1) b = 2 ^ poly;
-        while (e) { if (e & 1) r = mulmod(r, b); b = mulmod(b, b); e >>= 1; }
-        return r;
-    };
-    if (powx(order) != 1) return false;
-    uint64_t n = order;
-    for (uint64_t q = 2; q * q <= n; ++q) {
-        if (n % q) continue;
-        if (powx(order / q) == 1) return false;
-        while (n % q == 0) n /= q;
-    }
-    if (n > 1 && powx(order / n) == 1) return false;
-    return true;
-}
-}  // namespace
-
+// pbrt-v3's SobolMatrices32 (the reference's Sampler/SobolMatrices.cpp:69), regenerated from the
+// Joe-Kuo direction numbers it was built from (pbr_sobol_jk.h): dimension 0 is van der Corput,
+// dimension d >= 1 runs the Bratley-Fox recurrence over its primitive polynomial (degree s, inner
+// coefficients a) from m_1..m_s; column c holds v_{c+1} = m_{c+1} / 2^{c+1} as 32 bits (index bits
+// >= 32 keep v's top 32 bits).  tests/test_oracle_golden.py hash-matches all 1024 × 52 words.
 void build_sobol_matrices(int nDims, std::vector<uint32_t>* out) {
+    if (nDims > kSobolJKDims) fail("Sobol: at most 1024 dimensions");
     out->assign((size_t)nDims * kSobolMatrixSize, 0u);
     uint32_t* M = out->data();
     for (int c = 0; c < 32 && nDims > 0; ++c) M[c] = 0x80000000u >> c;
-    int d = 1;
-    for (int deg = 1; d < nDims && deg < 31; ++deg) {
-        for (uint32_t a = 0; a < (1u << (deg - 1)) && d < nDims; ++a) {
-            uint32_t poly = (1u << deg) | (a << 1) | 1u;
-            if (!gf2_primitive(poly, deg)) continue;
-            uint64_t m[kSobolMatrixSize + 1];
-            for (int k = 1; k <= kSobolMatrixSize; ++k) {
-                if (k <= deg) { m[k] = 1; continue; }
-                uint64_t v = m[k - deg] ^ (m[k - deg] << deg);
-                for (int i = 1; i < deg; ++i)
-                    if ((a >> (deg - 1 - i)) & 1u) v ^= m[k - i] << i;
-                m[k] = v;
-            }
-            // 32-bit columns of v_k = m_k / 2^k (index bits >= 32 keep v_k's top 32 bits)
-            for (int c = 0; c < kSobolMatrixSize; ++c)
-                M[(size_t)d * kSobolMatrixSize + c] = (uint32_t)(c < 32 ? m[c + 1] << (31 - c) : m[c + 1] >> (c - 31));
-            ++d;
+    const uint16_t* jk = kSobolJK;
+    for (int d = 1; d < nDims; ++d) {
+        const int deg = jk[0] & 15;
+        const uint32_t a = jk[0] >> 4;
+        uint64_t m[kSobolMatrixSize + 1];
+        for (int k = 1; k <= kSobolMatrixSize; ++k) {
+            if (k <= deg) { m[k] = jk[k]; continue; }
+            uint64_t v = m[k - deg] ^ (m[k - deg] << deg);
+            for (int i = 1; i < deg; ++i)
+                if ((a >> (deg - 1 - i)) & 1u) v ^= m[k - i] << i;
+            m[k] = v;
         }
+        for (int c = 0; c < kSobolMatrixSize; ++c)
+            M[(size_t)d * kSobolMatrixSize + c] = (uint32_t)(c < 32 ? m[c + 1] << (31 - c) : m[c + 1] >> (c - 31));
+        jk += 1 + deg;
     }
 }
 
 // SobolIntervalToIndex at resolution 2^m, restated as a GF(2) solve: the top m bits of
-// dimensions 0 and 1 of sample index i are T·i; with i = (frame << 2m) | j the low block of T is
+// dimensions 0 and 1 of sample index i are T·i; with i = (frame << 2m) | j (up to 52 bits) the low block of T is
 // invertible (the first two dimensions form a (0,2)-sequence), so j = T_low^-1 (p ^ T_high·frame)
-// with p = (px << m) | py.  out = T_low^-1 columns [2m], then T_high columns [32 - 2m].
+// with p = (px << m) | py.  out = T_low^-1 columns [2m], then T_high columns [52 - 2m].
 void sobol_pixel_tables(const uint32_t* mats, int m, std::vector<uint32_t>* out) {
     out->clear();
     if (m <= 0) return;
@@ -817,9 +787,9 @@ void sobol_pixel_tables(const uint32_t* mats, int m, std::vector<uint32_t>* out)
     }
     // now T_low · inv[r] (as a combination of index bits) = unit vector e_r: inv[r] is the index
     // bit pattern that produces pixel bit r
-    out->resize(32);
+    out->resize(kSobolMatrixSize);   // frame bits reach index bit 51 (64-bit pbrt-v3 indices)
     for (int r = 0; r < n; ++r) (*out)[r] = inv[r];
-    for (int k = 0; k < 32 - n; ++k) (*out)[n + k] = col(n + k);
+    for (int k = 0; k < kSobolMatrixSize - n; ++k) (*out)[n + k] = col(n + k);
 }
 
 }  // namespace pbr

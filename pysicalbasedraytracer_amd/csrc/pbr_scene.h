@@ -79,6 +79,7 @@ void halton_params(int resX, int resY, DeviceSampler* s);
 // Sobol (pbrt-v3 SobolSampler): built-in generator matrices [nDims][kSobolMatrixSize] and the
 // pixel → sample-index tables for resolution 2^m (see pbr_scene.cpp).
 constexpr int kSobolMatrixSize = 52;
+constexpr int kSobolMaxDims = 1024;   // SobolMatrices32 rows (NumSobolDimensions, SobolMatrices.h)
 void build_sobol_matrices(int nDims, std::vector<uint32_t>* out);
 void sobol_pixel_tables(const uint32_t* mats, int m, std::vector<uint32_t>* out);
 

@@ -110,7 +110,8 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams
     int x, y;
     pixel_xy(P, W.chunkPix0 + lp, &x, &y);
     SState st;
-    st.index = sample_index(P.smp, x, y, s);
+    st.index = sample_index(P.smp, x, y, s).lo;
+    st.sid = s;
     st.dim = 0;
     st.px = x;
     st.py = y;
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                     L = L + si_Le(S, isect, wo);
                     SState st;
                     st.index = W.sampleIndex[id];
+                    st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
                     st.dim = dim;
                     st.px = st.py = 0;   // dims >= 2 only past the camera
                     {   // the single light (WhittedIntegrator.cpp:39-54)
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
         BSDF bsdf;
         rgb L = sp(0.f);
         SState st;
-        st.index = 0; st.dim = 0; st.px = st.py = 0;
+        st.index = 0; st.dim = 0; st.px = st.py = 0; st.sid = 0;
         if (active) {
             float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
             id = level0 ? q : W.cur.id[q];
@@ -393,6 +395,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
                     shading = true;
                     L = sp(0.f) + si_Le(S, isect, isect.wo);
                     st.index = W.sampleIndex[id];
+                    st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
                     st.dim = dim;
                     nonSpecular = num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0;
                 }

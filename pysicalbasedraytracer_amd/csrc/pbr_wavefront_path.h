@@ -48,7 +48,8 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
     int x, y;
     pixel_xy(P, W.chunkPix0 + lp, &x, &y);
     SState st;
-    st.index = sample_index(P.smp, x, y, s);
+    st.index = sample_index(P.smp, x, y, s).lo;
+    st.sid = s;
     st.dim = 0;
     st.px = x;
     st.py = y;
@@ -130,6 +131,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
             } else if (alive) {
                 SState st;
                 st.index = W.sampleIndex[id];
+                st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
                 st.dim = dim;
                 st.px = st.py = 0;
                 const f3 wo = isect.wo;

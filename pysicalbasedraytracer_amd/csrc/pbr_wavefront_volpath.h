@@ -83,6 +83,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             float etaScale = bv.w;
             SState st;
             st.index = W.sampleIndex[id];
+            st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
             st.dim = dim;
             st.px = st.py = 0;
             Isect isect;
@@ -317,13 +318,14 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfv_tr(WfvParams V) {
             V.dTr[V.tid[q]] = make_float4(Tr.r, Tr.g, Tr.b, 0.f);
             continue;
         }
-        for (int guard = 0; guard < 256; ++guard) {
+        for (int guard = 0;; ++guard) {
             HitRec h;
             Counters c;
             const bool hit = traverse<false, false, SHORT>(S, ray, &h, &c);
             if (hit && S.primInfo[h.slot].y >= 0) { Tr = sp(0.0f); break; }
             if (ray.medium >= 0) Tr = Tr * medium_tr(S, ray.medium, ray);
             if (!hit) break;
+            if (guard == kMaxTrCrossings) { atomicOr(S.guard, kGuardTransmittance); break; }
             Isect isect;
             int flags = __float_as_int(S.triVerts[3 * (size_t)h.slot].w);
             if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)h.slot].x)], ray, ray.tMax, &isect);

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
+from parity import assert_parity
 from pysicalbasedraytracer_amd import HipRenderer, capi, scenes
 
 pytestmark = pytest.mark.gpu
@@ -83,7 +84,7 @@ def test_degenerate_frames_and_odd_spp(hip, w, h, spp):
         rd = scenes.render_desc(cam, integ, spp, 5)
         g, g8, st = hip.render(rd)
         c, c8, _ = O.render(s, rd)
-        assert np.abs(g - c).max() <= 1e-3 and np.abs(g8.astype(int) - c8.astype(int)).max() <= 1
+        assert_parity(g, c, g8, c8)
         assert st.samples == w * h * spp
 
 
@@ -133,7 +134,7 @@ def test_spp_beyond_one_finish_tile(hip, integrator):
     g, g8, st = hip.render(rd)
     c, c8, _ = O.render(s, rd)
     assert st.samples == 4 * 3 * 4100
-    assert np.abs(g - c).max() <= 1e-3 and np.abs(g8.astype(int) - c8.astype(int)).max() <= 1
+    assert_parity(g, c, g8, c8)
 
 
 def test_deep_whitted_mirror_box(hip, monkeypatch):
@@ -155,7 +156,7 @@ def test_deep_whitted_mirror_box(hip, monkeypatch):
         rd = scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 4, depth)
         g, g8, _ = hip.render(rd)
         c, c8, _ = O.render(s, rd)
-        assert np.abs(g - c).max() <= 1e-3 and np.abs(g8.astype(int) - c8.astype(int)).max() <= 1, depth
+        assert_parity(g, c, g8, c8)
         monkeypatch.setenv("PBR_WAVEFRONT", "0")
         mk, _, _ = hip.render(rd)
         monkeypatch.delenv("PBR_WAVEFRONT")

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
+from parity import assert_parity
 from pysicalbasedraytracer_amd import HipRenderer, capi, scenes
 
 pytestmark = pytest.mark.gpu
@@ -23,9 +24,7 @@ def check(hip, s, rd):
     hip.upload(s)
     g, g8, _ = hip.render(rd)
     c, c8, _ = O.render(s, rd)
-    d = float(np.abs(g.astype(np.float64) - c).max())
-    assert np.isfinite(g).all() and d <= 1e-3, d
-    assert np.abs(g8.astype(int) - c8.astype(int)).max() <= 1
+    assert_parity(g, c, g8, c8)
     return g
 
 
@@ -116,6 +115,66 @@ def test_material_less_medium_interface(hip, integrator, monkeypatch):
     monkeypatch.setenv("PBR_WAVEFRONT", "0")
     mk, _, _ = hip.render(rd)
     assert np.array_equal(mk.view(np.uint32), g.view(np.uint32))
+
+
+def nested_shells(n, r0=0.05, r1=0.6, medium=True, center=(0.0, 0.1, 0.2)):
+    """A matte patch behind n concentric material-less spheres (pass-through surfaces), the
+    outermost one bounding a homogeneous medium, and an area light."""
+    s = scenes.Scene()
+    P, I, UV = uv_patch()
+    s.mesh(P, I, s.matte((0.6, 0.6, 0.6)))
+    med = s.homogeneous_medium(0.3, 1.5, 0.3) if medium else -1
+    for k, r in enumerate(np.linspace(r1, r0, n)):
+        if k == 0 and medium:
+            s.sphere(center, float(r), -1, medium_inside=med, medium_outside=-1)
+        else:
+            s.sphere(center, float(r), -1)
+    Pl, Il = scenes.quad(1.8, 0.8, flip=True)
+    s.area_light_mesh(Pl, Il, (4.0, 4.0, 4.0), s.matte((0.5, 0.5, 0.5)))
+    return s
+
+
+@pytest.mark.parametrize("integrator", [capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH])
+def test_many_material_less_crossings(hip, integrator, monkeypatch):
+    """20 nested material-less shells: a path through the centre crosses 40 surfaces before its
+    first bounce, more than the 32 extra levels the wavefront schedules up front.  The schedule
+    keeps extending while continuations are queued, so it equals the megakernel (which loops
+    without a bound, as the reference does) bit for bit, and the oracle."""
+    s = nested_shells(20)
+    cam = scenes.camera(40, 28, CAM["eye"], CAM["look"])
+    rd = scenes.render_desc(cam, integrator, 4, 5)
+    g = check(hip, s, rd)
+    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    mk, _, _ = hip.render(rd)
+    assert np.array_equal(mk.view(np.uint32), g.view(np.uint32))
+
+
+def test_transmittance_walk_bound_fails_loudly(hip, monkeypatch):
+    """300 nested shells centred on a point of the patch: a shadow ray from there to the light
+    crosses 300 interfaces (VisibilityTester::Tr), past the 256-interface safety bound, so the
+    render fails with an error (both schedules) instead of returning a truncated transmittance.
+    The camera rays' 300 pass-through crossings are followed (the wavefront keeps extending).
+    Asynchronous frames report the failure at the next call (pbr_hip_sync)."""
+    import torch
+    s = nested_shells(300, r0=0.3, r1=0.6, center=(0.0, 0.0, -0.2))
+    cam = scenes.camera(16, 12, CAM["eye"], CAM["look"])
+    rd = scenes.render_desc(cam, capi.INTEGRATOR_VOLPATH, 2, 3)
+    hip.upload(s)
+    with pytest.raises(RuntimeError, match="transmittance walk"):
+        hip.render(rd)
+    g, _, _ = hip.render(scenes.render_desc(cam, capi.INTEGRATOR_PATH, 2, 3))   # Path has no Tr walk
+    assert np.isfinite(g).all()
+    n = 16 * 12
+    rgb = torch.empty((n, 3), dtype=torch.float32, device="cuda")
+    rgba = torch.empty((n, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    hip.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
+    with pytest.raises(RuntimeError, match="transmittance walk"):
+        hip.sync()
+    hip.sync()   # the failure is reported once
+    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    with pytest.raises(RuntimeError, match="transmittance walk"):
+        hip.render(rd)
 
 
 def test_none_material_is_no_material(hip):

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
+from parity import assert_parity
 from pysicalbasedraytracer_amd import HipRenderer, assemble, capi, scenes, tile_grid
 
 pytestmark = pytest.mark.gpu
@@ -30,15 +31,7 @@ def small_dragon(n=48):
 
 
 def compare(gpu_rgb, cpu_rgb, gpu8=None, cpu8=None):
-    d = np.abs(gpu_rgb.astype(np.float64) - cpu_rgb.astype(np.float64))
-    linf = float(np.nanmax(d)) if d.size else 0.0
-    exact = float(np.mean(np.all(gpu_rgb.view(np.uint32) == cpu_rgb.view(np.uint32), axis=1)))
-    assert np.isfinite(gpu_rgb).all()
-    assert linf <= LINF, f"per-pixel L∞ {linf} > {LINF} (bit-exact pixels {exact:.4f})"
-    if gpu8 is not None:
-        diff8 = np.abs(gpu8.astype(int) - cpu8.astype(int)).max()
-        assert diff8 <= 1
-    return linf, exact
+    return assert_parity(gpu_rgb, cpu_rgb, gpu8, cpu8, LINF)
 
 
 def test_halton_kats_on_device(hip):
@@ -198,6 +191,51 @@ def test_full_size_c2_properties(hip):
     compare(g[picks], c, g8[picks], c8)
 
 
+def test_benchmarked_c2_frame_bit_exact(hip):
+    """The exact path bench.py times: full C2 (1920×1080×64, 132.7 M samples → four 2^25-sample
+    chunks over the two chunk lanes, single-light wavefront Whitted with k_wf_shade), rendered
+    asynchronously into device buffers on a non-default stream with the bench's tile list, then
+    256 spot pixels (plus the four corners) compared with the oracle: float and RGBA8 bit for bit."""
+    import torch
+    s, rd = scenes.config_c2()
+    W, H, spp = rd.camera.width, rd.camera.height, rd.spp
+    rdr = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                             rd.sampler, tiles=[(0, 0, W, H)])
+    hip.upload(s)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    rgb = torch.full((W * H, 3), float("nan"), dtype=torch.float32, device=dev)
+    rgba = torch.zeros((W * H, 4), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    for _ in range(2):   # two frames back to back, as the bench queues them
+        hip.render_device(rdr, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
+    stream.synchronize()
+    g, g8 = rgb.cpu().numpy(), rgba.cpu().numpy()
+    assert np.isfinite(g).all() and (g8[:, 3] == 255).all()
+    rng = np.random.default_rng(2024)
+    picks = np.concatenate([rng.choice(W * H, 256, replace=False), [0, W - 1, (H - 1) * W, W * H - 1]])
+    tiles = [(int(p % W), int(p // W), int(p % W) + 1, int(p // W) + 1) for p in picks]
+    c, c8, _ = O.render(s, scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, tiles=tiles))
+    assert np.array_equal(g[picks].view(np.uint32), c.view(np.uint32)), \
+        f"float pixels differ: {int((g[picks].view(np.uint32) != c.view(np.uint32)).any(axis=1).sum())} of {len(picks)}"
+    assert np.array_equal(g8[picks], c8)
+
+
+def test_whitted_multichunk_two_lanes(hip, monkeypatch):
+    """Single-light wavefront Whitted over many chunks (PBR_CHUNK_LOG2=16: 2^16-sample chunks, so
+    a 160×90×32 frame is 8 chunks alternating over the two lanes and their streams) against the
+    oracle over the whole frame, float and RGBA8 bit for bit, and equal to the one-chunk render."""
+    s, rd = scenes.config_c2(160, 90, 32, mesh=small_dragon(64))
+    hip.upload(s)
+    one, one8, _ = hip.render(rd)
+    monkeypatch.setenv("PBR_CHUNK_LOG2", "16")
+    g, g8, _ = hip.render(rd)
+    c, c8, _ = O.render(s, rd)
+    assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+    assert np.array_equal(g8, c8)
+    assert np.array_equal(g.view(np.uint32), one.view(np.uint32))
+
+
 def test_errors_fail_loudly(hip):
     fresh = HipRenderer(0)
     s, rd = scenes.config_c1(8, 8, 1)
@@ -226,23 +264,42 @@ SOBOL = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "sobol_
 
 
 def test_sobol_kats_on_device(hip):
-    """Sample index + dims 0/1 of the reference-table fixture (32-bit index cases), on the device."""
+    """Sample index + dimensions 0-127 of the reference-table fixture on the device, bit for bit,
+    including the sample numbers whose 64-bit index needs bits >= 32 (no case skipped)."""
+    nd = SOBOL["high_dims"]
     for c in SOBOL["cases"]:
         (w, h), (px, py), s = c["raster"], c["pixel"], c["sample"]
-        if c["index"] >= 2 ** 32:
-            continue
-        v = hip.sampler_values(w, h, 1, [(px, py, s, 0), (px, py, s, 1)], sampler=capi.SAMPLER_SOBOL)
-        assert ["%08x" % u for u in v.view(np.uint32)] == [c["dim0"], c["dim1"]], c
+        v = hip.sampler_values(w, h, 1, [(px, py, s, d) for d in range(nd)], sampler=capi.SAMPLER_SOBOL)
+        bits = ["%08x" % u for u in v.view(np.uint32)]
+        assert bits[:2] == [c["dim0"], c["dim1"]], c
+        assert "".join(bits[2:]) == c["dims2_127"], c
 
 
 def test_sobol_random_queries_bit_exact(hip):
     rng = np.random.default_rng(5)
-    for (w, h, spp) in [(1920, 1080, 256), (256, 256, 16), (100, 37, 8), (1, 1, 4)]:
+    for (w, h, spp) in [(1920, 1080, 256), (256, 256, 16), (100, 37, 8), (1, 1, 4), (3840, 2160, 4096)]:
         q = np.stack([rng.integers(0, w, 4000), rng.integers(0, h, 4000), rng.integers(0, spp, 4000),
                       rng.integers(0, 1024, 4000)], axis=1).astype(np.int32)
         g = hip.sampler_values(w, h, spp, q, sampler=capi.SAMPLER_SOBOL)
         c, _ = O.sobol(w, h, q)
         assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+
+
+def test_sobol_wide_index_render(hip, monkeypatch):
+    """A Sobol Path render whose sample indices need more than 32 bits (resolution 2^12 from a
+    4096-pixel-wide raster, 512 spp → 2^33) through both schedules, against the oracle.  A tile
+    keeps the frame small; the sampler still works at the full raster's resolution."""
+    s, rd = scenes.config_c3(4096, 8, 512, mesh=small_dragon(24))
+    rd2 = scenes.render_desc(rd.camera, rd.integrator, 512, 3, rd.rr_threshold, rd.light_strategy,
+                             capi.SAMPLER_SOBOL, tiles=[(2040, 2, 2056, 4)])
+    hip.upload(s)
+    g, g8, st = hip.render(rd2)
+    assert st.samples == 16 * 2 * 512
+    c, c8, _ = O.render(s, rd2)
+    compare(g, c, g8, c8)
+    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    mk, mk8, _ = hip.render(rd2)
+    assert np.array_equal(g.view(np.uint32), mk.view(np.uint32))
 
 
 def test_c3_path_halton(hip):

@@ -132,23 +132,32 @@ SOBOL = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "sobol_
 
 
 def test_sobol_index_and_pixel_dims_bit_exact():
-    """pbrt-v3 SobolIntervalToIndex + SampleDimension dims 0/1 as evaluated with the reference's own
+    """pbrt-v3 SobolIntervalToIndex + SampleDimension as evaluated with the reference's own
     VdCSobolMatrices / SobolMatrices32 (tests/golden/make_sobol_kats.py), reproduced by the
-    oracle's GF(2) solve at five rasters including 1×1 (index 0) and 3840×2160."""
+    oracle's GF(2) solve at five rasters including 1×1 (index 0) and 3840×2160, with sample
+    numbers whose 64-bit index needs bits >= 32: the index and dimensions 0-127, bit for bit."""
+    wide = 0
     for c in SOBOL["cases"]:
         (w, h), (px, py), s = c["raster"], c["pixel"], c["sample"]
-        v, idx = O.sobol(w, h, [(px, py, s, 0), (px, py, s, 1)])
+        q = [(px, py, s, d) for d in range(SOBOL["high_dims"])]
+        v, idx = O.sobol(w, h, q)
         assert int(idx[0]) == c["index"], c
-        assert ["%08x" % u for u in v.view(np.uint32)] == [c["dim0"], c["dim1"]], c
+        bits = ["%08x" % u for u in v.view(np.uint32)]
+        assert bits[:2] == [c["dim0"], c["dim1"]], c
+        assert "".join(bits[2:]) == c["dims2_127"], c
+        wide += c["index"] >= 2 ** 32
+    assert wide >= 60   # the fixture exercises 64-bit indices
 
 
-def test_sobol_builtin_dims01_are_the_references():
-    """The built-in matrices' dimensions 0 and 1 (all 52 columns) hash to the reference's
-    SobolMatrices32 rows; the device library's host builder produces the oracle's table."""
+def test_sobol_builtin_is_the_reference_table():
+    """The built-in matrices — regenerated from the Joe-Kuo direction numbers of pbr_sobol_jk.h —
+    hash to the reference's whole SobolMatrices32 table (1024 dims × 52 columns) and to its
+    dimension-0/1 rows; the device library's host builder produces the oracle's table."""
     import ctypes as C
     import hashlib
     m = O.sobol_matrices(1024)
-    assert hashlib.sha256(m[:104].tobytes()).hexdigest() == SOBOL["dims01_sha256"]
+    assert hashlib.sha256(m[:104].astype("<u4").tobytes()).hexdigest() == SOBOL["dims01_sha256"]
+    assert hashlib.sha256(m.astype("<u4").tobytes()).hexdigest() == SOBOL["all_sha256"]
     d = np.empty(1024 * 52, np.uint32)
     assert capi.load_library().pbr_hip_sobol_matrices(1024, d.ctypes.data_as(C.POINTER(C.c_uint32))) == 0
     assert np.array_equal(d, m)
