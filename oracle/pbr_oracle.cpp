@@ -202,8 +202,12 @@ struct Builder {
                 return leaf(node, pi, start, end, bounds);
             }
         }
-        BuildNode* c0 = build(pi, start, mid, totalNodes);
+        // InitInterior(dim, recursiveBuild(start, mid), recursiveBuild(mid, end)) (BVHAccel.cpp:250-254):
+        // C++ leaves the order of the two argument evaluations open; GCC (and MSVC) evaluate them
+        // right to left, so the SECOND child's subtree is built — and its primitives appended to
+        // orderedPrims — first.  Pinned by the reference-built node array (ref_fixtures.json).
         BuildNode* c1 = build(pi, mid, end, totalNodes);
+        BuildNode* c0 = build(pi, start, mid, totalNodes);
         node->children[0] = c0;
         node->children[1] = c1;
         node->bounds = Union(c0->bounds, c1->bounds);

@@ -175,6 +175,7 @@ class SahBuilder {
     void run() {
         nodes_->clear();
         order_->clear();
+        leaves_.clear();
         if (it_.empty()) return;
         // explicit DFS: each task is (start, end, parentIndexToPatch or -1)
         struct Task { int start, end, patch; };
@@ -200,6 +201,18 @@ class SahBuilder {
             todo.push_back({mid, t.end, me});
             todo.push_back({t.start, mid, -1});
         }
+        // Primitive order.  BVHAccel::recursiveBuild appends a leaf's primitives to orderedPrims
+        // when the leaf is built, and builds an interior node's children inside one call,
+        // InitInterior(dim, recursiveBuild(start, mid), recursiveBuild(mid, end))
+        // (BVHAccel.cpp:250-254), whose arguments GCC and MSVC evaluate right to left: the second
+        // child's subtree comes first.  Over the whole tree that is the leaves in reverse of the
+        // left-first order collected above, each leaf's primitives in range order.  (The
+        // partitions are per disjoint range, so the build order changes nothing else.)
+        for (size_t k = leaves_.size(); k-- > 0;) {
+            const Leaf& l = leaves_[k];
+            (*nodes_)[l.node].offset = (int32_t)order_->size();
+            for (int i = l.start; i < l.end; ++i) order_->push_back((int32_t)it_[i].id);
+        }
     }
 
   private:
@@ -210,9 +223,8 @@ class SahBuilder {
     void emit_leaf(int me, int s, int e, const Box& box) {
         LinearBVHNode& n = (*nodes_)[me];
         put_box(n, box);
-        n.offset = (int32_t)order_->size();
         n.nPrimitives = (uint16_t)(e - s);
-        for (int i = s; i < e; ++i) order_->push_back((int32_t)it_[i].id);
+        leaves_.push_back({me, s, e});   // primitivesOffset: assigned in build order (run())
     }
     // Decide leaf vs interior for [s,e); on interior, partitions it_ and returns the split.
     bool split(int s, int e, int* mid, int* axis, Box* box) {
@@ -266,6 +278,8 @@ class SahBuilder {
         return true;
     }
 
+    struct Leaf { int node, start, end; };
+    std::vector<Leaf> leaves_;
     std::vector<Item>& it_;
     int maxPrims_;
     std::vector<LinearBVHNode>* nodes_;

@@ -227,9 +227,29 @@ def find_dragon():
     return P, I, "standin:displaced-uv-sphere-224"
 
 
+def rgbe_roundtrip(img):
+    """What stbi_loadf returns for `img` written with stbi_write_hdr: each pixel in the .hdr
+    format's shared-exponent RGBE bytes (stb_image_write's stbiw__linear_to_rgbe: frexp of the
+    largest component, channels scaled by mantissa·256/max and truncated) decoded as byte·2^(E−136)
+    (stb_image's stbi__hdr_convert).  The reference reads environment maps only from .hdr files
+    (SkyBoxLight.cpp:19-24, InfiniteAreaLight.cpp:14-21), so a map it can see has these values; they
+    survive another write/read unchanged."""
+    img = np.asarray(img, dtype=f32)
+    e = img.reshape(-1, img.shape[-1])
+    mx = e[:, :3].max(axis=1)
+    out = np.zeros_like(e)
+    ok = mx >= f32(1e-32)
+    mant, ex = np.frexp(mx[ok])
+    norm = (mant.astype(f32) * f32(256.0) / mx[ok]).astype(f32)
+    b = np.floor((e[ok, :3] * norm[:, None]).astype(f32)).astype(np.float64)
+    out[ok, :3] = (b * np.ldexp(1.0, ex - 8)[:, None]).astype(f32)
+    return np.ascontiguousarray(out.reshape(img.shape))
+
+
 def procedural_sky(width=2048, height=1024, seed=7):
     """Deterministic equirect HDR (sky gradient + sun + cloud noise), rows bottom-up as
-    stbi_loadf returns them after stbi_set_flip_vertically_on_load(true) (SkyBoxLight.cpp:20)."""
+    stbi_loadf returns them after stbi_set_flip_vertically_on_load(true) (SkyBoxLight.cpp:20), with
+    the values an .hdr file can hold (rgbe_roundtrip)."""
     rng = np.random.default_rng(seed)
     v = (np.arange(height, dtype=np.float64) + 0.5) / height          # 0 bottom .. 1 top
     u = (np.arange(width, dtype=np.float64) + 0.5) / width
@@ -254,7 +274,7 @@ def procedural_sky(width=2048, height=1024, seed=7):
     # sun
     sd = np.hypot((U - 0.3) * 2, (Vv - 0.75))
     img += (np.exp(-(sd / 0.02) ** 2) * 40.0)[..., None] * np.array([1.0, 0.95, 0.85])
-    return np.ascontiguousarray(img.astype(f32))
+    return rgbe_roundtrip(img.astype(f32))
 
 
 # ----------------------------------------------------------------------------- scene container

@@ -1,0 +1,96 @@
+"""Loader for the reference itself (oracle/_ref/libpbr_ref.so, built by oracle/ref/Makefile from the
+reference's unmodified sources) — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/golden/make_ref_fixtures.py (in the development container, where /root/reference
+exists) to write reference-output fixtures, and by bench.py's cpu_baseline leg when the library was
+built.  The same plain-data descriptors as oracle_lib / the product: scenes.Scene.desc() and
+scenes.render_desc()."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from pysicalbasedraytracer_amd import capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libpbr_ref.so")
+_lib = None
+
+
+def available():
+    return os.path.exists(REF_SO)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not available():
+        raise RuntimeError(f"{REF_SO} not built (make -C oracle/ref, development container only)")
+    lib = C.CDLL(REF_SO)
+    P = C.POINTER
+    lib.ref_render.argtypes = [P(capi.SceneDesc), P(capi.RenderDesc), C.c_void_p, C.c_void_p, C.c_int, P(C.c_double)]
+    lib.ref_render_frame.argtypes = [P(capi.SceneDesc), P(capi.RenderDesc), C.c_void_p, P(C.c_double)]
+    lib.ref_build_bvh.argtypes = [P(capi.SceneDesc), C.c_void_p, P(C.c_int), P(C.c_int32), P(C.c_int)]
+    lib.ref_intersect.argtypes = [P(capi.SceneDesc), C.c_int, P(C.c_float), P(C.c_float), C.c_int]
+    lib.ref_camera_rays.argtypes = [P(capi.CameraDesc), C.c_int, P(C.c_float), P(C.c_float)]
+    _lib = lib
+    return lib
+
+
+def _npx(rdesc):
+    if rdesc.n_tiles:
+        return sum((rdesc.tiles[i].x1 - rdesc.tiles[i].x0) * (rdesc.tiles[i].y1 - rdesc.tiles[i].y0)
+                   for i in range(rdesc.n_tiles))
+    return rdesc.camera.width * rdesc.camera.height
+
+
+def render(scene, rdesc, threads=0):
+    """(rgb float32 [n,3], rgba uint8 [n,4], seconds) in packed tile order, like oracle_lib.render."""
+    d = scene.desc()
+    n = _npx(rdesc)
+    rgb = np.empty((n, 3), np.float32)
+    rgba = np.empty((n, 4), np.uint8)
+    sec = C.c_double()
+    rc = load().ref_render(C.byref(d), C.byref(rdesc), rgb.ctypes.data, rgba.ctypes.data, threads, C.byref(sec))
+    assert rc == 0, rc
+    return rgb, rgba, sec.value
+
+
+def render_frame(scene, rdesc):
+    """The reference's own Integrator::Render on a square raster: its FrameBuffer bytes
+    [H, W, 4], row 0 = the image's bottom row (set_uc(i, H - j - 1, ...))."""
+    d = scene.desc()
+    W, H = rdesc.camera.width, rdesc.camera.height
+    out = np.empty((H, W, 4), np.uint8)
+    sec = C.c_double()
+    assert load().ref_render_frame(C.byref(d), C.byref(rdesc), out.ctypes.data, C.byref(sec)) == 0
+    return out, sec.value
+
+
+def build_bvh(scene):
+    d = scene.desc()
+    nn, npr = C.c_int(), C.c_int()
+    assert load().ref_build_bvh(C.byref(d), None, C.byref(nn), None, C.byref(npr)) == 0
+    nodes = np.empty(nn.value * 32, np.uint8)
+    ids = np.empty(npr.value, np.int32)
+    assert load().ref_build_bvh(C.byref(d), nodes.ctypes.data, C.byref(nn), capi.iptr(ids), C.byref(npr)) == 0
+    return nodes, ids
+
+
+def intersect(scene, rays, any_hit=False):
+    """{hit, t, original primitive index, p.xyz} per ray (o.xyz, d.xyz, tMax)."""
+    d = scene.desc()
+    r = np.ascontiguousarray(rays, np.float32).reshape(-1, 7)
+    out = np.empty((r.shape[0], 6), np.float32)
+    assert load().ref_intersect(C.byref(d), r.shape[0], capi.fptr(r), capi.fptr(out), int(any_hit)) == 0
+    return out
+
+
+def camera_rays(cam, pfilm):
+    pf = np.ascontiguousarray(pfilm, np.float32).reshape(-1, 2)
+    out = np.empty((pf.shape[0], 6), np.float32)
+    assert load().ref_camera_rays(C.byref(cam), pf.shape[0], capi.fptr(pf), capi.fptr(out)) == 0
+    return out
