@@ -1,69 +1,185 @@
 """Headline benchmark: Msamples/s of the MI355X render path on BASELINE config C2
 (1920×1080, 64 spp, WhittedIntegrator, dragon + mirror floor + SkyBox HDR), with the roofline of the
-dominant kernel and the CPU restatement timed beside it.
+dominant kernel and the reference's own CPU path timed beside it.
 
 One step = one full frame.  With --gpus N (launched by torch.distributed.run, one rank per GPU)
 the frame's 32×32 tiles are dealt round-robin over ranks and rank 0 gathers the per-tile RGBA8
 FrameBuffer spans over RCCL — total work is fixed, so scaling is strong.  The gather of frame k
 runs on a communication stream while frame k+1 renders into the other of two output buffers.
+
+Measurement windows (all after the warm-up frames):
+  1. the timed region: K frames back to back, barrier + synchronize on both sides → `value`;
+  2. K more frames with a HIP event pair around every kernel launch, on the stream it runs on
+     (pbr_hip_set_profiling(1)) → per-kernel-family launch durations;
+  3. one frame with work counters (pbr_hip_set_profiling(2)) → units and algorithmic HBM bytes per
+     family (the compulsory queue / record / output bytes of the wavefront design).
+The roofline names the family with the largest summed duration: achieved = its algorithmic bytes
+per launch ÷ its mean launch duration; traffic = rocprofv3 PMC bytes per launch of the same family
+(profiles/<config>_traffic.json, used only when measured on the very build that is loaded).
+
+The CPU baseline (rank 0, N=1) runs FIRST, in a child process started before this process touches
+the GPU: the reference itself (oracle/_ref/libpbr_ref.so, its unmodified sources built by
+oracle/ref/Makefile) when that library is present — else the oracle/ restatement — on the physical
+cores of socket 0 (lscpu), pinned one thread per core, OMP_PLACES=cores OMP_PROC_BIND=close, over
+an evenly spread sample of the frame's rows; plus the reference's as-shipped 4 threads
+(Integrator.cpp:282).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from pysicalbasedraytracer_amd import FrameGather, HipRenderer, scenes, tiles_for_rank  # noqa: E402
-
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# Algorithmic bytes model: 32 B per LinearBVHNode test, 48 B per primitive test,
-# 96 B of ray-queue traffic per traced ray, 64 B per shading event.  The counts come from an
-# instrumented pass that counts tests exactly as BVHAccel performs them (pbr_device.h traverse).
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6290.0        # measured device-to-device copy rate in the same guide
+# SURVEY §8(d) per-sample model (32 B per node test, 48 per primitive test, 96 per ray, 64 per
+# shading event): reported for reference only — it counts cache-served BVH/mesh fetches as HBM
+# bytes, so it is not a bound
 B_NODE, B_PRIM, B_RAY, B_SHADE = 32, 48, 96, 64
-# rocprofv3 PMC HBM bytes per frame (tools/pmc.sh + tools/summarize_prof.py --json=...); used only
-# when it was measured on the very build that is loaded (source hash from pbr_hip_build_info).
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "c2_traffic.json")
 
 
-def pmc_traffic(build_info):
+# ------------------------------------------------------------------------------- CPU baseline
+def cpu_topology():
+    """Socket-0 physical cores (first logical CPU of each), allowed CPUs, cgroup CPU quota."""
+    info = {"sockets": None, "physical_cores_socket0": None, "threads_per_core": None}
+    cores0 = {}
     try:
-        t = json.load(open(TRAFFIC_JSON))
+        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, check=True).stdout
+        sockets, per_core = set(), {}
+        for line in out.splitlines():
+            if not line or line.startswith("#"):
+                continue
+            cpu, core, sock = (int(x) if x else 0 for x in line.split(","))
+            sockets.add(sock)
+            per_core[(sock, core)] = per_core.get((sock, core), 0) + 1
+            if sock == 0:
+                cores0.setdefault(core, cpu)
+        info["sockets"] = len(sockets)
+        info["physical_cores_socket0"] = len(cores0)
+        info["threads_per_core"] = max(per_core.values()) if per_core else None
+    except (OSError, subprocess.CalledProcessError, ValueError):
+        pass
+    allowed = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
     except (OSError, ValueError):
-        return None, "no PMC summary"
-    if not t.get("build") or not build_info.endswith(t["build"]):
-        return None, f"PMC summary is for build {t.get('build')}, not this one"
-    return t["frame_read_bytes"] + t["frame_write_bytes"], f"{os.path.relpath(TRAFFIC_JSON, ROOT)} ({t['method']})"
+        pass
+    info["allowed_cpus"] = len(allowed)
+    info["cgroup_cpu_quota"] = quota
+    pin = [c for c in sorted(cores0.values()) if c in allowed] or allowed
+    n = len(pin)
+    if quota is not None:
+        n = max(1, min(n, int(quota)))
+    info["threads"] = n
+    info["pinned_cpus"] = pin[:n]
+    return info
 
 
-def cpu_baseline(scene, rd, budget_s=12.0):
-    """Oracle (CPU restatement, the reference algorithm) on the host cores, bounded sample."""
+def cpu_baseline_worker(config, threads, budget_s, kind):
+    """Child process: time the CPU render of an evenly spread sample of the frame's rows."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    from pysicalbasedraytracer_amd import scenes
+    if kind == "reference":
+        import ref_lib as lib          # the reference itself (test infrastructure, oracle/_ref)
+    else:
+        import oracle_lib as lib       # the CPU restatement (test infrastructure, oracle/)
+    scene, rd = scenes.CONFIGS[config]()
+    if kind == "reference" and rd.sampler != 0:
+        # the reference has no SobolSampler (F3): its HaltonSampler, same scene and spp
+        rd = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold, rd.light_strategy, 0)
     W, H, spp = rd.camera.width, rd.camera.height, rd.spp
-    rows_per_chunk = 24
-    done_px = 0
-    secs = 0.0
-    y = 0
-    while secs < budget_s and y < H:          # top-down row bands until the budget or the frame ends
-        y1 = min(H, y + rows_per_chunk)
+
+    def run(rows):
+        tiles = [(0, y, W, y + 1) for y in rows]
         rdc = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
-                                 rd.sampler, tiles=[(0, y, W, y1)])
-        _, _, sec = oracle_lib.render(scene, rdc, threads=threads)
-        secs += sec
-        done_px += W * (y1 - y)
-        y = y1
-    samples = done_px * spp
-    return {"value": samples / secs / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"C2 rows [0,{y}) × {W} px × {spp} spp = {samples} samples in {secs:.1f} s "
-                      f"(oracle/ CPU restatement, OpenMP dynamic schedule)"}
+                                 rd.sampler, tiles=tiles)
+        return lib.render(scene, rdc, threads=threads)[2]
+
+    probe_rows = list(range(H // 2, H, max(1, H // 8)))[:4]
+    t = run(probe_rows)
+    per_row = max(t / len(probe_rows), 1e-4)
+    n = int(max(4, min(H, budget_s / per_row)))
+    stride = max(1, H // n)
+    rows = list(range(stride // 2, H, stride))[:n]
+    secs = run(rows)
+    samples = len(rows) * W * spp
+    return {"value": samples / secs / 1e6, "seconds": secs, "rows": len(rows), "row_stride": stride,
+            "samples": samples}
+
+
+def cpu_baseline(config, budget_s):
+    topo = cpu_topology()
+    kind = "reference" if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libpbr_ref.so")) else "port"
+    out = {"unit": "Msamples/s", "kind": kind}
+    legs = [("socket0", topo["threads"], topo["pinned_cpus"], budget_s), ("as_shipped_4", 4, topo["pinned_cpus"][:4], budget_s / 2)]
+    for name, threads, cpus, b in legs:
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PLACES="cores", OMP_PROC_BIND="close",
+                   OMP_DYNAMIC="false")
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-worker", "--config", config,
+               "--threads", str(threads), "--budget", str(b), "--kind", kind]
+        p = None
+        try:
+            p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=60 + 4 * b,
+                               preexec_fn=(lambda c=cpus: os.sched_setaffinity(0, c)) if cpus else None)
+            res = json.loads(p.stdout.strip().splitlines()[-1])
+        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+            res = {"error": f"{type(e).__name__}: {(p.stderr or '')[-300:] if p is not None else ''}"}
+        res["threads"] = threads
+        out[name] = res
+    s0 = out["socket0"]
+    out["value"] = s0.get("value")
+    out["cores"] = topo["threads"]
+    out["sockets"] = topo["sockets"]
+    out["physical_cores"] = topo["physical_cores_socket0"]
+    out["threads"] = topo["threads"]
+    out["topology"] = {k: topo[k] for k in ("threads_per_core", "allowed_cpus", "cgroup_cpu_quota")}
+    if s0.get("value") and topo["physical_cores_socket0"] and topo["threads"] < topo["physical_cores_socket0"]:
+        # the job's CPU share is smaller than socket 0: linear scaling to all its physical cores, an
+        # upper bound on what the reference could reach there (labelled, never used as `value`)
+        out["socket0_linear_estimate"] = round(s0["value"] * topo["physical_cores_socket0"] / topo["threads"], 3)
+    what = ("the reference's own code (oracle/_ref/libpbr_ref.so: its unmodified sources, SamplerIntegrator::"
+            "Render's per-pixel body over the sampled rows)" if kind == "reference" else
+            "the oracle/ CPU restatement")
+    limit = ""
+    if topo["physical_cores_socket0"] and topo["threads"] < topo["physical_cores_socket0"]:
+        limit = (f"; the job may use {topo['threads']} of socket 0's {topo['physical_cores_socket0']} physical cores "
+                 f"(affinity {topo['allowed_cpus']} CPUs, cgroup quota {topo['cgroup_cpu_quota']})")
+    out["sample"] = (f"{config}: {s0.get('rows')} rows (every {s0.get('row_stride')}th) × full width × spp = "
+                     f"{s0.get('samples')} samples in {s0.get('seconds', 0):.1f} s, {what}, "
+                     f"{topo['threads']} threads pinned one per physical core of socket 0, OMP_PLACES=cores "
+                     f"OMP_PROC_BIND=close (no numactl in the image: memory is first-touch local){limit}")
+    return out
+
+
+# ------------------------------------------------------------------------------- GPU bench
+def pmc_traffic(config, build_info):
+    path = os.path.join(ROOT, "profiles", f"{config.lower()}_traffic.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None, f"no PMC summary ({os.path.relpath(path, ROOT)})"
+    if not t.get("build") or not build_info.endswith(t["build"]):
+        return None, f"{os.path.relpath(path, ROOT)} is for build {t.get('build')}, not this one"
+    return t, f"{os.path.relpath(path, ROOT)} ({t['method']})"
+
+
+def family_traffic(t, family):
+    """PMC bytes per frame of one kernel family (rocprof names carry template arguments)."""
+    rd = wr = 0.0
+    hit = False
+    for k, v in t["per_kernel"].items():
+        if k == family or k.startswith(family + "<"):
+            rd += v["read_bytes"]
+            wr += v["write_bytes"]
+            hit = True
+    return (rd + wr) if hit else None
 
 
 def main():
@@ -73,11 +189,28 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU render for the baseline")
+    ap.add_argument("--no-model", action="store_true", help="skip the SURVEY-model counting pass")
+    ap.add_argument("--cpu-baseline-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--threads", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--budget", type=float, default=10.0, help=argparse.SUPPRESS)
+    ap.add_argument("--kind", default="reference", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_baseline_worker:
+        print(json.dumps(cpu_baseline_worker(args.config, args.threads, args.budget, args.kind)), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the CPU baseline runs before this process initialises the GPU
+    cpu = cpu_baseline(args.config, args.cpu_budget) if (world == 1 and not args.no_cpu_baseline) else None
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from pysicalbasedraytracer_amd import FrameGather, HipRenderer, scenes, tiles_for_rank
+
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
@@ -100,8 +233,8 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     # multi-GPU: rank 0 gathers the packed RGBA8 tile spans (the FrameBuffer the reference's Render
-    # fills) over RCCL and scatters them into the frame; double-buffered outputs let the gather of
-    # frame k (communication stream) overlap the render of frame k+1 (render stream)
+    # fills) over RCCL; double-buffered outputs let the gather of frame k (communication stream)
+    # overlap the render of frame k+1 (render stream)
     nbuf = 2 if world > 1 else 1
     rgbs = [torch.empty((npx, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     rgbas = [torch.empty((npx, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
@@ -110,17 +243,13 @@ def main():
     released = [None] * nbuf   # event: the gather that read buffer b has finished
     frame_no = [0]
 
-    def render(ev0=None, ev1=None):
+    def render():
         b = frame_no[0] % nbuf
         frame_no[0] += 1
         if released[b] is not None:
             stream.wait_event(released[b])
-        if ev0 is not None:
-            ev0.record(stream)
         # asynchronous: the frame is enqueued on `stream` and the next one queues behind it
         r.render_device(rdr, rgbs[b].data_ptr(), rgbas[b].data_ptr(), stream=stream.cuda_stream, sync=False)
-        if ev1 is not None:
-            ev1.record(stream)
         if exchange is not None:
             rendered = torch.cuda.Event()
             rendered.record(stream)
@@ -131,81 +260,115 @@ def main():
                 done.record(comm)
             released[b] = done
 
-    # roofline counters: one instrumented, untimed pass on the same workload
-    st = r.render_device(rdr, rgbs[0].data_ptr(), rgbas[0].data_ptr(), stream=stream.cuda_stream, stats=True)
-    torch.cuda.synchronize(dev)
-    samples_rank = npx * spp
-    alg_bytes = B_NODE * st.node_visits + B_PRIM * st.prim_tests + B_RAY * st.rays + B_SHADE * st.shading_events
+    def window(k):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            render()
+        r.sync()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     for _ in range(args.warmup):
         render()
+    r.sync()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    # HIP events bracket each frame's launches on the render stream; read after the final sync
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for ev0, ev1 in evs:
-        render(ev0, ev1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kernel_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # roofline over the whole job: every rank's algorithmic bytes over the slowest rank's frame
-        ab = torch.tensor([float(alg_bytes)], dtype=torch.float64, device=dev)
-        dist.all_reduce(ab, op=dist.ReduceOp.SUM)
-        km = torch.tensor([float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        alg_bytes, kernel_ms, samples_rank = float(ab.item()), [float(km.item())], W * H * spp
+    # 1. the timed region
+    elapsed = window(args.steps)
+    # 2. per-kernel launch durations (HIP events on each launch's stream), same K frames
+    r.set_profiling(1)
+    elapsed_ev = window(args.steps)
+    timing = r.get_profile()
+    # 3. work counters of one frame (units, algorithmic bytes)
+    r.set_profiling(2)
+    window(1)
+    counts = r.get_profile()
+    r.set_profiling(0)
+    # SURVEY §8(d) model counts: the instrumented megakernel pass (binary traversal; same tests)
+    model = None
+    if not args.no_model:
+        st = r.render_device(rdr, rgbs[0].data_ptr(), rgbas[0].data_ptr(), stream=stream.cuda_stream, stats=True)
+        torch.cuda.synchronize(dev)
+        samples_rank = npx * spp
+        mb = B_NODE * st.node_visits + B_PRIM * st.prim_tests + B_RAY * st.rays + B_SHADE * st.shading_events
+        model = {"bytes_per_sample": round(mb / samples_rank, 1),
+                 "per_sample": {"rays": round(st.rays / samples_rank, 3), "node_tests": round(st.node_visits / samples_rank, 2),
+                                "prim_tests": round(st.prim_tests / samples_rank, 3),
+                                "shading_events": round(st.shading_events / samples_rank, 3)},
+                 "formula": "32*node_tests + 48*prim_tests + 96*rays + 64*shading_events (SURVEY 8(d))",
+                 "source": "instrumented megakernel pass (k_render<I,true,1>, binary traversal: the same "
+                           "node/primitive tests BVHAccel performs)",
+                 "note": "not a bound: counts every BVH-node and triangle fetch as HBM bytes, but the BVH and "
+                         "mesh are served by L2 / Infinity Cache / scalar cache"}
+
     ms_per_step = elapsed / args.steps * 1e3
-    total_samples = W * H * spp
-    value = total_samples / (elapsed / args.steps) / 1e6
+    value = W * H * spp / (elapsed / args.steps) / 1e6
 
     if rank == 0:
-        k_ms = float(np.mean(kernel_ms))
-        achieved = alg_bytes / (k_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(build_info) if (world == 1 and args.config == "C2") else (None, "C2, 1 GPU only")
+        pmc, pmc_src = pmc_traffic(args.config, build_info) if world == 1 else (None, "1 GPU only")
+        kernels = {}
+        for fam, tv in timing.items():
+            cv = counts.get(fam, {})
+            lpf = tv["launches"] / args.steps                     # launches per frame
+            avg_ms = tv["ms"] / max(1, tv["launches"])
+            cl = cv.get("launches", 0) or 1
+            alg_launch = cv.get("bytes", 0) / cl                  # algorithmic bytes per launch
+            k = {"launches_per_frame": round(lpf, 2), "ms_per_frame": round(tv["ms"] / args.steps, 3),
+                 "avg_launch_us": round(avg_ms * 1e3, 1), "units_per_frame": cv.get("units"),
+                 "alg_bytes_per_launch": round(alg_launch), "counts_per_frame": cv.get("counts"),
+                 "achieved_gbs": round(alg_launch / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None}
+            k["frac"] = round(k["achieved_gbs"] / HBM_PEAK_GBS, 4) if k["achieved_gbs"] is not None else None
+            if pmc is not None:
+                fb = family_traffic(pmc, fam)
+                if fb is not None and lpf > 0:
+                    k["traffic_per_launch"] = round(fb / lpf)
+                    k["traffic_gbs"] = round(fb / lpf / (avg_ms * 1e-3) / 1e9, 1)
+                    k["traffic_frac"] = round(k["traffic_gbs"] / HBM_PEAK_GBS, 4)
+            kernels[fam] = k
+        dom = max(kernels, key=lambda f: kernels[f]["ms_per_frame"]) if kernels else None
+        dk = kernels.get(dom, {})
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": dk.get("achieved_gbs"), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": dk.get("frac"), "traffic": dk.get("traffic_per_launch"),
+                    "traffic_gbs": dk.get("traffic_gbs"), "traffic_frac": dk.get("traffic_frac"),
+                    "copy_peak_gbs": HBM_COPY_GBS,
+                    "frac_of_copy_peak": round(dk["achieved_gbs"] / HBM_COPY_GBS, 4) if dk.get("achieved_gbs") else None,
+                    "alg_bytes_per_launch": dk.get("alg_bytes_per_launch"), "avg_launch_us": dk.get("avg_launch_us"),
+                    "launches_per_frame": dk.get("launches_per_frame"),
+                    "definition": "achieved = the family's algorithmic HBM bytes per launch (compulsory queue/record/"
+                                  "output bytes per counted unit, DESIGN.md 7, counted on the device) / its mean launch "
+                                  "duration (HIP events on its own stream); traffic = rocprofv3 PMC bytes per launch "
+                                  "(FETCH_SIZE x2 + WRITE_SIZE)",
+                    "traffic_source": pmc_src, "window_ms_per_step": round(elapsed_ev / args.steps * 1e3, 3),
+                    "kernels": kernels, "survey_model": model, "build": build_info}
         out = {
             "metric": "Msamples/sec (whole node) + wall-clock to 1080p/64spp frame; %HBM roofline",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.config}: {W}x{H}, {spp} spp, "
-                                   f"{['Whitted', 'Path', 'VolPath'][rd.integrator]} d{rd.max_depth}",
+                                   f"{['Whitted', 'Path', 'VolPath'][rd.integrator]} d{rd.max_depth}"
+                                   f"{', Sobol' if rd.sampler == 1 else ''}",
                        "scene": scene.info.get("dragon", ""), "triangles": scene.info.get("triangles"),
-                       "parallelism": f"tiles32x32 round-robin over {world} GPU(s), RCCL gather of RGBA8 spans",
+                       "parallelism": (f"tiles32x32 round-robin over {world} GPUs, RCCL gather of RGBA8 spans"
+                                       if world > 1 else "1 GPU, whole frame (no exchange)"),
                        "frame_ms": round(ms_per_step, 3), "scene_upload_s": round(upload_s, 3)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         # measured HBM bytes over the same frame time: what HBM actually moved
-                         # (the algorithmic bytes include BVH/mesh fetches that L2 and the
-                         # Infinity Cache serve, which is how `frac` can exceed 1)
-                         "traffic_gbs": None if traffic is None else round(traffic / (k_ms * 1e-3) / 1e9, 1),
-                         "traffic_frac": None if traffic is None else round(traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "kernel": ["wavefront frame: k_wf_camera_extend, (k_wf_shade, k_wf_shadow, k_wf_extend) per "
-                                    "level, k_wf_finish, per 2^25-sample chunk",
-                                    "wavefront frame: k_wfp_camera_extend, (k_wfp_shade, k_wfp_shadow, k_wfp_probe, "
-                                    "k_wfp_resolve, k_wf_extend) per bounce, k_wfp_finish, per 2^25-sample chunk",
-                                    "wavefront frame: k_wfp_camera_extend, (k_wfv_shade, k_wfv_tr, k_wfp_probe, "
-                                    "k_wfv_resolve, k_wf_extend) per bounce, k_wfp_finish, per 2^25-sample chunk"][rd.integrator],
-                         "kernel_ms": round(k_ms, 3),
-                         "bytes_per_sample": round(alg_bytes / samples_rank, 1),
-                         "model": "per sample: 32*node_tests + 48*prim_tests + 96*rays + 64*shading_events "
-                                  "(SURVEY 8(d)); counts from an instrumented pass over this frame",
-                         "note": "frac counts every BVH-node and triangle fetch as HBM bytes (the SURVEY 8(d) "
-                                 "model), but the 10 MB BVH + mesh are served by L2, the Infinity Cache and the "
-                                 "scalar cache, so frac can exceed 1; traffic_frac is the measured HBM fraction",
-                         "build": build_info},
+            "roofline": roofline,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(scene, rd)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
+            if cpu.get("value"):
+                out["gpu_over_cpu"] = round(value / cpu["value"], 1)
+            if cpu.get("socket0_linear_estimate"):
+                out["gpu_over_cpu_socket0_estimate"] = round(value / cpu["socket0_linear_estimate"], 1)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

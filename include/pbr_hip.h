@@ -232,6 +232,27 @@ const char* pbr_hip_last_error(const pbr_hip_ctx* ctx);
  * a safety bound (see above). */
 int pbr_hip_sync(pbr_hip_ctx* ctx);
 
+/* ---- per-kernel profile (measurement; no reference counterpart) ----
+ * While profiling is on, every kernel launch of a render is bracketed by a HIP event pair on the
+ * stream it runs on, and each kernel family counts the work units it processed.  `bytes` is the
+ * family's ALGORITHMIC HBM traffic: the compulsory queue / per-sample record / output bytes of the
+ * wavefront design per counted unit — BVH, mesh and texture fetches, which the
+ * caches serve, are not counted. */
+typedef struct pbr_kernel_profile {
+    char name[40];              /* kernel family, e.g. "k_wf_shade" (rocprof adds template args) */
+    int launches;
+    double ms;                  /* summed HIP-event durations of the family's launches */
+    uint64_t units;             /* work units: samples (camera), queued rays, pixels (finish) */
+    uint64_t bytes;             /* algorithmic HBM bytes */
+    uint64_t counts[8];         /* raw counters: [0] units, [1..4] pushes / rays that got through */
+} pbr_kernel_profile;
+/* on = 1: start a measurement window of event timings; on = 2: timings and work counters (the
+ * counters add one small counting launch after each queue kernel); 0: stop.  Either resets. */
+int pbr_hip_set_profiling(pbr_hip_ctx* ctx, int on);
+/* Waits for the context's work, returns the window's per-family profile (n = families seen; at most
+ * `max` written) and starts a new window. */
+int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int* n);
+
 /* ---- introspection used by the parity tests (no reference counterpart) ---- */
 /* Flattened BVH after upload: 32-B LinearBVHNode records (BVHAccel.cpp:46-55) and the ordered
  * primitive ids (position in the `prims` vector).  Pass NULL buffers to query counts. */

@@ -86,6 +86,20 @@ class HipRenderer:
                                             C.byref(st) if st is not None else None), "render")
         return st
 
+    def set_profiling(self, on: bool = True):
+        """Start (on) or stop a per-kernel measurement window (pbr_hip_set_profiling)."""
+        self._check(self.lib.pbr_hip_set_profiling(self.ctx, int(on)), "set_profiling")
+
+    def get_profile(self) -> dict:
+        """Per kernel family of the window: launches, summed HIP-event ms, work units, algorithmic
+        HBM bytes and raw counters (pbr_hip_get_profile); starts a new window."""
+        arr = (capi.KernelProfile * 32)()
+        n = C.c_int()
+        self._check(self.lib.pbr_hip_get_profile(self.ctx, arr, 32, C.byref(n)), "get_profile")
+        return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].ms, "units": int(arr[i].units),
+                                       "bytes": int(arr[i].bytes), "counts": [int(c) for c in arr[i].counts]}
+                for i in range(min(n.value, 32))}
+
     def get_bvh(self):
         nn, npr = C.c_int(), C.c_int()
         self._check(self.lib.pbr_hip_get_bvh(self.ctx, None, C.byref(nn), None, C.byref(npr)), "get_bvh")
@@ -123,7 +137,8 @@ TILE = 32
 
 
 def tile_grid(width, height, tile=TILE):
-    """64×64 pixel tiles in row-major order."""
+    """TILE×TILE (32×32) pixel tiles in row-major order (SURVEY §8(e) suggests 64×64; 32×32 measured
+    better, see the TILE comment)."""
     return [(x, y, min(x + tile, width), min(y + tile, height))
             for y in range(0, height, tile) for x in range(0, width, tile)]
 

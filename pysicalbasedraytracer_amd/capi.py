@@ -163,6 +163,17 @@ class RenderStats(C.Structure):
     ]
 
 
+class KernelProfile(C.Structure):
+    _fields_ = [
+        ("name", C.c_char * 40),
+        ("launches", C.c_int),
+        ("ms", C.c_double),
+        ("units", C.c_uint64),
+        ("bytes", C.c_uint64),
+        ("counts", C.c_uint64 * 8),
+    ]
+
+
 # Every symbol include/pbr_hip.h declares, with its ctypes signature.
 EXPORTS = {
     "pbr_hip_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -182,6 +193,8 @@ EXPORTS = {
     "pbr_hip_abi_version": (C.c_int, []),
     "pbr_hip_build_info": (C.c_char_p, []),
     "pbr_hip_sobol_matrices": (C.c_int, [C.c_int, C.POINTER(C.c_uint32)]),
+    "pbr_hip_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "pbr_hip_get_profile": (C.c_int, [C.c_void_p, C.POINTER(KernelProfile), C.c_int, C.POINTER(C.c_int)]),
 }
 
 PACKAGE_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -190,7 +203,7 @@ LIB_PATH = os.path.join(PACKAGE_DIR, "libpbr_hip.so")
 _lib = None
 
 
-OPTIONAL_FOR_AB = ("pbr_hip_sync",)
+OPTIONAL_FOR_AB = ("pbr_hip_sync", "pbr_hip_set_profiling", "pbr_hip_get_profile")
 
 
 def load_library(path: str | None = None) -> C.CDLL:

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <memory>
 #include <string>
 #include <vector>
@@ -641,6 +642,22 @@ __global__ void k_intersect(DeviceScene S, const int32_t* primIds, int n, const 
     }
 }
 
+// Profiling: adds the sums of up to kProfFields segment-count arrays (kWfBlocks ints each) to the
+// counter row dst[0..]; one workgroup, launched after the kernel it counts (outside its events).
+struct ProfSums {
+    const int* seg[kProfFields];
+    unsigned long long* dst;
+};
+__global__ __launch_bounds__(256) void k_prof_count(ProfSums a) {
+    for (int k = 0; k < kProfFields; ++k) {
+        if (!a.seg[k]) continue;
+        unsigned long long v = 0;
+        for (int i = threadIdx.x; i < kWfBlocks; i += 256) v += (unsigned long long)a.seg[k][i];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(a.dst + k, v);
+    }
+}
+
 }  // namespace
 
 // ======================================================================== C-ABI
@@ -704,6 +721,14 @@ struct pbr_hip_ctx {
     hipEvent_t evShade[kWfLanes][kWfMaxDepth + 2] = {}, evShadow[kWfLanes][kWfMaxDepth + 2] = {};
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
+    // per-kernel profile (pbr_hip_set_profiling): a HIP event pair around every launch, on the
+    // launch's stream, and the work counters of each kernel family (device rows + host-known counts)
+    bool profOn = false, profCount = false;
+    struct ProfEv { int kind; hipEvent_t a, b; };
+    std::vector<ProfEv> profEv;
+    size_t profUsed = 0;
+    DevBuf dProf;
+    unsigned long long profHost[KP_COUNT][kProfFields] = {};
     DevBuf dGuard;                       // DeviceScene::guard (kGuard* bits of tripped safety bounds)
     int* guardHost = nullptr;            // pinned copy, refreshed at the end of frames that can trip one
 };
@@ -913,6 +938,43 @@ dim3 resident_grid(pbr_hip_ctx* ctx, const void* fn) {
     return dim3((unsigned)(perCU * cus));
 }
 
+// ---- per-kernel profiling helpers
+int prof_begin(pbr_hip_ctx* ctx, int kind, hipStream_t st, int* idx) {
+    if (ctx->profUsed == ctx->profEv.size()) {
+        pbr_hip_ctx::ProfEv e{kind, nullptr, nullptr};
+        HIP_TRY(hipEventCreate(&e.a));
+        HIP_TRY(hipEventCreate(&e.b));
+        ctx->profEv.push_back(e);
+    }
+    pbr_hip_ctx::ProfEv& e = ctx->profEv[ctx->profUsed];
+    e.kind = kind;
+    *idx = (int)ctx->profUsed++;
+    HIP_TRY(hipEventRecord(e.a, st));
+    return PBR_OK;
+}
+// counts the segmented queues a launch consumed / filled into row `kind` (fields in order; null = skip)
+int prof_sums(pbr_hip_ctx* ctx, hipStream_t st, int kind, std::initializer_list<const int*> segs) {
+    if (!ctx->profCount) return PBR_OK;
+    ProfSums a;
+    std::memset(&a, 0, sizeof(a));
+    int k = 0;
+    for (const int* p : segs) a.seg[k++] = p;
+    a.dst = (unsigned long long*)ctx->dProf.p + (size_t)kind * kProfFields;
+    hipLaunchKernelGGL(k_prof_count, dim3(1), dim3(256), 0, st, a);
+    return PBR_OK;
+}
+void prof_host(pbr_hip_ctx* ctx, int kind, int field, unsigned long long v) {
+    if (ctx->profCount) ctx->profHost[kind][field] += v;
+}
+// a launch (any statement list) bracketed by the profile events of `kind` on stream ST
+#define PROF_LAUNCH(KIND, ST, ...)                                                  \
+    do {                                                                            \
+        int pi_ = -1;                                                               \
+        if (ctx->profOn) { if (int rc_ = prof_begin(ctx, KIND, ST, &pi_)) return rc_; } \
+        __VA_ARGS__;                                                                \
+        if (pi_ >= 0) HIP_TRY(hipEventRecord(ctx->profEv[pi_].b, ST));              \
+    } while (0)
+
 // Wavefront Whitted: chunks of up to 2^25 samples on two lanes, per level shade → shadow → extend
 // (pbr_wavefront.h).
 int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
@@ -990,6 +1052,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         W.depthOf = (int*)B.wDepth.p;
         W.sampleIndex = (uint32_t*)B.wIndex.p;
         W.initRecords = ctx->host.anyNoMaterial ? 1 : 0;
+        W.prof = ctx->profCount ? (unsigned long long*)ctx->dProf.p : nullptr;
         // Halton dims one sample reaches: 5 camera + per level 2 per light + 2 (SpecularReflect)
         W.P.smp.ldsDims = std::min(kLdsDims, 5 + (2 * lightsPerShade + 2) * levels + 2);
         W.cap = (int)cap;
@@ -1020,8 +1083,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
         W.cur = queue(l, 0);
-        if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
-        else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
+        PROF_LAUNCH(KP_WF_CAMERA, st,
+            if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
+            else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, st, W));
+        prof_host(ctx, KP_WF_CAMERA, 0, (unsigned long long)W.nSamples);
         const hipStream_t sst = shadowOverlap ? ctx->shadowStream[l] : st;
         WfBufs& B = ctx->wb[l];
         for (int level = 0; level < maxLevels; ++level) {
@@ -1036,6 +1101,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 if (level >= 2) HIP_TRY(hipStreamWaitEvent(st, ctx->evShadow[l][level - 2], 0));
             }
             const int l0 = level == 0 ? 1 : 0;
+            PROF_LAUNCH(KP_WF_SHADE, st,
             if (ml) {
                 if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
                 else if (simple) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
@@ -1044,25 +1110,34 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             } else if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
             else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, st, W, l0);
-            else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, st, W, l0);
+            else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, st, W, l0));
+            if (l0) prof_host(ctx, KP_WF_SHADE, 0, (unsigned long long)W.nSamples);
+            if (int rc = prof_sums(ctx, st, KP_WF_SHADE, {l0 ? nullptr : W.cur.segCount, W.shadowSeg, nullptr, nullptr,
+                                                          W.next.segCount, l0 ? nullptr : W.cur.segCount})) return rc;
             if (shadowOverlap) {
                 HIP_TRY(hipEventRecord(ctx->evShade[l][level], st));
                 HIP_TRY(hipStreamWaitEvent(sst, ctx->evShade[l][level], 0));
             }
-            if (ml) hipLaunchKernelGGL(k_wf_shadow_ml<kShortStack>, gShadowML, blk, 0, sst, W);
-            else if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, sst, W);
-            else hipLaunchKernelGGL(k_wf_shadow<0>, gShadow, blk, 0, sst, W);
+            PROF_LAUNCH(KP_WF_SHADOW, sst,
+                if (ml) hipLaunchKernelGGL(k_wf_shadow_ml<kShortStack>, gShadowML, blk, 0, sst, W);
+                else if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, sst, W);
+                else hipLaunchKernelGGL(k_wf_shadow<0>, gShadow, blk, 0, sst, W));
+            if (int rc = prof_sums(ctx, sst, KP_WF_SHADOW, {W.shadowSeg})) return rc;
             if (shadowOverlap) HIP_TRY(hipEventRecord(ctx->evShadow[l][level], sst));
             if (level + 1 == maxLevels) break;
             cur ^= 1;
             W.cur = queue(l, cur);
-            if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W);
-            else hipLaunchKernelGGL(k_wf_extend<0>, gExtend, blk, 0, st, W);
+            PROF_LAUNCH(KP_WF_EXTEND, st,
+                if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W);
+                else hipLaunchKernelGGL(k_wf_extend<0>, gExtend, blk, 0, st, W));
+            if (int rc = prof_sums(ctx, st, KP_WF_EXTEND, {W.cur.segCount})) return rc;
         }
         // the fold reads every level's records: after the last shadow launch (stream order on sst)
         if (shadowOverlap) HIP_TRY(hipStreamWaitEvent(st, ctx->evShadow[l][maxLevels - 1], 0));
         const int pb = finish_pixels(spp);
-        hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + pb - 1) / pb), blk, 0, st, W);
+        PROF_LAUNCH(KP_WF_FINISH, st, hipLaunchKernelGGL(k_wf_finish<0>, dim3((W.chunkPix + pb - 1) / pb), blk, 0, st, W));
+        prof_host(ctx, KP_WF_FINISH, 0, (unsigned long long)W.chunkPix);
+        prof_host(ctx, KP_WF_FINISH, 1, (unsigned long long)W.nSamples);
     }
     HIP_TRY(hipGetLastError());
     return wf_join(ctx, s, ch.lanes);
@@ -1113,6 +1188,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
             V.dLiA = (float4*)B.rLiA.p; V.dTr = (float4*)B.rTr.p; V.dWA = (float*)B.rWA.p;
         }
         W.P = P;
+        W.prof = ctx->profCount ? (unsigned long long*)ctx->dProf.p : nullptr;
         W.so = (float4*)B.wsO.p; W.sd = (float4*)B.wsD.p; W.sid = (int*)B.wsId.p;
         W.shadowSeg = cnt + 2 * kWfBlocks;
         W.segCap = ch.segCap;
@@ -1163,28 +1239,41 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
         W.cur = queue(l, 0);
-        hipLaunchKernelGGL(k_wfp_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, X);
+        PROF_LAUNCH(KP_WFP_CAMERA, st, hipLaunchKernelGGL(k_wfp_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, X));
+        prof_host(ctx, KP_WFP_CAMERA, 0, (unsigned long long)W.nSamples);
         for (int level = 0;; ++level) {   // ends below: at maxLevels, or when no continuation is queued
             W.cur = queue(l, cur);
             W.next = queue(l, cur ^ 1);
             const int l0 = level == 0 ? 1 : 0;
+            const int kShade = vol ? KP_WFV_SHADE : KP_WFP_SHADE;
             if (vol) {
-                if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0);
-                else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, st, V, l0);
-                else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0);
-                else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0);
-                hipLaunchKernelGGL(k_wfv_tr<kShortStack>, gShadow, blk, 0, st, V);
-                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, st, X);
-                hipLaunchKernelGGL(k_wfv_resolve, gResolve, blk, 0, st, V);
+                PROF_LAUNCH(KP_WFV_SHADE, st,
+                    if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0);
+                    else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, st, V, l0);
+                    else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0);
+                    else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0));
             } else {
-                if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
-                else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0);
-                else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, st, X, l0);
-                else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, st, X, l0);
-                hipLaunchKernelGGL(k_wfp_shadow<kShortStack>, gShadow, blk, 0, st, X);
-                hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, st, X);
-                hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, st, X);
+                PROF_LAUNCH(KP_WFP_SHADE, st,
+                    if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
+                    else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0);
+                    else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, st, X, l0);
+                    else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, st, X, l0));
             }
+            if (l0) prof_host(ctx, kShade, 0, (unsigned long long)W.nSamples);
+            if (int rc = prof_sums(ctx, st, kShade, {l0 ? nullptr : W.cur.segCount, vol ? V.trSeg : W.shadowSeg, X.probeSeg,
+                                                     X.directSeg, W.next.segCount, l0 ? nullptr : W.cur.segCount})) return rc;
+            if (vol) {
+                PROF_LAUNCH(KP_WFV_TR, st, hipLaunchKernelGGL(k_wfv_tr<kShortStack>, gShadow, blk, 0, st, V));
+                if (int rc = prof_sums(ctx, st, KP_WFV_TR, {V.trSeg})) return rc;
+            } else {
+                PROF_LAUNCH(KP_WFP_SHADOW, st, hipLaunchKernelGGL(k_wfp_shadow<kShortStack>, gShadow, blk, 0, st, X));
+                if (int rc = prof_sums(ctx, st, KP_WFP_SHADOW, {W.shadowSeg})) return rc;
+            }
+            PROF_LAUNCH(KP_WFP_PROBE, st, hipLaunchKernelGGL(k_wfp_probe<kShortStack>, gProbe, blk, 0, st, X));
+            if (int rc = prof_sums(ctx, st, KP_WFP_PROBE, {X.probeSeg})) return rc;
+            if (vol) PROF_LAUNCH(KP_WFV_RESOLVE, st, hipLaunchKernelGGL(k_wfv_resolve, gResolve, blk, 0, st, V));
+            else PROF_LAUNCH(KP_WFP_RESOLVE, st, hipLaunchKernelGGL(k_wfp_resolve, gResolve, blk, 0, st, X));
+            if (int rc = prof_sums(ctx, st, vol ? KP_WFV_RESOLVE : KP_WFP_RESOLVE, {X.directSeg})) return rc;
             if (level + 1 >= maxLevels) {
                 if (!ctx->host.anyNoMaterial) break;
                 HIP_TRY(hipMemcpyAsync(segHost.data(), W.next.segCount, kWfBlocks * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1197,10 +1286,13 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
             }
             cur ^= 1;
             W.cur = queue(l, cur);
-            hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W);
+            PROF_LAUNCH(KP_WF_EXTEND, st, hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W));
+            if (int rc = prof_sums(ctx, st, KP_WF_EXTEND, {W.cur.segCount})) return rc;
         }
         const int pb = finish_pixels(spp);
-        hipLaunchKernelGGL(k_wfp_finish, dim3((W.chunkPix + pb - 1) / pb), blk, 0, st, X);
+        PROF_LAUNCH(KP_WFP_FINISH, st, hipLaunchKernelGGL(k_wfp_finish, dim3((W.chunkPix + pb - 1) / pb), blk, 0, st, X));
+        prof_host(ctx, KP_WFP_FINISH, 0, (unsigned long long)W.chunkPix);
+        prof_host(ctx, KP_WFP_FINISH, 1, (unsigned long long)W.nSamples);
     }
     HIP_TRY(hipGetLastError());
     return wf_join(ctx, s, ch.lanes);
@@ -1472,10 +1564,15 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         } else if (wavefrontPath) {
             int rc = render_wavefront_path(ctx, P, s, d->integrator == PBR_INTEGRATOR_VOLPATH);
             if (rc) return rc;
-        } else switch (d->integrator) {
-        case PBR_INTEGRATOR_WHITTED: PBR_LAUNCH(PBR_INTEGRATOR_WHITTED) break;
-        case PBR_INTEGRATOR_PATH: PBR_LAUNCH(PBR_INTEGRATOR_PATH) break;
-        default: PBR_LAUNCH(PBR_INTEGRATOR_VOLPATH) break;
+        } else {
+            PROF_LAUNCH(KP_MEGA, s,
+                switch (d->integrator) {
+                case PBR_INTEGRATOR_WHITTED: PBR_LAUNCH(PBR_INTEGRATOR_WHITTED) break;
+                case PBR_INTEGRATOR_PATH: PBR_LAUNCH(PBR_INTEGRATOR_PATH) break;
+                default: PBR_LAUNCH(PBR_INTEGRATOR_VOLPATH) break;
+                });
+            prof_host(ctx, KP_MEGA, 0, (unsigned long long)npx * (unsigned long long)spp);
+            prof_host(ctx, KP_MEGA, 1, (unsigned long long)npx);
         }
 #undef PBR_LAUNCH
         HIP_TRY(hipGetLastError());
@@ -1511,6 +1608,92 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         stats->shading_events = hs[3];
         stats->n_launches = blocks > 0 ? 1 : 0;
     }
+    return PBR_OK;
+}
+
+int pbr_hip_set_profiling(pbr_hip_ctx* ctx, int on) {
+    if (!ctx) return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    ctx->profOn = on != 0;
+    ctx->profCount = on >= 2;
+    ctx->profUsed = 0;
+    std::memset(ctx->profHost, 0, sizeof(ctx->profHost));
+    if (ctx->profOn) {
+        const size_t bytes = (size_t)KP_COUNT * kProfFields * sizeof(unsigned long long);
+        HIP_TRY(ctx->dProf.ensure(bytes));
+        HIP_TRY(hipMemset(ctx->dProf.p, 0, bytes));
+    }
+    return PBR_OK;
+}
+
+int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int* n) {
+    if (!ctx || !n || (max > 0 && !out)) return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    static const char* kNames[KP_COUNT] = {
+        "k_wf_camera_extend", "k_wf_shade", "k_wf_shadow", "k_wf_extend", "k_wf_finish",
+        "k_wfp_camera_extend", "k_wfp_shade", "k_wfp_shadow", "k_wfp_probe", "k_wfp_resolve", "k_wfp_finish",
+        "k_wfv_shade", "k_wfv_tr", "k_wfv_resolve", "k_render"};
+    unsigned long long c[KP_COUNT][kProfFields];
+    std::memset(c, 0, sizeof(c));
+    if (ctx->profOn) HIP_TRY(hipMemcpy(c, ctx->dProf.p, sizeof(c), hipMemcpyDeviceToHost));
+    for (int k = 0; k < KP_COUNT; ++k)
+        for (int f = 0; f < kProfFields; ++f) c[k][f] += ctx->profHost[k][f];
+    int launches[KP_COUNT] = {};
+    double ms[KP_COUNT] = {};
+    for (size_t i = 0; i < ctx->profUsed; ++i) {
+        float t = 0;
+        HIP_TRY(hipEventElapsedTime(&t, ctx->profEv[i].a, ctx->profEv[i].b));
+        ms[ctx->profEv[i].kind] += t;
+        launches[ctx->profEv[i].kind] += 1;
+    }
+    // Algorithmic HBM bytes of each family: the compulsory queue / record / output traffic of the
+    // wavefront design, per counted unit; BVH, mesh and texture reads are cacheable
+    // and not counted.  f[0] units, f[1..4] pushes (any-hit kernels: f[1] = rays that got through),
+    // f[5] units read from a segmented queue (+4 B id each).
+    auto bytes = [&](int k) -> unsigned long long {
+        const unsigned long long* f = c[k];
+        switch (k) {
+        case KP_WF_CAMERA: return 52 * f[0];                                   // o, d, hit, index
+        case KP_WF_SHADE: return 72 * f[0] + 4 * f[5] + 52 * f[1] + 52 * f[4]; // ray + index + recA + depth; shadow; next + recF/P
+        case KP_WF_SHADOW: return 52 * f[0] + 32 * f[1];                       // o, d, contribution, id; recA RMW
+        case KP_WF_EXTEND: return 52 * f[0];                                   // o, d read; tMax, hit written
+        case KP_WF_FINISH: return 16 * f[0] + 4 * f[1] + 16 * c[KP_WF_SHADE][0] + 20 * c[KP_WF_SHADE][4];
+        case KP_WFP_CAMERA: return 84 * f[0];                                  // + L, beta
+        case KP_WFP_SHADE: return 116 * f[0] + 4 * f[5] + 36 * f[1] + 36 * f[2] + 60 * f[3] + 36 * f[4];
+        case KP_WFP_SHADOW: return 36 * f[0] + 8 * f[1];
+        case KP_WFP_PROBE: return 56 * f[0];
+        case KP_WFP_RESOLVE: return 108 * f[0];
+        case KP_WFP_FINISH: return 16 * f[0] + 16 * f[1];
+        case KP_WFV_SHADE: return 116 * f[0] + 4 * f[5] + 84 * f[1] + 36 * f[2] + 80 * f[3] + 36 * f[4];
+        case KP_WFV_TR: return 100 * f[0];
+        case KP_WFV_RESOLVE: return 144 * f[0];
+        default: return 16 * f[1];                                             // megakernel: the film output
+        }
+    };
+    int m = 0;
+    for (int k = 0; k < KP_COUNT; ++k) {
+        if (!launches[k]) continue;
+        if (m < max) {
+            pbr_kernel_profile& o = out[m];
+            std::memset(&o, 0, sizeof(o));
+            std::snprintf(o.name, sizeof(o.name), "%s", kNames[k]);
+            o.launches = launches[k];
+            o.ms = ms[k];
+            o.units = c[k][0];
+            o.bytes = bytes(k);
+            for (int f = 0; f < kProfFields && f < 8; ++f) o.counts[f] = c[k][f];
+        }
+        ++m;
+    }
+    *n = m;
+    // reset for the next measurement window
+    ctx->profUsed = 0;
+    std::memset(ctx->profHost, 0, sizeof(ctx->profHost));
+    if (ctx->profOn) HIP_TRY(hipMemset(ctx->dProf.p, 0, sizeof(c)));
     return PBR_OK;
 }
 

@@ -24,6 +24,22 @@
 constexpr int kWfMaxDepth = 16;   // Whitted levels of the wavefront schedule (deeper: the megakernel)
 constexpr int kWfBlocks = 2048;   // workgroups of the queue kernels = segments of a queue
 
+// Per-kernel profile (pbr_hip_set_profiling): kernel families and their work counters
+// [kind * kProfFields + field].  Field 0 counts the units a family processed, fields 1..4 the
+// entries it pushed (or, for the any-hit kernels, the rays that got through), field 5 the units
+// read from a segmented queue (beyond level 0: one more 4-B id each).
+enum ProfKind {
+    KP_WF_CAMERA, KP_WF_SHADE, KP_WF_SHADOW, KP_WF_EXTEND, KP_WF_FINISH,
+    KP_WFP_CAMERA, KP_WFP_SHADE, KP_WFP_SHADOW, KP_WFP_PROBE, KP_WFP_RESOLVE, KP_WFP_FINISH,
+    KP_WFV_SHADE, KP_WFV_TR, KP_WFV_RESOLVE, KP_MEGA, KP_COUNT
+};
+constexpr int kProfFields = 8;
+// wave-aggregated count of the lanes for which pred holds (every active lane must call it)
+__device__ __forceinline__ void prof_count(unsigned long long* ctr, bool pred) {
+    const unsigned long long m = __ballot(pred), act = __ballot(1);
+    if (m && (int)__lane_id() == __ffsll((long long)act) - 1) atomicAdd(ctr, (unsigned long long)__popcll(m));
+}
+
 struct WfQueue {
     float4* o;      // origin.xyz, tMax
     float4* d;      // dir.xyz, packed (dim | depth << 16) as int bits
@@ -54,6 +70,7 @@ struct WfParams {
     float4* recC;
     uint8_t* recV;
     int nLightsML;         // 0: the single-light schedule
+    unsigned long long* prof;   // profile counters (ProfKind rows) while profiling, else null
 };
 
 // LDS counter; the wave's lanes must be converged
@@ -312,7 +329,9 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
         Counters c;
-        if (!traverse<true, false, SHORT>(W.P.S, r, &h, &c)) {
+        const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
+        if (W.prof) prof_count(W.prof + KP_WF_SHADOW * kProfFields + 1, visible);
+        if (visible) {
             int id = W.sid[q];
             float4 cc = W.sc[q];
             size_t ri = (size_t)__float_as_int(d.w) * W.cap + id;
@@ -479,7 +498,9 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow_ml(WfParams W) 
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
         Counters c;
-        if (!traverse<true, false, SHORT>(W.P.S, r, &h, &c)) {
+        const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
+        if (W.prof) prof_count(W.prof + KP_WF_SHADOW * kProfFields + 1, visible);
+        if (visible) {
             const int code = __float_as_int(d.w);
             W.recV[((size_t)(code & 0xff) * W.nLightsML + (code >> 8)) * W.cap + W.sid[q]] = 1;
         }

@@ -276,7 +276,9 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_shadow(WfpParams X) {
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
         Counters c;
-        if (!traverse<true, false, SHORT>(W.P.S, r, &h, &c)) {
+        const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
+        if (W.prof) prof_count(W.prof + KP_WFP_SHADOW * kProfFields + 1, visible);
+        if (visible) {
             const int id = W.sid[q];
             X.dFlags[id] |= kWfpVisible;   // the only writer of this sample's record in this launch
         }

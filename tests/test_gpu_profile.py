@@ -1,0 +1,77 @@
+"""The per-kernel profile (pbr_hip_set_profiling / pbr_hip_get_profile) that bench.py's roofline
+reads: launch counts, units and pushes must agree with each other and with the frame's geometry, and
+profiling must not change the image."""
+import numpy as np
+import pytest
+
+from pysicalbasedraytracer_amd import HipRenderer, scenes
+
+
+@pytest.fixture(scope="module")
+def hip():
+    r = HipRenderer(0)
+    yield r
+    r.close()
+
+
+def _c2_small():
+    return scenes.config_c2(192, 108, 16)
+
+
+@pytest.mark.gpu
+def test_whitted_profile_counts_are_consistent(hip, monkeypatch):
+    monkeypatch.setenv("PBR_CHUNK_LOG2", "16")   # several chunks over both lanes
+    s, rd = _c2_small()
+    hip.upload(s)
+    ref, ref8, _ = hip.render(rd)
+    hip.set_profiling(2)
+    g, g8, _ = hip.render(rd)
+    prof = hip.get_profile()
+    hip.set_profiling(0)
+    assert np.array_equal(g, ref) and np.array_equal(g8, ref8)   # profiling changes nothing
+    n = 192 * 108 * 16
+    cam, shade, shadow, extend, fin = (prof[k] for k in ("k_wf_camera_extend", "k_wf_shade", "k_wf_shadow",
+                                                         "k_wf_extend", "k_wf_finish"))
+    assert cam["units"] == n and fin["units"] == 192 * 108 and fin["counts"][1] == n
+    assert cam["launches"] == fin["launches"] > 1
+    assert shade["launches"] == cam["launches"] * rd.max_depth == shadow["launches"]
+    # shade's level-0 input is every sample; deeper levels read what the previous level pushed
+    assert shade["units"] == n + extend["units"]
+    assert shadow["units"] == shade["counts"][1] and 0 < shadow["counts"][1] <= shadow["units"]
+    assert extend["units"] == shade["counts"][4] == shade["counts"][5]
+    for v in prof.values():
+        assert v["ms"] > 0 and v["bytes"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c3", "c5"])
+def test_path_profile_counts_are_consistent(hip, cfg):
+    s, rd = getattr(scenes, f"config_{cfg}")(64, 48, 16)
+    hip.upload(s)
+    hip.set_profiling(2)
+    hip.render(rd)
+    prof = hip.get_profile()
+    hip.set_profiling(0)
+    n = 64 * 48 * 16
+    shade = prof["k_wfv_shade" if cfg == "c5" else "k_wfp_shade"]
+    assert prof["k_wfp_camera_extend"]["units"] == n
+    assert shade["units"] == n + prof["k_wf_extend"]["units"]
+    anyhit = prof["k_wfv_tr"] if cfg == "c5" else prof["k_wfp_shadow"]
+    assert anyhit["units"] == shade["counts"][1]
+    assert prof["k_wfp_probe"]["units"] == shade["counts"][2]
+    assert prof["k_wfv_resolve" if cfg == "c5" else "k_wfp_resolve"]["units"] == shade["counts"][3]
+    assert prof["k_wfp_finish"]["units"] == 64 * 48
+
+
+@pytest.mark.gpu
+def test_profile_timing_only_window(hip):
+    s, rd = _c2_small()
+    hip.upload(s)
+    hip.set_profiling(1)
+    hip.render(rd)
+    hip.render(rd)
+    prof = hip.get_profile()
+    hip.set_profiling(0)
+    assert prof["k_wf_camera_extend"]["launches"] == 2
+    assert prof["k_wf_camera_extend"]["units"] == 0   # timings only: no counting launches
+    assert all(v["ms"] > 0 for v in prof.values())

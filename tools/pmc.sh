@@ -1,11 +1,12 @@
 #!/bin/bash
-# PMC passes over one C2 frame (separate runs: FETCH_SIZE and WRITE_SIZE do not fit one pass).
+# PMC passes over one frame of $CONFIG (default C2) (separate runs: FETCH_SIZE and WRITE_SIZE do not fit one pass).
 # Kernel-trace + counters only (no sys/runtime trace domains with --pmc).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT=$ROOT/gpurun_out/pmc
+CONFIG="${CONFIG:-C2}"
+OUT="${PMC_OUT:-$ROOT/gpurun_out/pmc}"
 mkdir -p "$OUT"
-CMD="python3 $ROOT/tools/tune_wavefront.py --steps 1 ${TUNE_VARIANT:-}"
+CMD="python3 $ROOT/tools/tune_wavefront.py --config $CONFIG --steps 1 ${TUNE_VARIANT:-}"
 cd /tmp && export TMPDIR=/tmp
 run() {   # name counters...
   local name=$1; shift

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 output (kernel stats + the PMC passes of tools/pmc.sh) into a markdown table.
 
-    python tools/summarize_prof.py gpurun_out/prof gpurun_out/pmc > profiles/rNN_summary.md
+    python tools/summarize_prof.py gpurun_out/prof gpurun_out/pmc [--json=traffic.json] > profiles/rNN_summary.md
+    (first argument "-": PMC tables only)
 
 FETCH_SIZE is doubled (gfx950 reports half the bytes of a 16-B/lane streaming read,
 MI355X_MICROARCH.md § HBM); WRITE_SIZE is taken as is.  Both are per frame (the PMC runs render
@@ -23,13 +24,15 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--json=")]
     js = [a[7:] for a in sys.argv[1:] if a.startswith("--json=")]
     prof, pmc = args[0], args[1] if len(args) > 1 else None
-    rows = list(csv.DictReader(open(os.path.join(prof, "run_kernel_stats.csv"))))
-    print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
-    print("| kernel | calls | total ms | avg µs | % |")
-    print("|---|---:|---:|---:|---:|")
-    for r in rows:
-        print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
-              f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
+    stats = os.path.join(prof, "run_kernel_stats.csv")
+    if prof != "-" and os.path.exists(stats):
+        rows = list(csv.DictReader(open(stats)))
+        print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
+        print("| kernel | calls | total ms | avg µs | % |")
+        print("|---|---:|---:|---:|---:|")
+        for r in rows:
+            print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
+                  f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
     if not pmc:
         return
     frames = 2.0
