@@ -250,21 +250,111 @@ __device__ __forceinline__ float4 as_f4(ScalarF4 v) { return make_float4(v.x, v.
 #define PBR_QUAD_TRAVERSAL 1
 #endif
 constexpr bool kQuadTraversal = PBR_QUAD_TRAVERSAL != 0;
+// Short stack without scratch (PBR_STACK_BACKTRACK, default): the LDS entries form a ring; a push
+// into a full ring overwrites the oldest entry and marks the traversal "dropped".  When the ring
+// runs empty after a drop, the next node is found by walking parent links instead (quad nodes keep
+// `parent << 2 | slot` in word 29, leaves in S.leafParent): from the last reference entered, up to
+// its parent, re-deriving that node's slab tests and visit order (the same float operations, so the
+// same tEnter values) and taking the first slot after the one we came from that passes against the
+// current tMax — which is exactly what popping the dropped entry would have given (the ring held,
+// for every node on the current path, the passing slots after the path; a dropped one is re-tested
+// against a tMax that can only have shrunk, like the pop test).  Leaves are therefore tested in the
+// reference's order, bit for bit, with no scratch stack (the deeper entries of the 64-entry stack
+// used to spill to scratch: ≈ 19 B of HBM writes per camera ray on C2).  Closest hit keeps the
+// smallest tEnter of the overwritten entries: once it is >= tMax every one of them would fail its
+// pop test, and the walk is skipped.  Bit-identical frames with 1-, 2- and 6-entry rings, but
+// slower than spilling to scratch, which the caches absorb: C2 18.5 → 19.6 ms, C3 331 → 382 ms,
+// C5 1752 → 1951 ms (profiles/r2_stackless_ab.log) — a parent walk re-fetches and re-tests a
+// node where a pop reads 8 B — so it is off by default.
+#ifndef PBR_STACK_BACKTRACK
+#define PBR_STACK_BACKTRACK 0
+#endif
+constexpr bool kBacktrack = PBR_STACK_BACKTRACK != 0;
+
+struct QuadSlots {   // one quad node's four slots in visit order
+    float t[4];
+    int ref[4];
+    bool k[4];       // slab passes (box valid)
+    bool sA, sB, sN; // the swaps that produced the order (for the parent-link slot → position map)
+};
+template <bool ANY>
+__device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const Ray& r, f3 inv, bool n0, bool n1, bool n2,
+                                           QuadSlots* q) {
+    float4 LX, LY, LZ, HX, HY, HZ, R;
+    int meta;
+    // Coherent waves (a pixel's samples share a wave) often have every active lane at the
+    // same node: then it is fetched once through the scalar cache.
+    const int ucur = __builtin_amdgcn_readfirstlane(cur);
+    if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
+        const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
+        LX = as_f4(w[0]); LY = as_f4(w[1]); LZ = as_f4(w[2]); HX = as_f4(w[3]); HY = as_f4(w[4]);
+        HZ = as_f4(w[5]); R = as_f4(w[6]);
+        meta = __float_as_int(w[7].x);
+    } else {
+        const float4* w = S.quad + 8 * (size_t)cur;
+        LX = w[0]; LY = w[1]; LZ = w[2]; HX = w[3]; HY = w[4]; HZ = w[5]; R = w[6];
+        meta = __float_as_int(w[7].x);
+    }
+    float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    bool k0 = node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t0) & ((meta >> 8) & 1);
+    bool k1 = node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t1) & ((meta >> 9) & 1);
+    bool k2 = node_slab(mk(LX.z, LY.z, LZ.z), mk(HX.z, HY.z, HZ.z), r, inv, n0, n1, n2, &t2) & ((meta >> 10) & 1);
+    bool k3 = node_slab(mk(LX.w, LY.w, LZ.w), mk(HX.w, HY.w, HZ.w), r, inv, n0, n1, n2, &t3) & ((meta >> 11) & 1);
+    int r0 = __float_as_int(R.x), r1 = __float_as_int(R.y), r2 = __float_as_int(R.z), r3 = __float_as_int(R.w);
+    auto swp = [](bool c, auto& a, auto& b) { auto x = c ? b : a; b = c ? a : b; a = x; };
+    auto neg = [&](int axis) { return axis == 0 ? n0 : (axis == 1 ? n1 : n2); };
+    q->sA = q->sB = q->sN = false;
+    // Any-hit (IntersectP) keeps the slots in build order instead.  Its answer does not
+    // depend on the visit order: ray.tMax never shrinks, so every box test and the set of
+    // reachable leaves are order-free, and the result is whether any primitive there is
+    // hit.  Build order reaches occluders of C2's shadow rays sooner (C2 19.95 → 18.55 ms).
+    if constexpr (!ANY) {
+        const bool sA = neg((meta >> 2) & 3), sB = neg((meta >> 4) & 3), sN = neg(meta & 3);
+        swp(sA, k0, k1); swp(sA, t0, t1); swp(sA, r0, r1);
+        swp(sB, k2, k3); swp(sB, t2, t3); swp(sB, r2, r3);
+        swp(sN, k0, k2); swp(sN, t0, t2); swp(sN, r0, r2);
+        swp(sN, k1, k3); swp(sN, t1, t3); swp(sN, r1, r3);
+        q->sA = sA; q->sB = sB; q->sN = sN;
+    }
+    q->t[0] = t0; q->t[1] = t1; q->t[2] = t2; q->t[3] = t3;
+    q->ref[0] = r0; q->ref[1] = r1; q->ref[2] = r2; q->ref[3] = r3;
+    q->k[0] = k0; q->k[1] = k1; q->k[2] = k2; q->k[3] = k3;
+}
+
 template <bool ANY, int SHORT>
 __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, bool n0, bool n1, bool n2) {
-    int stackRef[64 - SHORT];
-    float stackT[64 - SHORT];
+    constexpr bool BT = kBacktrack && SHORT > 0;
+    constexpr int PRIV = BT ? 1 : 64 - SHORT;
+    int stackRef[PRIV];
+    float stackT[PRIV];
     int* lref = nullptr;
     float* lt = nullptr;
     if constexpr (SHORT > 0) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
+    int sp = 0;             // entries held (stack depth; with BT at most SHORT)
+    int top = 0;            // BT: ring position of the next push
+    bool dropped = false;   // BT: an entry was overwritten
+    float dropT = __builtin_inff();   // BT, closest hit: smallest entry distance of an overwritten entry
     // any-hit: ray.tMax never shrinks, so a pushed slot (tEnter < tMax) always passes its re-test
     // on the way out and only the reference is kept
-    auto push = [&](int ref, float t, int sp) {
-        if (SHORT && sp < SHORT) { lref[sp * 256] = ref; if (!ANY) lt[sp * 256] = t; }
-        else { stackRef[sp - SHORT] = ref; if (!ANY) stackT[sp - SHORT] = t; }
+    auto push = [&](int ref, float t) {
+        if constexpr (BT) {
+            if (sp == SHORT) {   // overwriting the oldest entry
+                dropped = true;
+                if (!ANY) dropT = fminf(dropT, lt[top * 256]);
+            }
+            lref[top * 256] = ref;
+            if (!ANY) lt[top * 256] = t;
+            top = top + 1 == SHORT ? 0 : top + 1;
+            if (sp < SHORT) ++sp;
+        } else {
+            if (SHORT && sp < SHORT) { lref[sp * 256] = ref; if (!ANY) lt[sp * 256] = t; }
+            else { stackRef[sp - SHORT] = ref; if (!ANY) stackT[sp - SHORT] = t; }
+            ++sp;
+        }
     };
-    auto neg = [&](int axis) { return axis == 0 ? n0 : (axis == 1 ? n1 : n2); };
-    int cur = S.quadRootRef, sp = 0;
+    int cur = S.quadRootRef;
+    int last = cur;   // BT: the reference entered last (the subtree in progress)
+    int from = -1;    // BT: re-entering node `cur` from its slot `from` (parent-link walk), else -1
     bool found = false;
     while (true) {
         if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
@@ -294,62 +384,53 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
                 ++slot;
             }
         } else {
-            float4 LX, LY, LZ, HX, HY, HZ, R;
-            int meta;
-            // Coherent waves (a pixel's samples share a wave) often have every active lane at the
-            // same node: then it is fetched once through the scalar cache.
-            const int ucur = __builtin_amdgcn_readfirstlane(cur);
-            if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
-                const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
-                LX = as_f4(w[0]); LY = as_f4(w[1]); LZ = as_f4(w[2]); HX = as_f4(w[3]); HY = as_f4(w[4]);
-                HZ = as_f4(w[5]); R = as_f4(w[6]);
-                meta = __float_as_int(w[7].x);
-            } else {
-                const float4* w = S.quad + 8 * (size_t)cur;
-                LX = w[0]; LY = w[1]; LZ = w[2]; HX = w[3]; HY = w[4]; HZ = w[5]; R = w[6];
-                meta = __float_as_int(w[7].x);
-            }
-            float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-            bool k0 = node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t0) & ((meta >> 8) & 1);
-            bool k1 = node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t1) & ((meta >> 9) & 1);
-            bool k2 = node_slab(mk(LX.z, LY.z, LZ.z), mk(HX.z, HY.z, HZ.z), r, inv, n0, n1, n2, &t2) & ((meta >> 10) & 1);
-            bool k3 = node_slab(mk(LX.w, LY.w, LZ.w), mk(HX.w, HY.w, HZ.w), r, inv, n0, n1, n2, &t3) & ((meta >> 11) & 1);
-            int r0 = __float_as_int(R.x), r1 = __float_as_int(R.y), r2 = __float_as_int(R.z), r3 = __float_as_int(R.w);
-            auto swp = [](bool c, auto& a, auto& b) { auto x = c ? b : a; b = c ? a : b; a = x; };
-            const bool sA = neg((meta >> 2) & 3), sB = neg((meta >> 4) & 3), sN = neg(meta & 3);
-            // Any-hit (IntersectP) keeps the slots in build order instead.  Its answer does not
-            // depend on the visit order: ray.tMax never shrinks, so every box test and the set of
-            // reachable leaves are order-free, and the result is whether any primitive there is
-            // hit.  Build order reaches occluders of C2's shadow rays sooner (C2 19.95 → 18.55 ms).
-            if constexpr (!ANY) {
-                swp(sA, k0, k1); swp(sA, t0, t1); swp(sA, r0, r1);
-                swp(sB, k2, k3); swp(sB, t2, t3); swp(sB, r2, r3);
-                swp(sN, k0, k2); swp(sN, t0, t2); swp(sN, r0, r2);
-                swp(sN, k1, k3); swp(sN, t1, t3); swp(sN, r1, r3);
+            QuadSlots q;
+            quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
+            // slots at or before the visit position of `from` are done (only on a parent-link walk)
+            int done = -1;
+            if (BT && from >= 0) {
+                const int rh = from >> 1, rl = from & 1;   // inverse of quad_slots' swaps
+                done = ((rh ^ (int)q.sN) << 1) | (rl ^ (int)(rh ? q.sB : q.sA));
             }
             const float tM = r.tMax;
-            const bool p0 = k0 && t0 < tM, p1 = k1 && t1 < tM, p2 = k2 && t2 < tM, p3 = k3 && t3 < tM;
+            const bool p0 = done < 0 && q.k[0] && q.t[0] < tM, p1 = done < 1 && q.k[1] && q.t[1] < tM,
+                       p2 = done < 2 && q.k[2] && q.t[2] < tM, p3 = done < 3 && q.k[3] && q.t[3] < tM;
+            from = -1;
             if (p0 | p1 | p2 | p3) {
-                if (sp > 64 - 3) break;   // never reached: SAH trees here stay < 30 binary levels
+                if (!BT && sp > 64 - 3) break;   // never reached: SAH trees here stay < 30 binary levels
                 const int first = p0 ? 0 : (p1 ? 1 : (p2 ? 2 : 3));
-                if (p3 && first < 3) push(r3, t3, sp++);
-                if (p2 && first < 2) push(r2, t2, sp++);
-                if (p1 && first < 1) push(r1, t1, sp++);
-                cur = first == 0 ? r0 : (first == 1 ? r1 : (first == 2 ? r2 : r3));
+                if (p3 && first < 3) push(q.ref[3], q.t[3]);
+                if (p2 && first < 2) push(q.ref[2], q.t[2]);
+                if (p1 && first < 1) push(q.ref[1], q.t[1]);
+                cur = first == 0 ? q.ref[0] : (first == 1 ? q.ref[1] : (first == 2 ? q.ref[2] : q.ref[3]));
+                last = cur;
                 continue;
             }
         }
         bool more = false;   // pop until an entry passes its box test against the current tMax
         while (sp > 0) {
             --sp;
+            int e = sp;
+            if constexpr (BT) { top = top == 0 ? SHORT - 1 : top - 1; e = top; }
             int rr;
             float tt;
-            if (ANY) { cur = (SHORT && sp < SHORT) ? lref[sp * 256] : stackRef[sp - SHORT]; more = true; break; }
-            if (SHORT && sp < SHORT) { rr = lref[sp * 256]; tt = lt[sp * 256]; }
-            else { rr = stackRef[sp - SHORT]; tt = stackT[sp - SHORT]; }
+            if (ANY) { cur = (SHORT && e < SHORT) ? lref[e * 256] : stackRef[e - SHORT]; more = true; break; }
+            if (SHORT && e < SHORT) { rr = lref[e * 256]; tt = lt[e * 256]; }
+            else { rr = stackRef[e - SHORT]; tt = stackT[e - SHORT]; }
             if (tt < r.tMax) { cur = rr; more = true; break; }
         }
+        // ring empty after a drop: re-enter the parent of `last` after the slot it came from — unless
+        // every overwritten entry would fail its pop test now (closest hit: tEnter >= tMax)
+        if (BT && !more && dropped && (ANY || dropT < r.tMax)) {
+            const int link = last < 0 ? S.leafParent[last & 0x7fffffff] : __float_as_int(S.quad[8 * (size_t)last + 7].y);
+            if (link >= 0) {
+                cur = link >> 2;
+                from = link & 3;
+                more = true;
+            }
+        }
         if (!more) break;
+        last = cur;
     }
     return found;
 }

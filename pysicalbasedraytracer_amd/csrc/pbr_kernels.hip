@@ -701,6 +701,7 @@ struct pbr_hip_ctx {
     HostScene host;
     HaltonTables halton;
     DevBuf dInfTex, dInfCF, dInfCC, dInfMF, dInfMC, dInfRec;
+    DevBuf dLeafParent;
     DevBuf dNodes, dWide, dQuad, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dSobol, dSobolHi, dSobolPix;  // active Sobol nibble tables (index bits 0-31, 32-51), pixel tables
@@ -775,6 +776,7 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     S.rootRef = h.rootRef;
     S.quad = (const float4*)ctx->dQuad.p;
     S.quadRootRef = h.quadRootRef;
+    S.leafParent = (const int*)ctx->dLeafParent.p;
     S.triVerts = (const float4*)ctx->dTri.p;
     S.guard = (int*)ctx->dGuard.p;
     S.primInfo = (const int4*)ctx->dInfo.p;
@@ -1396,6 +1398,7 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     HIP_TRY(ctx->dNodes.upload(h.nodes, ctx->stream));
     HIP_TRY(ctx->dWide.upload(h.wide, ctx->stream));
     HIP_TRY(ctx->dQuad.upload(h.quad, ctx->stream));
+    HIP_TRY(ctx->dLeafParent.upload(h.leafParent, ctx->stream));
     HIP_TRY(ctx->dTri.upload(h.triVerts, ctx->stream));
     HIP_TRY(ctx->dInfo.upload(h.primInfo, ctx->stream));
     HIP_TRY(ctx->dUV.upload(h.triUV, ctx->stream));

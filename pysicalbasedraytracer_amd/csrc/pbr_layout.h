@@ -74,6 +74,7 @@ struct DeviceScene {
     int rootRef;
     const float4* quad;            // 8 float4 per quad node (two binary levels, pbr_scene.cpp build_quad_nodes)
     int quadRootRef;
+    const int* leafParent;         // per leaf's first slot: parentQuad << 2 | raw slot (-1: root)
     const float4* triVerts;
     const int4* primInfo;
     const float2* triUV;

@@ -70,6 +70,7 @@ template <class Ref>
 void build_quad_nodes(HostScene* S, Ref&& binRef) {
     const std::vector<LinearBVHNode>& L = S->nodes;
     S->quad.clear();
+    S->leafParent.assign(std::max<size_t>(1, S->primIds.size()), -1);
     S->quadRootRef = binRef(0);
     if (L.empty() || L[0].nPrimitives > 0) return;
     std::vector<int32_t> qid(L.size(), -1);
@@ -117,6 +118,18 @@ void build_quad_nodes(HostScene* S, Ref&& binRef) {
         std::memcpy(&w[24], refs, 16);
         int32_t meta = (int32_t)L[i].axis | axes[0] << 2 | axes[1] << 4 | mask << 8;
         std::memcpy(&w[28], &meta, 4);
+        // parent links for the backtracking traversal (pbr_device.h traverse_quad): every slot's
+        // child knows (this node, slot); quad children in w[29], leaves in leafParent[first slot]
+        for (int s = 0; s < 4; ++s) {
+            if (!((mask >> s) & 1)) continue;
+            const int32_t link = qid[i] << 2 | s;
+            if (refs[s] < 0) S->leafParent[refs[s] & 0x7fffffff] = link;
+            else std::memcpy(&S->quad[(size_t)refs[s] * 32 + 29], &link, 4);
+        }
+    }
+    {
+        const int32_t none = -1;
+        std::memcpy(&S->quad[29], &none, 4);   // the root quad node (qid 0, preorder)
     }
     S->quadRootRef = qid[0];
 }
