@@ -6,6 +6,6 @@ mkdir -p gpurun_out
 for C in ${CONFIGS:-C2}; do
   REF=${REFDIR:-/tmp}/ref_$C.npy; rm -f $REF
   for L in $LIBS; do
-    timeout -k 10 300 python -u tools/tune_wavefront.py --config $C --steps ${STEPS:-5} --lib $L --ref-file $REF $VARIANTS || exit 1
+    timeout -k 10 300 python -u tools/tune_wavefront.py --config $C --steps ${STEPS:-5} --lib $L --ref-file $REF ${TUNE_ARGS:-} $VARIANTS || exit 1
   done
 done

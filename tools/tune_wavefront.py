@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--tile", type=int, default=32, help="tile edge of the --shard partition")
     ap.add_argument("--ref-file", default=None, help=".npy frame to compare against (written if absent), "
                                                      "so experimental builds can be checked against each other")
+    ap.add_argument("--profile", action="store_true", help="per-kernel-family ms per frame (HIP events)")
     ap.add_argument("variants", nargs="*", default=[""])
     a = ap.parse_args()
     if a.lib:
@@ -71,9 +72,18 @@ def main():
             if a.ref_file:
                 np.save(a.ref_file, out)
         m = float(np.median(ms))
+        kern = ""
+        if a.profile and hasattr(r.lib, "pbr_hip_set_profiling"):
+            r.set_profiling(1)
+            for _ in range(a.steps):
+                r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            prof = r.get_profile()
+            r.set_profiling(0)
+            kern = "  [" + ", ".join(f"{k.replace('k_', '')} {v['ms'] / a.steps:.2f}" for k, v in prof.items()) + "]"
         tag = f" shard {a.shard} tile {a.tile} ({npx} px)" if a.shard else ""
         print(f"{a.config}{tag} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  "
-              f"{npx * spp / m / 1e3:8.1f} Msamples/s  {same}", flush=True)
+              f"{npx * spp / m / 1e3:8.1f} Msamples/s  {same}{kern}", flush=True)
         for k, old in saved.items():
             if old is None:
                 os.environ.pop(k, None)
