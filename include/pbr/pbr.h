@@ -94,6 +94,36 @@ struct Bounds2f {
     Bounds2f(const Point2f& a, const Point2f& b) : pMin(a), pMax(b) {}
 };
 
+struct Bounds3f {   // Core/Geometry.h: an empty box is (+max, -max)
+    Point3f pMin, pMax;
+    Bounds3f();
+    Bounds3f(const Point3f& a, const Point3f& b) : pMin(a), pMax(b) {}
+};
+struct Vector2f {
+    float x = 0, y = 0;
+};
+class Medium;
+// Core/Geometry.h Ray: tMax is mutable (Intersect shortens it)
+struct Ray {
+    Ray() = default;
+    Ray(const Point3f& o, const Vector3f& d, float tMax = 3.40282347e+38f * 2.f, float time = 0.f,
+        const Medium* medium = nullptr)
+        : o(o), d(d), tMax(tMax), time(time), medium(medium) {}
+    Point3f operator()(float t) const { return Point3f(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t); }
+    Point3f o;
+    Vector3f d;
+    mutable float tMax = 3.40282347e+38f * 2.f;   // Infinity
+    float time = 0.f;
+    const Medium* medium = nullptr;
+};
+struct RayDifferential : Ray {   // the differentials are never read on the render path (F5)
+    using Ray::Ray;
+    RayDifferential() = default;
+    RayDifferential(const Ray& r) : Ray(r) {}
+    void ScaleDifferentials(float) {}
+    bool hasDifferentials = false;
+};
+
 // ---------------------------------------------------------------------------- Core/Spectrum.h
 class Spectrum {   // RGBSpectrum
   public:
@@ -337,57 +367,150 @@ class InfiniteAreaLight : public Light {   // Light/InfiniteAreaLight.h
     std::vector<float> data;
 };
 
+// ---------------------------------------------------------------------------- Core/Interaction.h
+class Primitive;
+enum class TransportMode { Radiance, Importance };   // Material/Material.h
+// SurfaceInteraction (Core/Interaction.h:56-105) as Scene::Intersect fills it: the hit's fields come
+// from the device (pbr_hip_query); the BSDF itself is built and evaluated on the device by the
+// integrators, so ComputeScatteringFunctions records the scattering material and mode only.
+class SurfaceInteraction {
+  public:
+    Point3f p;
+    Vector3f pError;
+    Vector3f wo;
+    Normal3f n;
+    float time = 0;
+    MediumInterface mediumInterface;
+    Point2f uv;
+    Vector3f dpdu;
+    struct {
+        Normal3f n;
+        Vector3f dpdu;
+    } shading;
+    const Primitive* primitive = nullptr;
+    // set by ComputeScatteringFunctions (Primitive.cpp:46-53): the material the device scatters with
+    const Material* bsdfMaterial = nullptr;
+    TransportMode mode = TransportMode::Radiance;
+    bool allowMultipleLobes = false;
+    // not in the reference: the watertight test's barycentrics and the primitive's index in the
+    // BVHAccel's primitive vector
+    float b0 = 0, b1 = 0, b2 = 0;
+    int primIndex = -1;
+    const Medium* GetMedium(const Vector3f& w) const;   // Interaction.h:48-50
+};
+
 // ---------------------------------------------------------------------------- Core/Primitive.h
-class Primitive {
+class Scene;
+class Primitive {   // Core/Primitive.h:11-22
   public:
     virtual ~Primitive() = default;
+    virtual Bounds3f WorldBound() const = 0;
+    virtual bool Intersect(const Ray& r, SurfaceInteraction*) const = 0;
+    virtual bool IntersectP(const Ray& r) const = 0;
+    virtual const AreaLight* GetAreaLight() const = 0;
+    virtual const Material* GetMaterial() const = 0;
+    virtual void ComputeScatteringFunctions(SurfaceInteraction* isect, TransportMode mode, bool allowMultipleLobes) const = 0;
 };
-class GeometricPrimitive : public Primitive {
+// Intersection queries run on the device of the Scene that holds the primitive (a primitive that
+// belongs to no Scene throws std::logic_error): one query per call, or batched through
+// Scene::Intersect(const std::vector<Ray>&, ...).
+class GeometricPrimitive : public Primitive {   // Core/Primitive.h:24-45, Core/Primitive.cpp
   public:
     GeometricPrimitive(const std::shared_ptr<Shape>& shape, const std::shared_ptr<Material>& material,
                        const std::shared_ptr<AreaLight>& areaLight, const MediumInterface& mediumInterface)
         : material(material), areaLight(areaLight), shape(shape), mediumInterface(mediumInterface) {}
+    Bounds3f WorldBound() const override;
+    bool Intersect(const Ray& r, SurfaceInteraction* isect) const override;
+    bool IntersectP(const Ray& r) const override;
+    const AreaLight* GetAreaLight() const override { return areaLight.get(); }
+    const Material* GetMaterial() const override { return material.get(); }
+    void ComputeScatteringFunctions(SurfaceInteraction* isect, TransportMode mode, bool allowMultipleLobes) const override;
     std::shared_ptr<Material> material;
     std::shared_ptr<AreaLight> areaLight;
     std::shared_ptr<Shape> shape;
     MediumInterface mediumInterface;
+    // the Scene (and index in its BVHAccel) whose device answers this primitive's queries
+    mutable const Scene* owner = nullptr;
+    mutable int ownerIndex = -1;
 };
-class Aggregate : public Primitive {};
+class Aggregate : public Primitive {   // Core/Primitive.h:47-55
+  public:
+    const AreaLight* GetAreaLight() const override { return nullptr; }
+    const Material* GetMaterial() const override { return nullptr; }
+    void ComputeScatteringFunctions(SurfaceInteraction*, TransportMode, bool) const override {}
+};
 class BVHAccel : public Aggregate {   // Accelerator/BVHAccel.h:16-21; built on the device at upload
   public:
+    // SAH is the reference's builder; HLBVH falls through to SAH there (BVHAccel.cpp:131-160, no
+    // HLBVH code path) and here.  Middle and EqualCounts are not on the GPU path (refused).
     enum class SplitMethod { SAH, HLBVH, Middle, EqualCounts };
     BVHAccel(std::vector<std::shared_ptr<Primitive>> p, int maxPrimsInNode = 1, SplitMethod splitMethod = SplitMethod::SAH);
     const std::vector<std::shared_ptr<Primitive>>& Primitives() const { return primitives; }
+    Bounds3f WorldBound() const override;
+    bool Intersect(const Ray& r, SurfaceInteraction* isect) const override;
+    bool IntersectP(const Ray& r) const override;
     const int maxPrimsInNode;
     const SplitMethod splitMethod;
+    mutable const Scene* owner = nullptr;
 
   private:
     std::vector<std::shared_ptr<Primitive>> primitives;
 };
 
 // ---------------------------------------------------------------------------- Core/Scene.h
-class Scene {
+struct SceneDevice;
+class Scene {   // Core/Scene.h:13-29
   public:
     Scene(std::shared_ptr<Primitive> aggregate, const std::vector<std::shared_ptr<Light>>& lights);
+    ~Scene();
+    Scene(const Scene&) = delete;
+    Scene& operator=(const Scene&) = delete;
+    const Bounds3f& WorldBound() const;   // the BVH root box
+    bool Intersect(const Ray& ray, SurfaceInteraction* isect) const;
+    bool IntersectP(const Ray& ray) const;
+    // batched queries (one device launch): hit[i] = whether rays[i] hit; rays' tMax are updated
+    void Intersect(const std::vector<Ray>& rays, std::vector<SurfaceInteraction>* isects, std::vector<char>* hit) const;
+    void IntersectP(const std::vector<Ray>& rays, std::vector<char>* hit) const;
+    // one primitive of the BVHAccel (GeometricPrimitive::Intersect / IntersectP on the device)
+    bool IntersectPrimitive(int index, const Ray& ray, SurfaceInteraction* isect) const;
+    bool IntersectPPrimitive(int index, const Ray& ray) const;
+    Bounds3f PrimitiveBound(int index) const;
     std::vector<std::shared_ptr<Light>> lights;
     std::vector<std::shared_ptr<Light>> infiniteLights;
     const std::shared_ptr<Primitive>& GetAggregate() const { return aggregate; }
     uint64_t Id() const { return id; }   // identifies the scene for upload caching
+    void SetQueryDevice(int device) { queryDevice = device; }   // the GPU that answers the queries (default 0)
 
   private:
+    SceneDevice& device() const;
     std::shared_ptr<Primitive> aggregate;
     uint64_t id;
+    int queryDevice = 0;
+    mutable std::unique_ptr<SceneDevice> dev;
 };
 
 // ---------------------------------------------------------------------------- Camera/
+struct CameraSample {   // Camera/Camera.h
+    Point2f pFilm, pLens;
+    float time = 0;
+};
+// Camera rays, sampler values and SamplerIntegrator::Li below are computed on a GPU (device 0 for the
+// camera and sampler helpers, the integrator's device for Li): the reference's per-sample loop
+// (Integrator.cpp:286-313) can be written against these classes and gives the frame Render gives.
 class Camera {
   public:
     virtual ~Camera() = default;
+    virtual float GenerateRay(const CameraSample& sample, Ray* ray) const = 0;
+    virtual float GenerateRayDifferential(const CameraSample& sample, RayDifferential* rd) const {
+        return GenerateRay(sample, rd);   // differentials are dead on the render path (F5)
+    }
 };
 class PerspectiveCamera : public Camera {   // Camera/Perspective.h
   public:
     PerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& CameraToWorld, const Bounds2f& screenWindow,
                       float lensRadius, float focalDistance, float fov, const Medium* medium);
+    // Perspective.cpp:44-62 on the device (pbr_hip_camera_rays); pinhole cameras only
+    float GenerateRay(const CameraSample& sample, Ray* ray) const override;
     const int RasterWidth, RasterHeight;
     const Transform CameraToWorld;
     const Bounds2f screenWindow;
@@ -397,15 +520,27 @@ class PerspectiveCamera : public Camera {   // Camera/Perspective.h
 PerspectiveCamera* CreatePerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& cam2world, Medium* media);
 
 // ---------------------------------------------------------------------------- Sampler/
+// GlobalSampler state (Sampler/Sampler.h:60-105): current pixel, sample number and the next
+// dimension; the values come from the device (pbr_hip_sampler_values).
 class Sampler {
   public:
     explicit Sampler(int64_t samplesPerPixel) : samplesPerPixel(samplesPerPixel) {}
     virtual ~Sampler() = default;
+    virtual void StartPixel(const Point2i& p) { currentPixel = p; currentPixelSampleIndex = 0; dimension = 0; }
+    virtual bool StartNextSample() { dimension = 0; return ++currentPixelSampleIndex < samplesPerPixel; }
+    virtual bool SetSampleNumber(int64_t sampleNum) { dimension = 0; currentPixelSampleIndex = sampleNum; return sampleNum < samplesPerPixel; }
+    int64_t CurrentSampleNumber() const { return currentPixelSampleIndex; }
+    // Sampler.cpp:10-21: pFilm = pRaster + Get2D(), time = Get1D(), pLens = Get2D()
+    virtual CameraSample GetCameraSample(const Point2i& pRaster) = 0;
     const int64_t samplesPerPixel;
+    Point2i currentPixel;
+    int64_t currentPixelSampleIndex = 0;
+    int dimension = 0;   // the next dimension a Get1D/Get2D would read
 };
 class HaltonSampler : public Sampler {   // Sampler/Halton.h
   public:
     HaltonSampler(int nsamp, const Bounds2i& sampleBounds, bool sampleAtCenter = false);
+    CameraSample GetCameraSample(const Point2i& pRaster) override;
     const Bounds2i sampleBounds;
 };
 HaltonSampler* CreateHaltonSampler(const Bounds2i& sampleBounds);   // 16 spp, as Halton.cpp:98-104
@@ -430,6 +565,15 @@ class SamplerIntegrator : public Integrator {
     // Scene), renders every pixel × sample, fills m_FrameBuffer's 8-bit buffer exactly as the
     // reference (XYZ round trip, gamma, vertical flip) and its float buffer.
     void Render(const Scene& scene, double& timeConsume) override;
+    // Uploads the scene to the integrator's device (BVHAccel build, lights, media); Render and Li
+    // do it on first use.  The reference's SamplerIntegrator::Preprocess is a no-op hook.
+    virtual void Preprocess(const Scene& scene, Sampler& sampler);
+    // SamplerIntegrator::Li (Integrator.h:44) on the device for one ray, the sampler positioned at
+    // its current pixel / sample / dimension (after GetCameraSample: dimension 5)
+    virtual Spectrum Li(const RayDifferential& ray, const Scene& scene, Sampler& sampler, int depth = 0) const;
+    // batched: ray i with the sampler at (pixels[i], samples[i], dimension)
+    std::vector<Spectrum> Li(const std::vector<Ray>& rays, const std::vector<Point2i>& pixels,
+                             const std::vector<int64_t>& samples, int dimension, const Scene& scene, int depth = 0) const;
     // Extensions: device ordinal; restrict to tiles (multi-GPU sharding); last stats.
     void SetDevice(int device) { this->device = device; }
     void SetTiles(const std::vector<Bounds2i>& tiles) { this->tiles = tiles; }
@@ -443,14 +587,16 @@ class SamplerIntegrator : public Integrator {
     std::shared_ptr<const Camera> camera;
 
   private:
+    void ensure_scene(const Scene& scene) const;   // context + upload (once per Scene)
     std::shared_ptr<Sampler> sampler;
     const Bounds2i pixelBounds;
     FrameBuffer* m_FrameBuffer;
     int device = 0;
     std::vector<Bounds2i> tiles;
     RenderStats stats;
-    pbr_hip_ctx* ctx = nullptr;
-    uint64_t uploadedScene = 0;
+    mutable pbr_hip_ctx* ctx = nullptr;
+    mutable uint64_t uploadedScene = 0;
+    mutable const Medium* uploadedCameraMedium = nullptr;
 };
 class WhittedIntegrator : public SamplerIntegrator {   // Integrator/WhittedIntegrator.h
   public:

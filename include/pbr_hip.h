@@ -264,6 +264,37 @@ int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height,
 int pbr_hip_camera_rays(pbr_hip_ctx* ctx, const pbr_camera_desc* cam, int n, const float* pfilm, float* out);
 /* Closest-hit queries on the device: rays = o.xyz d.xyz tmax; out = {hit, t, prim_id, b1, b2} as floats */
 int pbr_hip_intersect(pbr_hip_ctx* ctx, int n, const float* rays, float* out, int any_hit);
+/* ---- the reference's C++ query surface, batched (include/pbr/pbr.h builds on these) ---- */
+/* SurfaceInteraction fields of a hit (Core/Interaction.h:56-105), as GeometricPrimitive::Intersect
+ * leaves them (Primitive.cpp:22-36): t = the ray's new tMax. */
+typedef struct pbr_surface_hit {
+    int hit;                    /* 0 / 1 */
+    int prim;                   /* index in the prims vector (shape order), -1 on a miss */
+    float t;
+    float b[3];                 /* barycentrics of the watertight test (triangles; 0 for spheres) */
+    float p[3], p_error[3];
+    float n[3];                 /* geometric normal (Triangle.cpp:197-206 orientation rules) */
+    float ns[3], dpdu[3];       /* shading frame after the per-vertex normals */
+    float wo[3];
+    float uv[2];                /* surface (u, v) of the hit (Triangle.cpp:160-190; sphere: phi/phiMax, (theta-thetaMin)/range) */
+    int medium_inside, medium_outside;   /* the primitive's MediumInterface (indices, -1 = none) */
+} pbr_surface_hit;
+/* Scene::Intersect (Core/Scene.cpp:20-24) or, with any_hit, IntersectP (:26-28) for n rays
+ * (7 floats each: o.xyz, d.xyz, tMax).  prim >= 0 restricts the query to that one primitive
+ * (GeometricPrimitive::Intersect / IntersectP, Core/Primitive.cpp:22-44).  Any-hit queries fill
+ * only `hit`. */
+int pbr_hip_query(pbr_hip_ctx* ctx, int n, const float* rays, int any_hit, int prim, pbr_surface_hit* out);
+/* World bounds (lo.xyz, hi.xyz): prim = -1 → Scene::WorldBound (the BVH root, Scene.cpp:7-17);
+ * prim >= 0 → GeometricPrimitive::WorldBound of that primitive (Primitive.cpp:18-20). */
+int pbr_hip_bounds(pbr_hip_ctx* ctx, int prim, float* out6);
+/* SamplerIntegrator::Li (Integrator.h:44) for n rays (7 floats each) on the device, with the
+ * integrator / sampler / light strategy of `desc` (its tiles and outputs are ignored): each ray's
+ * sampler is GlobalSampler-positioned at (pixel x, y; sample s) with its next dimension `dim`
+ * (px_py_sample_dim: 4 ints per ray; dim 5 after GetCameraSample of a pinhole camera).  depth is
+ * the recursion depth argument (Whitted).  rgb_out: 3 floats per ray. */
+int pbr_hip_li(pbr_hip_ctx* ctx, const pbr_render_desc* desc, int n, const float* rays,
+               const int32_t* px_py_sample_dim, int depth, float* rgb_out);
+
 /* Device build info: ABI version, gfx arch string. */
 int pbr_hip_abi_version(void);
 const char* pbr_hip_build_info(void);

@@ -123,6 +123,30 @@ class HipRenderer:
                     "camera_rays")
         return out
 
+    def query(self, rays, any_hit=False, prim=-1):
+        """Scene::Intersect / IntersectP (prim >= 0: GeometricPrimitive::Intersect of that primitive)
+        with the SurfaceInteraction fields of each hit: an array of capi.SurfaceHit."""
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 7)
+        out = (capi.SurfaceHit * max(1, r.shape[0]))()
+        self._check(self.lib.pbr_hip_query(self.ctx, r.shape[0], capi.fptr(r), int(any_hit), int(prim), out), "query")
+        return out[:r.shape[0]]
+
+    def bounds(self, prim=-1):
+        """Scene::WorldBound (prim = -1) or GeometricPrimitive::WorldBound: (lo[3], hi[3])."""
+        b = np.empty(6, dtype=np.float32)
+        self._check(self.lib.pbr_hip_bounds(self.ctx, int(prim), capi.fptr(b)), "bounds")
+        return b[:3], b[3:]
+
+    def li(self, rdesc, rays, px_py_sample_dim, depth=0):
+        """SamplerIntegrator::Li on the device for caller-given rays: float32 [n, 3]."""
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 7)
+        q = np.ascontiguousarray(px_py_sample_dim, dtype=np.int32).reshape(-1, 4)
+        assert q.shape[0] == r.shape[0]
+        out = np.empty((r.shape[0], 3), dtype=np.float32)
+        self._check(self.lib.pbr_hip_li(self.ctx, C.byref(rdesc), r.shape[0], capi.fptr(r), capi.iptr(q), int(depth),
+                                        capi.fptr(out)), "li")
+        return out
+
     def intersect(self, rays, any_hit=False):
         r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 7)
         out = np.empty((r.shape[0], 5), dtype=np.float32)

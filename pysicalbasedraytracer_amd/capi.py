@@ -163,6 +163,15 @@ class RenderStats(C.Structure):
     ]
 
 
+class SurfaceHit(C.Structure):
+    _fields_ = [
+        ("hit", C.c_int), ("prim", C.c_int), ("t", C.c_float), ("b", C.c_float * 3),
+        ("p", C.c_float * 3), ("p_error", C.c_float * 3), ("n", C.c_float * 3), ("ns", C.c_float * 3),
+        ("dpdu", C.c_float * 3), ("wo", C.c_float * 3), ("uv", C.c_float * 2),
+        ("medium_inside", C.c_int), ("medium_outside", C.c_int),
+    ]
+
+
 class KernelProfile(C.Structure):
     _fields_ = [
         ("name", C.c_char * 40),
@@ -193,6 +202,10 @@ EXPORTS = {
     "pbr_hip_abi_version": (C.c_int, []),
     "pbr_hip_build_info": (C.c_char_p, []),
     "pbr_hip_sobol_matrices": (C.c_int, [C.c_int, C.POINTER(C.c_uint32)]),
+    "pbr_hip_query": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_int, C.c_int, C.POINTER(SurfaceHit)]),
+    "pbr_hip_bounds": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float)]),
+    "pbr_hip_li": (C.c_int, [C.c_void_p, C.POINTER(RenderDesc), C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int32),
+                             C.c_int, C.POINTER(C.c_float)]),
     "pbr_hip_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "pbr_hip_get_profile": (C.c_int, [C.c_void_p, C.POINTER(KernelProfile), C.c_int, C.POINTER(C.c_int)]),
 }
@@ -203,7 +216,8 @@ LIB_PATH = os.path.join(PACKAGE_DIR, "libpbr_hip.so")
 _lib = None
 
 
-OPTIONAL_FOR_AB = ("pbr_hip_sync", "pbr_hip_set_profiling", "pbr_hip_get_profile")
+OPTIONAL_FOR_AB = ("pbr_hip_sync", "pbr_hip_set_profiling", "pbr_hip_get_profile", "pbr_hip_query", "pbr_hip_bounds",
+                   "pbr_hip_li")
 
 
 def load_library(path: str | None = None) -> C.CDLL:

@@ -642,6 +642,94 @@ __global__ void k_intersect(DeviceScene S, const int32_t* primIds, int n, const 
     }
 }
 
+// Scene::Intersect / IntersectP (or one primitive's GeometricPrimitive::Intersect / IntersectP when
+// slotOnly >= 0) with the SurfaceInteraction fields of the hit (pbr_hip_query).
+__global__ void k_query(DeviceScene S, const int32_t* primIds, int n, const float* rays, int any, int slotOnly,
+                        pbr_surface_hit* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* rr = rays + 7 * i;
+    Ray r = mkray(mk(rr[0], rr[1], rr[2]), mk(rr[3], rr[4], rr[5]), rr[6], -1);
+    pbr_surface_hit o;
+    memset(&o, 0, sizeof(o));
+    o.prim = -1;
+    o.medium_inside = o.medium_outside = -1;
+    HitRec h;
+    h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
+    bool hit;
+    if (slotOnly >= 0) {   // GeometricPrimitive::Intersect: the shape's test against ray.tMax
+        float t = 0.f;
+        hit = prim_hit(S, slotOnly, r, &t, &h.b0, &h.b1, &h.b2);
+        if (hit && !any) { r.tMax = t; h.slot = slotOnly; }
+    } else {
+        Counters c;
+        hit = any ? traverse<true, false>(S, r, &h, &c) : traverse<false, false>(S, r, &h, &c);
+    }
+    o.hit = hit ? 1 : 0;
+    if (hit && !any) {
+        const int flags = __float_as_int(S.triVerts[3 * (size_t)h.slot].w);
+        Isect si;
+        if (flags & PRIM_SPHERE) {
+            const SphereRec& sph = S.spheres[__float_as_int(S.triVerts[3 * (size_t)h.slot].x)];
+            sphere_si(sph, r, r.tMax, &si);
+            // pbrt-v3 Sphere::Intersect's (u, v): phi / phiMax, (theta - thetaMin) / (thetaMax - thetaMin)
+            f3 ob = xf_point(sph.w2o, r.o), db = xf_vector(sph.w2o, r.d);
+            f3 ph = ob + db * r.tMax;
+            ph = ph * (sph.radius / len(ph));
+            if (ph.x == 0 && ph.y == 0) ph.x = 1e-5f * sph.radius;
+            float phi = t_atan2(ph.y, ph.x);
+            if (phi < 0) phi += 2 * kPi;
+            const float theta = t_acos(clampf(ph.z / sph.radius, -1, 1));
+            o.uv[0] = phi / (2 * kPi);
+            o.uv[1] = (theta - kPi) / (0.f - kPi);
+        } else {
+            triangle_si(S, h.slot, r, h.b0, h.b1, h.b2, flags, &si);
+            float u0x = 0, u0y = 0, u1x = 1, u1y = 0, u2x = 1, u2y = 1;   // Triangle::GetUVs default
+            if (flags & PRIM_HAS_UV) {
+                const float2* uv = S.triUV + 3 * (size_t)h.slot;
+                u0x = uv[0].x; u0y = uv[0].y; u1x = uv[1].x; u1y = uv[1].y; u2x = uv[2].x; u2y = uv[2].y;
+            }
+            o.uv[0] = h.b0 * u0x + h.b1 * u1x + h.b2 * u2x;   // Triangle.cpp:170
+            o.uv[1] = h.b0 * u0y + h.b1 * u1y + h.b2 * u2y;
+        }
+        const int4 info = S.primInfo[h.slot];
+        o.prim = primIds[h.slot];
+        o.t = r.tMax;
+        o.b[0] = h.b0; o.b[1] = h.b1; o.b[2] = h.b2;
+        o.p[0] = si.p.x; o.p[1] = si.p.y; o.p[2] = si.p.z;
+        o.p_error[0] = si.pError.x; o.p_error[1] = si.pError.y; o.p_error[2] = si.pError.z;
+        o.n[0] = si.n.x; o.n[1] = si.n.y; o.n[2] = si.n.z;
+        o.ns[0] = si.sn.x; o.ns[1] = si.sn.y; o.ns[2] = si.sn.z;
+        o.dpdu[0] = si.dpdu.x; o.dpdu[1] = si.dpdu.y; o.dpdu[2] = si.dpdu.z;
+        o.wo[0] = si.wo.x; o.wo[1] = si.wo.y; o.wo[2] = si.wo.z;
+        o.medium_inside = (int)(short)(info.w & 0xffff);
+        o.medium_outside = (int)(short)((info.w >> 16) & 0xffff);
+    }
+    out[i] = o;
+}
+
+// SamplerIntegrator::Li for caller-given rays (pbr_hip_li): each ray's sampler positioned at
+// (pixel, sample) with its next dimension given.
+template <int INTEGRATOR>
+__global__ void k_li(KParams P, int n, const float* rays, const int32_t* q, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* rr = rays + 7 * i;
+    Ray r = mkray(mk(rr[0], rr[1], rr[2]), mk(rr[3], rr[4], rr[5]), rr[6], -1);   // camera rays carry no medium (F12)
+    SState st;
+    st.index = sample_index(P.smp, q[4 * i], q[4 * i + 1], q[4 * i + 2]).lo;
+    st.sid = q[4 * i + 2];
+    st.dim = q[4 * i + 3];
+    st.px = q[4 * i];
+    st.py = q[4 * i + 1];
+    Counters c = {0, 0, 0, 0};
+    rgb L;
+    if (INTEGRATOR == PBR_INTEGRATOR_WHITTED) L = whitted_li<false>(P, r, st, &c);
+    else if (INTEGRATOR == PBR_INTEGRATOR_PATH) L = path_li<false>(P, r, st, &c);
+    else L = volpath_li<false>(P, r, st, &c);
+    out[3 * i] = L.r; out[3 * i + 1] = L.g; out[3 * i + 2] = L.b;
+}
+
 // Profiling: adds the sums of up to kProfFields segment-count arrays (kWfBlocks ints each) to the
 // counter row dst[0..]; one workgroup, launched after the kernel it counts (outside its events).
 struct ProfSums {
@@ -1300,11 +1388,139 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     return wf_join(ctx, s, ch.lanes);
 }
 
+// The integrator, sampler and scene parameters of a render descriptor (validated): shared by
+// pbr_hip_render and the per-ray pbr_hip_li.
+int make_params(pbr_hip_ctx* ctx, const pbr_render_desc* d, KParams* out) {
+    if (d->spp <= 0) return set_err(ctx, PBR_E_INVALID, "spp must be positive");
+    if (d->max_depth < 0) return set_err(ctx, PBR_E_INVALID, "max_depth must be >= 0");
+    if (d->integrator == PBR_INTEGRATOR_WHITTED && d->max_depth > kMaxWhittedDepth)
+        return set_err(ctx, PBR_E_UNSUPPORTED, "Whitted max_depth above 64 is not supported");
+    if (d->integrator < PBR_INTEGRATOR_WHITTED || d->integrator > PBR_INTEGRATOR_VOLPATH)
+        return set_err(ctx, PBR_E_INVALID, "unknown integrator");
+    if (d->sampler != PBR_SAMPLER_HALTON && d->sampler != PBR_SAMPLER_SOBOL) return set_err(ctx, PBR_E_INVALID, "unknown sampler");
+    // SobolSampler rounds spp up to a power of two (GlobalSampler(RoundUpPow2(spp)), Sobol.h)
+    int spp = d->spp;
+    if (d->sampler == PBR_SAMPLER_SOBOL) {
+        int p2 = 1;
+        while (p2 < spp) p2 <<= 1;
+        spp = p2;
+        int res = 1, m = 0;
+        while (res < std::max(d->camera.width, d->camera.height)) { res <<= 1; ++m; }
+        // pbrt-v3's SobolSampleFloat reads one 52-column matrix per dimension: indices below 2^52
+        if (2 * m + 31 - __builtin_clz((unsigned)spp) > kSobolMatrixSize) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol sample index beyond 52 bits");
+    } else if ((long long)spp * (long long)31104 >= (1ll << 32)) {
+        return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
+    }
+    KParams& P = *out;
+    std::memset(&P, 0, sizeof(P));
+    try {
+        build_camera(&d->camera, &P.cam);
+    } catch (const std::exception& e) {
+        return set_err(ctx, PBR_E_INVALID, e.what());
+    }
+    if (d->light_strategy != ctx->curStrategy) {
+        int rc = upload_light_distribution(ctx, d->light_strategy);
+        if (rc) return rc;
+    }
+    P.S = device_scene(ctx);
+    P.smp = device_sampler(ctx, d->sampler, spp, d->camera.width, d->camera.height);
+    if (d->sampler == PBR_SAMPLER_SOBOL) {
+        int rc = prepare_sobol(ctx, d->sobol_matrices, d->sobol_dims, d->camera.width, d->camera.height, &P.smp);
+        if (rc) return rc;
+        // sample indices (frame << 2m) | j with frame < spp: bits >= 32 exist iff 2m + log2(spp) > 32
+        P.smp.wideIndex = 2 * P.smp.sobolLog2Res + 31 - __builtin_clz((unsigned)spp) > 32;
+        P.smp.hiShift = 32 - 2 * P.smp.sobolLog2Res;
+    }
+    P.integrator = d->integrator;
+    P.maxDepth = d->max_depth;
+    P.rrThreshold = d->rr_threshold;
+    P.spp = spp;
+    P.ppb = spp >= 256 ? 1 : 256 / spp;
+    return PBR_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int pbr_hip_abi_version(void) { return PBR_HIP_ABI_VERSION; }
+
+int pbr_hip_query(pbr_hip_ctx* ctx, int n, const float* rays, int any_hit, int prim, pbr_surface_hit* out) {
+    if (!ctx || n < 0 || (n > 0 && (!rays || !out))) return PBR_E_INVALID;
+    if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    if (prim >= (int)ctx->host.slotOf.size()) return set_err(ctx, PBR_E_INVALID, "primitive index out of range");
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    if (n == 0) return PBR_OK;
+    const int slot = prim >= 0 ? ctx->host.slotOf[prim] : -1;
+    HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 7 * sizeof(float)));
+    HIP_TRY(ctx->dScratchOut.ensure((size_t)n * sizeof(pbr_surface_hit)));
+    HIP_TRY(hipMemcpyAsync(ctx->dScratchIn.p, rays, (size_t)n * 7 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_query, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, device_scene(ctx),
+                       (const int32_t*)ctx->dPrimIds.p, n, (const float*)ctx->dScratchIn.p, any_hit ? 1 : 0, slot,
+                       (pbr_surface_hit*)ctx->dScratchOut.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->dScratchOut.p, (size_t)n * sizeof(pbr_surface_hit), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PBR_OK;
+}
+
+int pbr_hip_bounds(pbr_hip_ctx* ctx, int prim, float* out6) {
+    if (!ctx || !out6) return PBR_E_INVALID;
+    if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    const HostScene& h = ctx->host;
+    if (prim < 0) {
+        if (h.nodes.empty()) {   // an empty scene: Bounds3f() (pMin = +max, pMax = -max)
+            const float M = 3.40282347e+38f;
+            const float e[6] = {M, M, M, -M, -M, -M};
+            std::memcpy(out6, e, sizeof(e));
+            return PBR_OK;
+        }
+        std::memcpy(out6, h.nodes[0].pMin, 12);
+        std::memcpy(out6 + 3, h.nodes[0].pMax, 12);
+        return PBR_OK;
+    }
+    if ((size_t)prim * 6 + 6 > h.primBounds.size()) return set_err(ctx, PBR_E_INVALID, "primitive index out of range");
+    std::memcpy(out6, &h.primBounds[(size_t)prim * 6], 24);
+    return PBR_OK;
+}
+
+int pbr_hip_li(pbr_hip_ctx* ctx, const pbr_render_desc* d, int n, const float* rays, const int32_t* q, int depth,
+               float* rgb_out) {
+    if (!ctx || !d || n < 0 || (n > 0 && (!rays || !q || !rgb_out)) || depth < 0) return PBR_E_INVALID;
+    if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    if (int rc = check_guard(ctx)) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    KParams P;
+    if (int rc = make_params(ctx, d, &P)) return rc;
+    // Whitted recurses while depth + 1 < maxDepth: starting at `depth` is starting at 0 with
+    // maxDepth - depth levels left
+    if (d->integrator == PBR_INTEGRATOR_WHITTED) P.maxDepth = std::max(0, P.maxDepth - depth);
+    if (n == 0) return PBR_OK;
+    for (int i = 0; i < n; ++i) {
+        if (q[4 * i] < 0 || q[4 * i + 1] < 0 || q[4 * i] >= d->camera.width || q[4 * i + 1] >= d->camera.height ||
+            q[4 * i + 2] < 0 || q[4 * i + 2] >= P.spp || q[4 * i + 3] < 0)
+            return set_err(ctx, PBR_E_INVALID, "pixel / sample / dimension out of range");
+    }
+    const size_t rb = (size_t)n * 7 * 4, qb = (size_t)n * 16, ob = (size_t)n * 12;
+    HIP_TRY(ctx->dScratchIn.ensure(rb + qb));
+    HIP_TRY(ctx->dScratchOut.ensure(ob));
+    char* in = (char*)ctx->dScratchIn.p;
+    HIP_TRY(hipMemcpyAsync(in, rays, rb, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(in + rb, q, qb, hipMemcpyHostToDevice, ctx->stream));
+    const dim3 g((n + 63) / 64), b(64);
+    float* o = (float*)ctx->dScratchOut.p;
+    const int32_t* qd = (const int32_t*)(in + rb);
+    if (d->integrator == PBR_INTEGRATOR_WHITTED) hipLaunchKernelGGL(k_li<PBR_INTEGRATOR_WHITTED>, g, b, 0, ctx->stream, P, n, (const float*)in, qd, o);
+    else if (d->integrator == PBR_INTEGRATOR_PATH) hipLaunchKernelGGL(k_li<PBR_INTEGRATOR_PATH>, g, b, 0, ctx->stream, P, n, (const float*)in, qd, o);
+    else hipLaunchKernelGGL(k_li<PBR_INTEGRATOR_VOLPATH>, g, b, 0, ctx->stream, P, n, (const float*)in, qd, o);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(rgb_out, o, ob, hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->host.anyNoMaterial) HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return check_guard(ctx);
+}
 #ifndef PBR_SRC_HASH
 #define PBR_SRC_HASH "unknown"
 #endif
@@ -1441,55 +1657,12 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (!d) return set_err(ctx, PBR_E_INVALID, "null render desc");
     if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
     if (int rc = check_guard(ctx)) return rc;   // an earlier asynchronous frame stopped at a bound
-    if (d->spp <= 0) return set_err(ctx, PBR_E_INVALID, "spp must be positive");
-    if (d->max_depth < 0) return set_err(ctx, PBR_E_INVALID, "max_depth must be >= 0");
-    if (d->integrator == PBR_INTEGRATOR_WHITTED && d->max_depth > kMaxWhittedDepth)
-        return set_err(ctx, PBR_E_UNSUPPORTED, "Whitted max_depth above 64 is not supported");
-    if (d->integrator < PBR_INTEGRATOR_WHITTED || d->integrator > PBR_INTEGRATOR_VOLPATH)
-        return set_err(ctx, PBR_E_INVALID, "unknown integrator");
-    if (d->sampler != PBR_SAMPLER_HALTON && d->sampler != PBR_SAMPLER_SOBOL) return set_err(ctx, PBR_E_INVALID, "unknown sampler");
-    // SobolSampler rounds spp up to a power of two (GlobalSampler(RoundUpPow2(spp)), Sobol.h)
-    int spp = d->spp;
-    if (d->sampler == PBR_SAMPLER_SOBOL) {
-        int p2 = 1;
-        while (p2 < spp) p2 <<= 1;
-        spp = p2;
-        int res = 1, m = 0;
-        while (res < std::max(d->camera.width, d->camera.height)) { res <<= 1; ++m; }
-        // pbrt-v3's SobolSampleFloat reads one 52-column matrix per dimension: indices below 2^52
-        if (2 * m + 31 - __builtin_clz((unsigned)spp) > kSobolMatrixSize) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol sample index beyond 52 bits");
-    } else if ((long long)spp * (long long)31104 >= (1ll << 32)) {
-        return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
-    }
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = d->stream ? (hipStream_t)d->stream : ctx->stream;
-
     KParams P;
-    std::memset(&P, 0, sizeof(P));
-    try {
-        build_camera(&d->camera, &P.cam);
-    } catch (const std::exception& e) {
-        return set_err(ctx, PBR_E_INVALID, e.what());
-    }
-    if (d->light_strategy != ctx->curStrategy) {
-        int rc = upload_light_distribution(ctx, d->light_strategy);
-        if (rc) return rc;
-    }
-    P.S = device_scene(ctx);
-    P.smp = device_sampler(ctx, d->sampler, spp, d->camera.width, d->camera.height);
-    if (d->sampler == PBR_SAMPLER_SOBOL) {
-        int rc = prepare_sobol(ctx, d->sobol_matrices, d->sobol_dims, d->camera.width, d->camera.height, &P.smp);
-        if (rc) return rc;
-        // sample indices (frame << 2m) | j with frame < spp: bits >= 32 exist iff 2m + log2(spp) > 32
-        P.smp.wideIndex = 2 * P.smp.sobolLog2Res + 31 - __builtin_clz((unsigned)spp) > 32;
-        P.smp.hiShift = 32 - 2 * P.smp.sobolLog2Res;
-    }
-    P.integrator = d->integrator;
-    P.maxDepth = d->max_depth;
-    P.rrThreshold = d->rr_threshold;
-    P.spp = spp;
-    P.ppb = spp >= 256 ? 1 : 256 / spp;
+    if (int rc = make_params(ctx, d, &P)) return rc;
+    const int spp = P.spp;
     // tiles
     std::vector<int32_t> tiles;
     std::vector<long long> starts;

@@ -493,6 +493,8 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
     };
     // 2. SAH BVH over primitive world bounds
     std::vector<Item> items(np);
+    S->primBounds.clear();
+    S->primBounds.reserve((size_t)np * 6);
     for (int i = 0; i < np; ++i) {
         Box b;
         if (prims[i].tri >= 0) {   // Triangle::WorldBound (Triangle.cpp:55-62)
@@ -511,11 +513,13 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
         }
         items[i].id = (size_t)i;
         items[i].box = b;
+        S->primBounds.insert(S->primBounds.end(), {b.lo.x, b.lo.y, b.lo.z, b.hi.x, b.hi.y, b.hi.z});
         items[i].c = .5f * b.lo + .5f * b.hi;
     }
     SahBuilder(items, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1, &S->nodes, &S->primIds).run();
     // 3. primitive payloads in BVH order
-    std::vector<int> slotOf(np, -1);
+    std::vector<int>& slotOf = S->slotOf;
+    slotOf.assign(np, -1);
     bool anyUV = false;
     for (int i = 0; i < ns; ++i) if (d->shapes[i].type == PBR_SHAPE_TRIANGLE_MESH && d->shapes[i].UV) anyUV = true;
     S->triVerts.assign((size_t)np * 12, 0.f);

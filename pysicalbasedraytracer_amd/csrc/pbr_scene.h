@@ -51,6 +51,8 @@ struct HostScene {
     int32_t rootRef = 0;
     std::vector<float> quad;                // 32 floats per quad node (build_quad_nodes)
     int32_t quadRootRef = 0;
+    std::vector<float> primBounds;          // 6 floats (lo, hi) per primitive in prims order: GeometricPrimitive::WorldBound
+    std::vector<int32_t> slotOf;            // prims index → BVH slot
     std::vector<int32_t> leafParent;        // per primitive slot that starts a leaf: parentQuad << 2 | raw slot, -1 at the root
     InfiniteHost inf;                       // the InfiniteAreaLight, if any (pbr_infinite.cpp)
 };

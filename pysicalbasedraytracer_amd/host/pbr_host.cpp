@@ -443,13 +443,56 @@ InfiniteAreaLight::InfiniteAreaLight(const Transform& LightToWorld, const Spectr
 // ============================================================================ aggregate, scene, camera, sampler
 BVHAccel::BVHAccel(std::vector<std::shared_ptr<Primitive>> p, int maxPrimsInNode, SplitMethod splitMethod)
     : maxPrimsInNode(std::min(255, maxPrimsInNode)), splitMethod(splitMethod), primitives(std::move(p)) {
-    if (splitMethod != SplitMethod::SAH) throw std::invalid_argument("BVHAccel: only SplitMethod::SAH is on the GPU path");
+    // BVHAccel.cpp:131-160: the reference's switch has no HLBVH branch, so HLBVH builds with SAH
+    if (splitMethod == SplitMethod::Middle || splitMethod == SplitMethod::EqualCounts)
+        throw std::invalid_argument("BVHAccel: only SplitMethod::SAH (and HLBVH, which the reference builds with SAH) "
+                                    "is on the GPU path");
 }
+
+Bounds3f::Bounds3f() {
+    const float M = 3.40282347e+38f;
+    pMin = Point3f(M, M, M);
+    pMax = Point3f(-M, -M, -M);
+}
+
+const Medium* SurfaceInteraction::GetMedium(const Vector3f& w) const {
+    const float d = w.x * n.x + w.y * n.y + w.z * n.z;
+    return d > 0 ? mediumInterface.outside : mediumInterface.inside;
+}
+
+// ---- device-side queries of a Scene (pbr_hip_query / pbr_hip_bounds on the scene's own context)
+struct SceneDevice {
+    pbr_hip_ctx* ctx = nullptr;
+    std::shared_ptr<FlatScene> flat;
+    std::vector<const Primitive*> prims;   // the BVHAccel's primitive vector
+    Bounds3f worldBound;
+    ~SceneDevice() {
+        if (ctx) pbr_hip_destroy(ctx);
+    }
+};
 
 Scene::Scene(std::shared_ptr<Primitive> aggregate, const std::vector<std::shared_ptr<Light>>& lights)
     : lights(lights), aggregate(std::move(aggregate)), id(g_sceneIds++) {
     for (const auto& l : lights)
         if (l->IsInfinite()) infiniteLights.push_back(l);
+    // the primitives answer their own queries through this scene's device context
+    if (auto* bvh = dynamic_cast<const BVHAccel*>(this->aggregate.get())) {
+        bvh->owner = this;
+        int k = 0;
+        for (const auto& p : bvh->Primitives()) {
+            if (auto* gp = dynamic_cast<const GeometricPrimitive*>(p.get())) { gp->owner = this; gp->ownerIndex = k; }
+            ++k;
+        }
+    }
+}
+
+Scene::~Scene() {
+    if (auto* bvh = dynamic_cast<const BVHAccel*>(aggregate.get())) {
+        if (bvh->owner == this) bvh->owner = nullptr;
+        for (const auto& p : bvh->Primitives())
+            if (auto* gp = dynamic_cast<const GeometricPrimitive*>(p.get()))
+                if (gp->owner == this) { gp->owner = nullptr; gp->ownerIndex = -1; }
+    }
 }
 
 PerspectiveCamera::PerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& CameraToWorld, const Bounds2f& screenWindow,
@@ -747,6 +790,23 @@ void check(pbr_hip_ctx* ctx, int rc, const char* what) {
     if (ctx) msg += ": " + std::string(pbr_hip_last_error(ctx));
     throw std::runtime_error(msg);
 }
+void camera_desc(const PerspectiveCamera& cam, pbr_camera_desc* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->width = cam.RasterWidth;
+    c->height = cam.RasterHeight;
+    fill_transform(cam.CameraToWorld, &c->camera_to_world);
+    c->fov = cam.fov;
+    c->lens_radius = cam.lensRadius;
+    c->focal_distance = cam.focalDistance;
+    c->medium = -1;
+}
+// Device 0 context for the stateless helpers (camera rays, sampler values).  Kept for the life of the
+// process: destroying it from a static destructor could run after the HIP runtime has shut down.
+pbr_hip_ctx* helper_ctx() {
+    static pbr_hip_ctx* h = nullptr;
+    if (!h) check(nullptr, pbr_hip_create(0, &h), "pbr_hip_create");
+    return h;
+}
 }  // namespace
 
 void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
@@ -764,12 +824,8 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     if (cam->screenWindow.pMin.x != -sx || cam->screenWindow.pMax.x != sx || cam->screenWindow.pMin.y != -sy ||
         cam->screenWindow.pMax.y != sy)
         throw std::invalid_argument("Render: custom screen windows are not on the GPU path");
-    if (!ctx) check(nullptr, pbr_hip_create(device, &ctx), "pbr_hip_create");
-    auto flat = FlattenScene(scene, cam->medium);
-    if (uploadedScene != scene.Id()) {
-        check(ctx, pbr_hip_upload_scene(ctx, SceneDesc(*flat)), "pbr_hip_upload_scene");
-        uploadedScene = scene.Id();
-    }
+    ensure_scene(scene);
+    auto flat = FlattenScene(scene, cam->medium);   // for the camera medium's index
     pbr_render_desc rd;
     std::memset(&rd, 0, sizeof(rd));
     rd.integrator = IntegratorType();
@@ -778,14 +834,8 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     rd.light_strategy = LightStrategy();
     rd.sampler = PBR_SAMPLER_HALTON;
     rd.spp = (int)halton->samplesPerPixel;
-    pbr_camera_desc& c = rd.camera;
-    c.width = cam->RasterWidth;
-    c.height = cam->RasterHeight;
-    fill_transform(cam->CameraToWorld, &c.camera_to_world);
-    c.fov = cam->fov;
-    c.lens_radius = cam->lensRadius;
-    c.focal_distance = cam->focalDistance;
-    c.medium = MediumIndex(*flat, cam->medium);
+    camera_desc(*cam, &rd.camera);
+    rd.camera.medium = MediumIndex(*flat, cam->medium);
     std::vector<pbr_tile> tl;
     if (!tiles.empty()) {
         for (const Bounds2i& b : tiles) tl.push_back({b.pMin.x, b.pMin.y, b.pMax.x, b.pMax.y});
@@ -818,6 +868,241 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     stats.samples = st.samples;
     timeConsume = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     IntegratorRenderTime = (float)timeConsume;
+}
+
+// ============================================================================ scene queries
+SceneDevice& Scene::device() const {
+    if (dev) return *dev;
+    auto d = std::make_unique<SceneDevice>();
+    auto* bvh = dynamic_cast<const BVHAccel*>(aggregate.get());
+    if (!bvh) throw std::invalid_argument("Scene queries need a BVHAccel aggregate");
+    for (const auto& p : bvh->Primitives()) d->prims.push_back(p.get());
+    d->flat = FlattenScene(*this, nullptr);
+    check(nullptr, pbr_hip_create(queryDevice, &d->ctx), "pbr_hip_create");
+    check(d->ctx, pbr_hip_upload_scene(d->ctx, SceneDesc(*d->flat)), "pbr_hip_upload_scene");
+    float b[6];
+    check(d->ctx, pbr_hip_bounds(d->ctx, -1, b), "pbr_hip_bounds");
+    d->worldBound = Bounds3f(Point3f(b[0], b[1], b[2]), Point3f(b[3], b[4], b[5]));
+    dev = std::move(d);
+    return *dev;
+}
+
+const Bounds3f& Scene::WorldBound() const { return device().worldBound; }
+
+namespace {
+void ray_floats(const Ray& r, float* o) {
+    o[0] = r.o.x; o[1] = r.o.y; o[2] = r.o.z; o[3] = r.d.x; o[4] = r.d.y; o[5] = r.d.z; o[6] = r.tMax;
+}
+const Medium* medium_at(const FlatScene& f, int index) {
+    if (index < 0) return nullptr;
+    for (const auto& kv : f.mediumIndex)
+        if (kv.second == index) return kv.first;
+    return nullptr;
+}
+// GeometricPrimitive::Intersect's bookkeeping (Primitive.cpp:22-36): r.tMax = tHit, the
+// interaction's primitive and medium interface
+void fill_isect(const SceneDevice& d, const pbr_surface_hit& h, const Ray& r, SurfaceInteraction* si) {
+    r.tMax = h.t;
+    if (!si) return;
+    si->p = Point3f(h.p[0], h.p[1], h.p[2]);
+    si->pError = Vector3f(h.p_error[0], h.p_error[1], h.p_error[2]);
+    si->wo = Vector3f(h.wo[0], h.wo[1], h.wo[2]);
+    si->n = Normal3f(h.n[0], h.n[1], h.n[2]);
+    si->shading.n = Normal3f(h.ns[0], h.ns[1], h.ns[2]);
+    si->dpdu = si->shading.dpdu = Vector3f(h.dpdu[0], h.dpdu[1], h.dpdu[2]);
+    si->uv = Point2f(h.uv[0], h.uv[1]);
+    si->time = r.time;
+    si->b0 = h.b[0]; si->b1 = h.b[1]; si->b2 = h.b[2];
+    si->primIndex = h.prim;
+    si->primitive = h.prim >= 0 && h.prim < (int)d.prims.size() ? d.prims[h.prim] : nullptr;
+    const Medium* in = medium_at(*d.flat, h.medium_inside);
+    const Medium* out = medium_at(*d.flat, h.medium_outside);
+    si->mediumInterface = in != out ? MediumInterface(in, out) : MediumInterface(r.medium);
+    si->bsdfMaterial = nullptr;
+}
+}  // namespace
+
+void Scene::Intersect(const std::vector<Ray>& rays, std::vector<SurfaceInteraction>* isects, std::vector<char>* hit) const {
+    SceneDevice& d = device();
+    std::vector<float> rf(rays.size() * 7);
+    for (size_t i = 0; i < rays.size(); ++i) ray_floats(rays[i], &rf[7 * i]);
+    std::vector<pbr_surface_hit> out(rays.size());
+    check(d.ctx, pbr_hip_query(d.ctx, (int)rays.size(), rf.data(), 0, -1, out.data()), "pbr_hip_query");
+    if (isects) isects->assign(rays.size(), SurfaceInteraction());
+    if (hit) hit->assign(rays.size(), 0);
+    for (size_t i = 0; i < rays.size(); ++i) {
+        if (hit) (*hit)[i] = (char)out[i].hit;
+        if (out[i].hit) fill_isect(d, out[i], rays[i], isects ? &(*isects)[i] : nullptr);
+    }
+}
+
+void Scene::IntersectP(const std::vector<Ray>& rays, std::vector<char>* hit) const {
+    SceneDevice& d = device();
+    std::vector<float> rf(rays.size() * 7);
+    for (size_t i = 0; i < rays.size(); ++i) ray_floats(rays[i], &rf[7 * i]);
+    std::vector<pbr_surface_hit> out(rays.size());
+    check(d.ctx, pbr_hip_query(d.ctx, (int)rays.size(), rf.data(), 1, -1, out.data()), "pbr_hip_query");
+    hit->assign(rays.size(), 0);
+    for (size_t i = 0; i < rays.size(); ++i) (*hit)[i] = (char)out[i].hit;
+}
+
+bool Scene::Intersect(const Ray& ray, SurfaceInteraction* isect) const {   // Scene.cpp:20-24
+    SceneDevice& d = device();
+    float rf[7];
+    ray_floats(ray, rf);
+    pbr_surface_hit h;
+    check(d.ctx, pbr_hip_query(d.ctx, 1, rf, 0, -1, &h), "pbr_hip_query");
+    if (!h.hit) return false;
+    fill_isect(d, h, ray, isect);
+    return true;
+}
+
+bool Scene::IntersectP(const Ray& ray) const {   // Scene.cpp:26-28
+    std::vector<char> hit;
+    IntersectP(std::vector<Ray>{ray}, &hit);
+    return hit[0] != 0;
+}
+
+bool Scene::IntersectPrimitive(int index, const Ray& ray, SurfaceInteraction* isect) const {
+    SceneDevice& d = device();
+    float rf[7];
+    ray_floats(ray, rf);
+    pbr_surface_hit h;
+    check(d.ctx, pbr_hip_query(d.ctx, 1, rf, 0, index, &h), "pbr_hip_query");
+    if (!h.hit) return false;
+    fill_isect(d, h, ray, isect);
+    return true;
+}
+
+bool Scene::IntersectPPrimitive(int index, const Ray& ray) const {
+    SceneDevice& d = device();
+    float rf[7];
+    ray_floats(ray, rf);
+    pbr_surface_hit h;
+    check(d.ctx, pbr_hip_query(d.ctx, 1, rf, 1, index, &h), "pbr_hip_query");
+    return h.hit != 0;
+}
+
+Bounds3f Scene::PrimitiveBound(int index) const {
+    SceneDevice& d = device();
+    float b[6];
+    check(d.ctx, pbr_hip_bounds(d.ctx, index, b), "pbr_hip_bounds");
+    return Bounds3f(Point3f(b[0], b[1], b[2]), Point3f(b[3], b[4], b[5]));
+}
+
+namespace {
+const Scene& owner_of(const Scene* s, const char* what) {
+    if (!s) throw std::logic_error(std::string(what) + ": the primitive belongs to no Scene (queries run on its device)");
+    return *s;
+}
+}  // namespace
+
+Bounds3f GeometricPrimitive::WorldBound() const { return owner_of(owner, "GeometricPrimitive::WorldBound").PrimitiveBound(ownerIndex); }
+bool GeometricPrimitive::Intersect(const Ray& r, SurfaceInteraction* isect) const {
+    return owner_of(owner, "GeometricPrimitive::Intersect").IntersectPrimitive(ownerIndex, r, isect);
+}
+bool GeometricPrimitive::IntersectP(const Ray& r) const {
+    return owner_of(owner, "GeometricPrimitive::IntersectP").IntersectPPrimitive(ownerIndex, r);
+}
+void GeometricPrimitive::ComputeScatteringFunctions(SurfaceInteraction* isect, TransportMode mode, bool allowMultipleLobes) const {
+    // Primitive.cpp:46-53: the material builds the BSDF; here the BSDF lives on the device, so the
+    // interaction records which material scatters and how
+    isect->bsdfMaterial = material.get();
+    isect->mode = mode;
+    isect->allowMultipleLobes = allowMultipleLobes;
+}
+Bounds3f BVHAccel::WorldBound() const { return owner_of(owner, "BVHAccel::WorldBound").WorldBound(); }
+bool BVHAccel::Intersect(const Ray& r, SurfaceInteraction* isect) const {
+    return owner_of(owner, "BVHAccel::Intersect").Intersect(r, isect);
+}
+bool BVHAccel::IntersectP(const Ray& r) const { return owner_of(owner, "BVHAccel::IntersectP").IntersectP(r); }
+
+// ============================================================================ camera, sampler, Li
+float PerspectiveCamera::GenerateRay(const CameraSample& sample, Ray* ray) const {   // Perspective.cpp:44-62
+    if (lensRadius > 0) throw std::invalid_argument("PerspectiveCamera::GenerateRay: thin-lens cameras are not on the GPU path");
+    pbr_camera_desc c;
+    camera_desc(*this, &c);
+    const float pf[2] = {sample.pFilm.x, sample.pFilm.y};
+    float out[6];
+    pbr_hip_ctx* h = helper_ctx();
+    check(h, pbr_hip_camera_rays(h, &c, 1, pf, out), "pbr_hip_camera_rays");
+    *ray = Ray(Point3f(out[0], out[1], out[2]), Vector3f(out[3], out[4], out[5]));
+    ray->time = sample.time;
+    ray->medium = medium;
+    return 1;
+}
+
+CameraSample HaltonSampler::GetCameraSample(const Point2i& pRaster) {   // Sampler.cpp:10-21
+    const int W = sampleBounds.pMax.x - sampleBounds.pMin.x, H = sampleBounds.pMax.y - sampleBounds.pMin.y;
+    int32_t q[20];
+    for (int k = 0; k < 5; ++k) {
+        q[4 * k] = pRaster.x; q[4 * k + 1] = pRaster.y; q[4 * k + 2] = (int32_t)currentPixelSampleIndex; q[4 * k + 3] = k;
+    }
+    float v[5];
+    pbr_hip_ctx* h = helper_ctx();
+    check(h, pbr_hip_sampler_values(h, PBR_SAMPLER_HALTON, W, H, (int)samplesPerPixel, 5, q, v), "pbr_hip_sampler_values");
+    CameraSample cs;
+    cs.pFilm = Point2f((float)pRaster.x + v[0], (float)pRaster.y + v[1]);
+    cs.time = v[2];
+    cs.pLens = Point2f(v[3], v[4]);
+    dimension = 5;
+    return cs;
+}
+
+void SamplerIntegrator::ensure_scene(const Scene& scene) const {
+    auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
+    const Medium* cm = cam ? cam->medium : nullptr;
+    if (!ctx) check(nullptr, pbr_hip_create(device, &ctx), "pbr_hip_create");
+    if (uploadedScene != scene.Id() || uploadedCameraMedium != cm) {
+        auto flat = FlattenScene(scene, cm);
+        check(ctx, pbr_hip_upload_scene(ctx, SceneDesc(*flat)), "pbr_hip_upload_scene");
+        uploadedScene = scene.Id();
+        uploadedCameraMedium = cm;
+    }
+}
+
+void SamplerIntegrator::Preprocess(const Scene& scene, Sampler&) { ensure_scene(scene); }
+
+std::vector<Spectrum> SamplerIntegrator::Li(const std::vector<Ray>& rays, const std::vector<Point2i>& pixels,
+                                            const std::vector<int64_t>& samples, int dimension, const Scene& scene,
+                                            int depth) const {
+    if (pixels.size() != rays.size() || samples.size() != rays.size())
+        throw std::invalid_argument("Li: rays, pixels and samples differ in length");
+    auto* halton = dynamic_cast<const HaltonSampler*>(sampler.get());
+    if (!halton) throw std::invalid_argument("Li: only HaltonSampler is on the GPU path");
+    ensure_scene(scene);
+    pbr_render_desc rd;
+    std::memset(&rd, 0, sizeof(rd));
+    rd.integrator = IntegratorType();
+    rd.max_depth = MaxDepth();
+    rd.rr_threshold = RRThreshold();
+    rd.light_strategy = LightStrategy();
+    rd.sampler = PBR_SAMPLER_HALTON;
+    rd.spp = (int)halton->samplesPerPixel;
+    rd.camera.width = halton->sampleBounds.pMax.x - halton->sampleBounds.pMin.x;   // the sampler's raster
+    rd.camera.height = halton->sampleBounds.pMax.y - halton->sampleBounds.pMin.y;
+    rd.camera.fov = 90.f;
+    rd.camera.camera_to_world.m[0] = rd.camera.camera_to_world.m[5] = rd.camera.camera_to_world.m[10] =
+        rd.camera.camera_to_world.m[15] = 1.f;
+    rd.camera.camera_to_world.m_inv[0] = rd.camera.camera_to_world.m_inv[5] = rd.camera.camera_to_world.m_inv[10] =
+        rd.camera.camera_to_world.m_inv[15] = 1.f;
+    rd.camera.medium = -1;
+    std::vector<float> rf(rays.size() * 7);
+    std::vector<int32_t> q(rays.size() * 4);
+    for (size_t i = 0; i < rays.size(); ++i) {
+        ray_floats(rays[i], &rf[7 * i]);
+        q[4 * i] = pixels[i].x; q[4 * i + 1] = pixels[i].y; q[4 * i + 2] = (int32_t)samples[i]; q[4 * i + 3] = dimension;
+    }
+    std::vector<float> L(rays.size() * 3);
+    check(ctx, pbr_hip_li(ctx, &rd, (int)rays.size(), rf.data(), q.data(), depth, L.data()), "pbr_hip_li");
+    std::vector<Spectrum> out(rays.size());
+    for (size_t i = 0; i < rays.size(); ++i) { out[i][0] = L[3 * i]; out[i][1] = L[3 * i + 1]; out[i][2] = L[3 * i + 2]; }
+    return out;
+}
+
+Spectrum SamplerIntegrator::Li(const RayDifferential& ray, const Scene& scene, Sampler& s, int depth) const {
+    return Li(std::vector<Ray>{ray}, std::vector<Point2i>{s.currentPixel}, std::vector<int64_t>{s.currentPixelSampleIndex},
+              s.dimension, scene, depth)[0];
 }
 
 }  // namespace PBR

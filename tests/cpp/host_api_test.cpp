@@ -220,6 +220,130 @@ int run_cpu() {
     return failures ? 1 : 0;
 }
 
+// Scene::Intersect / IntersectP / WorldBound and the Primitive virtuals (Scene.h:19-21,
+// Primitive.h:13-21) on the device, against the oracle's Scene::Intersect on the same scene.
+void scene_queries() {
+    Built b;
+    build_area(b, 32, 24, true);
+    const Scene& sc = *b.scene;
+    auto flat = FlattenScene(sc, nullptr);
+    // rays: a fan from two origins through the scene, plus a few that must miss
+    std::vector<Ray> rays;
+    for (int i = 0; i < 24; ++i)
+        for (int j = 0; j < 16; ++j) {
+            const float u = -1.5f + 3.f * (float)i / 23.f, v = -1.2f + 2.4f * (float)j / 15.f;
+            rays.emplace_back(Point3f(0.1f, 0.6f, 3.f), Vector3f(u, v - 0.3f, -2.5f));
+            rays.emplace_back(Point3f(-2.f, 2.5f, 0.3f), Vector3f(1.f + 0.2f * u, -1.f + 0.3f * v, -0.1f * v));
+        }
+    rays.emplace_back(Point3f(0.f, 0.f, 50.f), Vector3f(0.f, 0.f, 1.f));
+    rays.emplace_back(Point3f(0.1f, 0.6f, 3.f), Vector3f(0.f, -0.3f, -2.5f), 0.01f);   // short tMax
+    const int n = (int)rays.size();
+    std::vector<float> rf((size_t)n * 7);
+    for (int i = 0; i < n; ++i) {
+        const Ray& r = rays[i];
+        const float v[7] = {r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.tMax};
+        std::memcpy(&rf[7 * (size_t)i], v, sizeof v);
+    }
+    std::vector<float> oc((size_t)n * 5), oa((size_t)n * 5);
+    expect(oracle_intersect(SceneDesc(*flat), n, rf.data(), oc.data(), 0) == 0 &&
+               oracle_intersect(SceneDesc(*flat), n, rf.data(), oa.data(), 1) == 0, "oracle Intersect / IntersectP");
+    std::vector<Ray> batch = rays;
+    std::vector<SurfaceInteraction> si;
+    std::vector<char> hit, hitP;
+    sc.Intersect(batch, &si, &hit);
+    sc.IntersectP(rays, &hitP);
+    auto* bvh = dynamic_cast<const BVHAccel*>(sc.GetAggregate().get());
+    int nHit = 0, bad = 0, badP = 0, badSingle = 0, badPrim = 0, badBox = 0;
+    const Bounds3f wb = sc.WorldBound();
+    for (int i = 0; i < n; ++i) {
+        const float* o = &oc[5 * (size_t)i];
+        if ((o[0] != 0.f) != (hit[i] != 0)) { ++bad; continue; }
+        if ((oa[5 * (size_t)i] != 0.f) != (hitP[i] != 0) || (sc.IntersectP(rays[i]) != (hitP[i] != 0))) ++badP;
+        if (!hit[i]) continue;
+        ++nHit;
+        const SurfaceInteraction& s = si[i];
+        if (batch[i].tMax != o[1] || s.primIndex != (int)o[2] || s.b1 != o[3] || s.b2 != o[4] ||
+            s.primitive != bvh->Primitives()[s.primIndex].get())
+            ++bad;
+        // the single-ray call and the aggregate's own Intersect agree with the batch
+        Ray r1 = rays[i];
+        SurfaceInteraction s1;
+        if (!sc.Intersect(r1, &s1) || r1.tMax != batch[i].tMax || std::memcmp(&s1.p, &s.p, sizeof(Point3f)) != 0) ++badSingle;
+        Ray r2 = rays[i];
+        SurfaceInteraction s2;
+        if (!bvh->Intersect(r2, &s2) || r2.tMax != batch[i].tMax) ++badSingle;
+        // GeometricPrimitive::Intersect of the hit primitive alone finds the same t
+        Ray r3 = rays[i];
+        SurfaceInteraction s3;
+        if (!s.primitive->Intersect(r3, &s3) || r3.tMax != batch[i].tMax || !s.primitive->IntersectP(rays[i])) ++badPrim;
+        s.primitive->ComputeScatteringFunctions(&s3, TransportMode::Radiance, true);
+        if (s3.bsdfMaterial != s.primitive->GetMaterial()) ++badPrim;
+        // the hit point lies in the primitive's and the scene's bounds (up to the hit's error bound)
+        const Bounds3f pb = s.primitive->WorldBound();
+        for (int a = 0; a < 3; ++a) {
+            const float e = s.pError[a] + 1e-6f;
+            if (s.p[a] < pb.pMin[a] - e || s.p[a] > pb.pMax[a] + e || s.p[a] < wb.pMin[a] - e || s.p[a] > wb.pMax[a] + e) ++badBox;
+        }
+    }
+    char msg[200];
+    std::snprintf(msg, sizeof msg, "Scene::Intersect batch = oracle on %d rays (%d hits): hit, tMax, primitive, b1, b2", n, nHit);
+    expect(bad == 0 && nHit > n / 4, msg);
+    expect(badP == 0, "Scene::IntersectP (batch and single) = oracle IntersectP");
+    expect(badSingle == 0, "single-ray Scene::Intersect and BVHAccel::Intersect = the batch");
+    expect(badPrim == 0, "GeometricPrimitive::Intersect / IntersectP / ComputeScatteringFunctions of the hit primitive");
+    expect(badBox == 0, "hit points inside GeometricPrimitive::WorldBound and Scene::WorldBound");
+    expect(bvh->WorldBound().pMin.x == wb.pMin.x && wb.pMin.x < wb.pMax.x, "BVHAccel::WorldBound = Scene::WorldBound");
+    // a primitive outside any scene cannot answer
+    auto lone = std::make_shared<GeometricPrimitive>(std::static_pointer_cast<GeometricPrimitive>(bvh->Primitives()[0])->shape,
+                                                     nullptr, nullptr, MediumInterface());
+    bool threw = false;
+    try { lone->IntersectP(rays[0]); } catch (const std::logic_error&) { threw = true; }
+    expect(threw, "GeometricPrimitive outside a Scene throws");
+}
+
+// The reference's per-sample loop (Integrator.cpp:286-313) written against the host API —
+// StartPixel, GetCameraSample, GenerateRayDifferential, Li, colObj += L, StartNextSample,
+// colObj / spp — gives bit for bit the frame Render gives.
+void decomposed_render_loop() {
+    for (int itype = 0; itype < 2; ++itype) {
+        Built b;
+        const int W = 20, H = 14, spp = 4;
+        if (itype == 0) build_c1(b, W, H); else build_area(b, W, H, false);
+        FrameBuffer fb;
+        fb.InitBuffer(W, H, 4);
+        auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        std::shared_ptr<SamplerIntegrator> integ;
+        if (itype == 0) integ = std::make_shared<WhittedIntegrator>(5, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), &fb);
+        else integ = std::make_shared<PathIntegrator>(6, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &fb);
+        double t = 0;
+        integ->Render(*b.scene, t);
+        integ->Preprocess(*b.scene, *sampler);
+        int bad = 0, checked = 0;
+        for (int y = 0; y < H; y += 3)
+            for (int x = 0; x < W; x += 2) {
+                const Point2i pixel(x, y);
+                sampler->StartPixel(pixel);
+                float col[3] = {0.f, 0.f, 0.f};
+                do {
+                    CameraSample cs = sampler->GetCameraSample(pixel);
+                    RayDifferential r;
+                    b.cam->GenerateRayDifferential(cs, &r);
+                    r.ScaleDifferentials(1 / std::sqrt((float)sampler->samplesPerPixel));
+                    Spectrum L = integ->Li(r, *b.scene, *sampler, 0);
+                    for (int c = 0; c < 3; ++c) col[c] = col[c] + L[c];
+                } while (sampler->StartNextSample());
+                for (int c = 0; c < 3; ++c) col[c] = col[c] / (float)spp;
+                const float* f = &fb.getFCbuffer()[((size_t)x + (size_t)(H - 1 - y) * W) * 4];
+                if (std::memcmp(col, f, sizeof col) != 0) ++bad;
+                ++checked;
+            }
+        char msg[200];
+        std::snprintf(msg, sizeof msg, "%s: the reference's per-sample loop through GetCameraSample / GenerateRay / Li "
+                      "= Render, bit for bit (%d pixels)", itype == 0 ? "Whitted C1" : "Path area light", checked);
+        expect(bad == 0, msg);
+    }
+}
+
 int run_gpu() {
     {
         Built b;
@@ -262,6 +386,8 @@ int run_gpu() {
         auto v = std::make_shared<VolPathIntegrator>(10, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 1.f, "uniform", &fb);
         compare("VolPath medium + InfiniteAreaLight", b, v, fb, PBR_INTEGRATOR_VOLPATH, spp, 10, 1.f);
     }
+    scene_queries();
+    decomposed_render_loop();
     return failures ? 1 : 0;
 }
 

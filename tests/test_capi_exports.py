@@ -31,6 +31,8 @@ def test_struct_sizes_match_c():
     assert C.sizeof(capi.Transform) == 128
     assert C.sizeof(capi.Tile) == 16
     assert C.sizeof(capi.RenderStats) == 8 * 8 + 8
+    assert C.sizeof(capi.SurfaceHit) == 112
+    assert C.sizeof(capi.KernelProfile) == 136
 
 
 def test_no_device_returns_error_without_gpu():
@@ -48,3 +50,8 @@ def test_null_arguments_are_rejected():
     assert lib.pbr_hip_upload_scene(None, None) == capi.PBR_E_INVALID
     assert lib.pbr_hip_render(None, None, None, None, None) == capi.PBR_E_INVALID
     assert lib.pbr_hip_destroy(None) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_query(None, 1, None, 0, -1, None) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_bounds(None, -1, None) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_li(None, None, 1, None, None, 0, None) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_set_profiling(None, 1) == capi.PBR_E_INVALID
+    assert lib.pbr_hip_get_profile(None, None, 0, None) == capi.PBR_E_INVALID
