@@ -576,6 +576,12 @@ class SamplerIntegrator : public Integrator {
                              const std::vector<int64_t>& samples, int dimension, const Scene& scene, int depth = 0) const;
     // Extensions: device ordinal; restrict to tiles (multi-GPU sharding); last stats.
     void SetDevice(int device) { this->device = device; }
+    // Multi-GPU Render: the frame's 32×32 tiles are dealt round-robin over these
+    // devices (one context each, frames rendered concurrently), and the per-rank RGBA8 and float
+    // FrameBuffer spans are gathered to the first device with one RCCL ncclGather each (distinct
+    // devices), then scattered into m_FrameBuffer.  A device listed twice gets two contexts and its
+    // spans are copied instead (RCCL needs distinct devices).  Empty: the single-device Render.
+    void SetDevices(const std::vector<int>& devices) { this->devices = devices; }
     void SetTiles(const std::vector<Bounds2i>& tiles) { this->tiles = tiles; }
     const RenderStats& LastStats() const { return stats; }
 
@@ -597,6 +603,10 @@ class SamplerIntegrator : public Integrator {
     mutable pbr_hip_ctx* ctx = nullptr;
     mutable uint64_t uploadedScene = 0;
     mutable const Medium* uploadedCameraMedium = nullptr;
+    std::vector<int> devices;
+    struct MultiGPU;
+    std::shared_ptr<MultiGPU> multi;
+    void RenderMulti(const Scene& scene, double& timeConsume);
 };
 class WhittedIntegrator : public SamplerIntegrator {   // Integrator/WhittedIntegrator.h
   public:
@@ -640,6 +650,17 @@ class VolPathIntegrator : public PathIntegrator {   // Integrator/VolPathIntegra
 using HipWhittedIntegrator = WhittedIntegrator;
 using HipPathIntegrator = PathIntegrator;
 using HipVolPathIntegrator = VolPathIntegrator;
+
+// ---------------------------------------------------------------------------- multi-GPU tiles
+// The partition the multi-GPU Render (and bench.py's ranks) use: TILE×TILE tiles in row-major order,
+// tile i owned by rank i mod world (so the dragon's expensive tiles spread over the GPUs).
+constexpr int kTile = 32;
+std::vector<Bounds2i> TileGrid(int width, int height, int tile = kTile);
+std::vector<Bounds2i> TilesForRank(int width, int height, int rank, int world, int tile = kTile);
+// Scatter a rank's packed span (its tiles in order, each row-major, `channels` values per pixel)
+// into a row-major width-wide frame.
+void AssembleTiles(const std::vector<Bounds2i>& tiles, const uint8_t* packed, int channels, int width, uint8_t* frame);
+void AssembleTiles(const std::vector<Bounds2i>& tiles, const float* packed, int channels, int width, float* frame);
 
 // ---------------------------------------------------------------------------- flattening
 // The scene as the C-ABI takes it (pbr_scene_desc + owned arrays); exposed for tests and for

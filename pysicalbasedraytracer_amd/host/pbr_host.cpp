@@ -13,6 +13,9 @@
 #include <sstream>
 #include <unordered_map>
 
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
 #include "../../include/pbr_hip.h"
 #include "../csrc/pbr_xform.h"
 
@@ -810,6 +813,7 @@ pbr_hip_ctx* helper_ctx() {
 }  // namespace
 
 void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
+    if (!devices.empty()) return RenderMulti(scene, timeConsume);
     auto t0 = std::chrono::steady_clock::now();
     auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
     if (!cam) throw std::invalid_argument("Render: only PerspectiveCamera is on the GPU path");
@@ -1103,6 +1107,207 @@ std::vector<Spectrum> SamplerIntegrator::Li(const std::vector<Ray>& rays, const 
 Spectrum SamplerIntegrator::Li(const RayDifferential& ray, const Scene& scene, Sampler& s, int depth) const {
     return Li(std::vector<Ray>{ray}, std::vector<Point2i>{s.currentPixel}, std::vector<int64_t>{s.currentPixelSampleIndex},
               s.dimension, scene, depth)[0];
+}
+
+// ============================================================================ multi-GPU
+std::vector<Bounds2i> TileGrid(int width, int height, int tile) {
+    std::vector<Bounds2i> t;
+    for (int y = 0; y < height; y += tile)
+        for (int x = 0; x < width; x += tile)
+            t.emplace_back(Point2i(x, y), Point2i(std::min(x + tile, width), std::min(y + tile, height)));
+    return t;
+}
+std::vector<Bounds2i> TilesForRank(int width, int height, int rank, int world, int tile) {
+    std::vector<Bounds2i> all = TileGrid(width, height, tile), mine;
+    for (size_t i = 0; i < all.size(); ++i)
+        if ((int)(i % (size_t)world) == rank) mine.push_back(all[i]);
+    return mine;
+}
+namespace {
+template <class T>
+void assemble(const std::vector<Bounds2i>& tiles, const T* packed, int ch, int width, T* frame) {
+    size_t k = 0;
+    for (const Bounds2i& t : tiles)
+        for (int y = t.pMin.y; y < t.pMax.y; ++y)
+            for (int x = t.pMin.x; x < t.pMax.x; ++x, ++k)
+                std::memcpy(frame + ((size_t)y * width + x) * ch, packed + k * ch, sizeof(T) * ch);
+}
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+void nccl_check(ncclResult_t e, const char* what) {
+    if (e != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(e));
+}
+}  // namespace
+void AssembleTiles(const std::vector<Bounds2i>& tiles, const uint8_t* packed, int ch, int width, uint8_t* frame) {
+    assemble(tiles, packed, ch, width, frame);
+}
+void AssembleTiles(const std::vector<Bounds2i>& tiles, const float* packed, int ch, int width, float* frame) {
+    assemble(tiles, packed, ch, width, frame);
+}
+
+struct SamplerIntegrator::MultiGPU {
+    std::vector<int> devs;
+    int W = 0, H = 0;
+    std::vector<pbr_hip_ctx*> ctx;
+    std::vector<hipStream_t> streams;
+    std::vector<ncclComm_t> comms;          // one per rank when the devices are distinct
+    std::vector<std::vector<Bounds2i>> tiles;
+    std::vector<size_t> npx;
+    size_t maxPx = 0;
+    std::vector<void*> sendU8, sendF32;     // per rank, on its device: maxPx pixels
+    void *recvU8 = nullptr, *recvF32 = nullptr;   // on the first device: world × maxPx pixels
+    std::vector<uint64_t> uploaded;
+    std::vector<const Medium*> uploadedMedium;
+    ~MultiGPU() {
+        for (size_t r = 0; r < ctx.size(); ++r) {
+            (void)hipSetDevice(devs[r]);
+            if (r < streams.size() && streams[r]) (void)hipStreamSynchronize(streams[r]);
+            if (r < sendU8.size() && sendU8[r]) (void)hipFree(sendU8[r]);
+            if (r < sendF32.size() && sendF32[r]) (void)hipFree(sendF32[r]);
+        }
+        for (ncclComm_t c : comms) (void)ncclCommDestroy(c);
+        if (!devs.empty()) {
+            (void)hipSetDevice(devs[0]);
+            if (recvU8) (void)hipFree(recvU8);
+            if (recvF32) (void)hipFree(recvF32);
+        }
+        for (size_t r = 0; r < ctx.size(); ++r) {
+            if (ctx[r]) pbr_hip_destroy(ctx[r]);
+            if (r < streams.size() && streams[r]) { (void)hipSetDevice(devs[r]); (void)hipStreamDestroy(streams[r]); }
+        }
+    }
+};
+
+void SamplerIntegrator::RenderMulti(const Scene& scene, double& timeConsume) {
+    auto t0 = std::chrono::steady_clock::now();
+    auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
+    if (!cam) throw std::invalid_argument("Render: only PerspectiveCamera is on the GPU path");
+    auto* halton = dynamic_cast<const HaltonSampler*>(sampler.get());
+    if (!halton) throw std::invalid_argument("Render: only HaltonSampler is on the GPU path");
+    if (!tiles.empty()) throw std::invalid_argument("Render: SetTiles and SetDevices are exclusive");
+    const int W = pixelBounds.pMax.x, H = pixelBounds.pMax.y;
+    if (W <= 0 || H <= 0 || W > cam->RasterWidth || H > cam->RasterHeight)
+        throw std::invalid_argument("Render: pixelBounds outside the camera raster");
+    if (!m_FrameBuffer || m_FrameBuffer->width != W || m_FrameBuffer->height != H || m_FrameBuffer->channals < 3)
+        throw std::invalid_argument("Render: FrameBuffer not initialised to the pixel bounds");
+    const int world = (int)devices.size();
+    if (!multi || multi->devs != devices || multi->W != W || multi->H != H) {
+        multi.reset();   // release the old set first
+        auto m = std::make_shared<MultiGPU>();
+        m->devs = devices;
+        m->W = W;
+        m->H = H;
+        for (int r = 0; r < world; ++r) {
+            pbr_hip_ctx* c = nullptr;
+            check(nullptr, pbr_hip_create(devices[r], &c), "pbr_hip_create");
+            m->ctx.push_back(c);
+            m->tiles.push_back(TilesForRank(W, H, r, world));
+            size_t n = 0;
+            for (const Bounds2i& t : m->tiles.back()) n += (size_t)(t.pMax.x - t.pMin.x) * (t.pMax.y - t.pMin.y);
+            m->npx.push_back(n);
+            m->maxPx = std::max(m->maxPx, n);
+        }
+        m->uploaded.assign(world, 0);
+        m->uploadedMedium.assign(world, nullptr);
+        for (int r = 0; r < world; ++r) {
+            hip_check(hipSetDevice(devices[r]), "hipSetDevice");
+            hipStream_t st;
+            hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+            m->streams.push_back(st);
+            void *u = nullptr, *f = nullptr;
+            hip_check(hipMalloc(&u, std::max<size_t>(1, m->maxPx) * 4), "hipMalloc");
+            hip_check(hipMalloc(&f, std::max<size_t>(1, m->maxPx) * 12), "hipMalloc");
+            m->sendU8.push_back(u);
+            m->sendF32.push_back(f);
+        }
+        hip_check(hipSetDevice(devices[0]), "hipSetDevice");
+        hip_check(hipMalloc(&m->recvU8, std::max<size_t>(1, m->maxPx) * 4 * world), "hipMalloc");
+        hip_check(hipMalloc(&m->recvF32, std::max<size_t>(1, m->maxPx) * 12 * world), "hipMalloc");
+        std::vector<int> sorted = devices;
+        std::sort(sorted.begin(), sorted.end());
+        if (std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end()) {   // distinct: one RCCL communicator
+            m->comms.resize(world);
+            nccl_check(ncclCommInitAll(m->comms.data(), world, devices.data()), "ncclCommInitAll");
+        }
+        multi = m;
+    }
+    MultiGPU& m = *multi;
+    auto flat = FlattenScene(scene, cam->medium);
+    pbr_render_desc rd;
+    std::memset(&rd, 0, sizeof(rd));
+    rd.integrator = IntegratorType();
+    rd.max_depth = MaxDepth();
+    rd.rr_threshold = RRThreshold();
+    rd.light_strategy = LightStrategy();
+    rd.sampler = PBR_SAMPLER_HALTON;
+    rd.spp = (int)halton->samplesPerPixel;
+    camera_desc(*cam, &rd.camera);
+    rd.camera.medium = MediumIndex(*flat, cam->medium);
+    rd.outputs_on_device = 1;
+    // every rank's frame is enqueued on its own stream (asynchronous: no stats, device outputs)
+    std::vector<std::vector<pbr_tile>> tl(world);
+    for (int r = 0; r < world; ++r) {
+        if (m.uploaded[r] != scene.Id() || m.uploadedMedium[r] != cam->medium) {
+            check(m.ctx[r], pbr_hip_upload_scene(m.ctx[r], SceneDesc(*flat)), "pbr_hip_upload_scene");
+            m.uploaded[r] = scene.Id();
+            m.uploadedMedium[r] = cam->medium;
+        }
+        for (const Bounds2i& b : m.tiles[r]) tl[r].push_back({b.pMin.x, b.pMin.y, b.pMax.x, b.pMax.y});
+        if (tl[r].empty()) continue;   // more ranks than tiles
+        pbr_render_desc rr = rd;
+        rr.n_tiles = (int)tl[r].size();
+        rr.tiles = tl[r].data();
+        rr.stream = m.streams[r];
+        check(m.ctx[r], pbr_hip_render(m.ctx[r], &rr, (float*)m.sendF32[r], (uint8_t*)m.sendU8[r], nullptr), "pbr_hip_render");
+    }
+    // the exchange: rank spans → the first device
+    std::vector<uint8_t> u8((size_t)world * m.maxPx * 4);
+    std::vector<float> f32((size_t)world * m.maxPx * 3);
+    if (!m.comms.empty()) {
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        for (int r = 0; r < world; ++r) {
+            nccl_check(ncclGather(m.sendU8[r], r == 0 ? m.recvU8 : nullptr, m.maxPx * 4, ncclUint8, 0, m.comms[r], m.streams[r]),
+                       "ncclGather");
+            nccl_check(ncclGather(m.sendF32[r], r == 0 ? m.recvF32 : nullptr, m.maxPx * 3, ncclFloat32, 0, m.comms[r],
+                                  m.streams[r]), "ncclGather");
+        }
+        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        for (int r = 0; r < world; ++r) {
+            hip_check(hipSetDevice(devices[r]), "hipSetDevice");
+            hip_check(hipStreamSynchronize(m.streams[r]), "hipStreamSynchronize");
+        }
+        hip_check(hipSetDevice(devices[0]), "hipSetDevice");
+        hip_check(hipMemcpy(u8.data(), m.recvU8, u8.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+        hip_check(hipMemcpy(f32.data(), m.recvF32, f32.size() * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    } else {
+        for (int r = 0; r < world; ++r) {
+            hip_check(hipSetDevice(devices[r]), "hipSetDevice");
+            hip_check(hipStreamSynchronize(m.streams[r]), "hipStreamSynchronize");
+            hip_check(hipMemcpy(&u8[(size_t)r * m.maxPx * 4], m.sendU8[r], m.npx[r] * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+            hip_check(hipMemcpy(&f32[(size_t)r * m.maxPx * 3], m.sendF32[r], m.npx[r] * 12, hipMemcpyDeviceToHost), "hipMemcpy");
+        }
+    }
+    for (int r = 0; r < world; ++r) check(m.ctx[r], pbr_hip_sync(m.ctx[r]), "pbr_hip_sync");   // deferred failures
+    // scatter into the row-major frame, then into the FrameBuffer (flipped, Integrator.cpp:341-344)
+    std::vector<uint8_t> frameU8((size_t)W * H * 4);
+    std::vector<float> frameF((size_t)W * H * 3);
+    for (int r = 0; r < world; ++r) {
+        AssembleTiles(m.tiles[r], &u8[(size_t)r * m.maxPx * 4], 4, W, frameU8.data());
+        AssembleTiles(m.tiles[r], &f32[(size_t)r * m.maxPx * 3], 3, W, frameF.data());
+    }
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+            for (int ch = 0; ch < m_FrameBuffer->channals; ++ch) {
+                const size_t k = (size_t)y * W + x;
+                m_FrameBuffer->set_uc(x, H - y - 1, ch, frameU8[4 * k + ch]);
+                m_FrameBuffer->set_fc(x, H - y - 1, ch, ch < 3 ? frameF[3 * k + ch] : 1.f);
+            }
+    stats.samples = (uint64_t)W * H * (uint64_t)rd.spp;
+    timeConsume = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    stats.seconds = timeConsume;
+    stats.kernel_ms = 0;
+    IntegratorRenderTime = (float)timeConsume;
 }
 
 }  // namespace PBR

@@ -6,6 +6,7 @@
 //   host_api_test gpu   renders through WhittedIntegrator / PathIntegrator / VolPathIntegrator on
 //                       the GPU and compares the FrameBuffer with the oracle (L∞ ≤ 1e-3; u8 identical where the float pixel is, else ≤ 1)
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -14,6 +15,7 @@
 
 #include "../../include/pbr/pbr.h"
 #include "../../include/pbr_hip.h"
+#include <hip/hip_runtime_api.h>
 #include "../../oracle/pbr_oracle.h"
 
 using namespace PBR;
@@ -211,6 +213,32 @@ int run_cpu() {
         std::printf("     (%s)\n", e.what());
     }
     expect(threw, "Render without a GPU throws from pbr_hip_create");
+    // multi-GPU partition and assembly: every pixel in exactly one rank's tiles, tile i on rank
+    // i mod world, and the packed spans scatter back to the frame
+    {
+        const int W = 100, H = 70, world = 3;
+        std::vector<int> owner(W * H, -1);
+        std::vector<uint32_t> frame(W * H, 0);
+        bool ok = TileGrid(W, H).size() == 4 * 3;
+        std::vector<Bounds2i> all = TileGrid(W, H);
+        for (int r = 0; r < world; ++r) {
+            std::vector<Bounds2i> mine = TilesForRank(W, H, r, world);
+            std::vector<uint32_t> packed;
+            for (size_t i = 0; i < mine.size(); ++i) {
+                const Bounds2i& t = mine[i];
+                ok &= t.pMin.x == all[r + i * world].pMin.x && t.pMin.y == all[r + i * world].pMin.y;
+                for (int y = t.pMin.y; y < t.pMax.y; ++y)
+                    for (int x = t.pMin.x; x < t.pMax.x; ++x) {
+                        ok &= owner[y * W + x] < 0;
+                        owner[y * W + x] = r;
+                        packed.push_back((uint32_t)(y * W + x));
+                    }
+            }
+            AssembleTiles(mine, reinterpret_cast<const uint8_t*>(packed.data()), 4, W, reinterpret_cast<uint8_t*>(frame.data()));
+        }
+        for (int k = 0; k < W * H; ++k) ok &= owner[k] >= 0 && frame[k] == (uint32_t)k;
+        expect(ok, "TilesForRank deals 32x32 tiles round-robin, covering the frame once; AssembleTiles restores it");
+    }
     Matrix4x4 m(2, 0, 0, 1, 0, 3, 0, 2, 0, 0, 4, 3, 0, 0, 0, 1);
     Matrix4x4 p = Mul(m, Inverse(m));
     bool ident = true;
@@ -344,6 +372,38 @@ void decomposed_render_loop() {
     }
 }
 
+// SetDevices: tiles dealt over devices, spans gathered (RCCL over distinct devices; a repeated
+// device gets its own context and a copy) — the FrameBuffer equals the single-device Render's.
+void multi_gpu_render() {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    std::vector<std::vector<int>> sets = {{0}, {0, 0}, {0, 0, 0}};
+    if (ndev >= 2) sets.push_back({0, 1});
+    Built b;
+    const int W = 77, H = 45, spp = 4;
+    build_area(b, W, H, false);
+    FrameBuffer ref, fb;
+    ref.InitBuffer(W, H, 4);
+    fb.InitBuffer(W, H, 4);
+    auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+    PathIntegrator single(6, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &ref);
+    double t = 0;
+    single.Render(*b.scene, t);
+    for (const auto& devs : sets) {
+        PathIntegrator multi(6, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &fb);
+        multi.SetDevices(devs);
+        std::memset(fb.getUCbuffer(), 0, (size_t)W * H * 4);
+        multi.Render(*b.scene, t);
+        multi.Render(*b.scene, t);   // a second frame reuses contexts, buffers and communicator
+        const bool same = std::memcmp(fb.getUCbuffer(), ref.getUCbuffer(), (size_t)W * H * 4) == 0 &&
+                          std::memcmp(fb.getFCbuffer(), ref.getFCbuffer(), (size_t)W * H * 4 * sizeof(float)) == 0;
+        std::string d;
+        for (int x : devs) d += std::to_string(x) + " ";
+        expect(same, "multi-GPU Render over devices { " + d + "}" + (devs.size() == 1 || devs[0] != devs[1] ? " (RCCL gather)" : " (copies)") +
+                         " = single-device Render, bit for bit");
+    }
+}
+
 int run_gpu() {
     {
         Built b;
@@ -388,6 +448,7 @@ int run_gpu() {
     }
     scene_queries();
     decomposed_render_loop();
+    multi_gpu_render();
     return failures ? 1 : 0;
 }
 
@@ -418,6 +479,12 @@ int main(int argc, char** argv) {
     std::string mode = argc > 1 ? argv[1] : "cpu";
     try {
         if (mode == "png") return run_png(argc > 2 ? argv[2] : "host_api_test.png");
+        if (mode == "tiles" && argc > 4) {   // tiles W H world: one "rank x0 y0 x1 y1" line per tile
+            const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), world = std::atoi(argv[4]);
+            for (int r = 0; r < world; ++r)
+                for (const Bounds2i& t : TilesForRank(W, H, r, world)) std::printf("%d %d %d %d %d\n", r, t.pMin.x, t.pMin.y, t.pMax.x, t.pMax.y);
+            return 0;
+        }
         int rc = mode == "gpu" ? run_gpu() : run_cpu();
         std::printf("%s: %d failure(s)\n", mode.c_str(), failures);
         return rc;
