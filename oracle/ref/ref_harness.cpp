@@ -68,6 +68,7 @@
 #include "Media\HomogeneousMedium.h"
 #include "Sampler\Halton.h"
 #include "Shape\Triangle.h"
+#include "Shape\plyRead.h"
 #include "Texture\ConstantTexture.h"
 
 #include "../../include/pbr_hip.h"
@@ -490,6 +491,25 @@ int ref_camera_rays(const pbr_camera_desc* cd, int n, const float* pfilm, float*
         return PBR_OK;
     } catch (const std::exception& e) {
         return fail(e);
+    }
+}
+
+// Shape/plyRead.h:22-47: the reference's ".3d" reader (vertices ×20); pass NULL arrays for counts.
+int ref_ply_info(const char* path, int* n_vertices, int* n_triangles, float* verts, int32_t* indices) {
+    try {
+        PBR::plyInfo info(path);
+        *n_vertices = info.nVertices;
+        *n_triangles = info.nTriangles;
+        if (verts)
+            for (int i = 0; i < info.nVertices; ++i)
+                for (int k = 0; k < 3; ++k) verts[3 * i + k] = info.vertexArray[i][k];
+        if (indices)
+            for (int i = 0; i < 3 * info.nTriangles; ++i) indices[i] = info.vertexIndices[i];
+        delete[] info.vertexArray;
+        delete[] info.vertexIndices;
+        return 0;
+    } catch (...) {
+        return -1;
     }
 }
 

@@ -479,6 +479,19 @@ int main(int argc, char** argv) {
     std::string mode = argc > 1 ? argv[1] : "cpu";
     try {
         if (mode == "png") return run_png(argc > 2 ? argv[2] : "host_api_test.png");
+        if ((mode == "ply3d" || mode == "ply") && argc > 2) {   // mesh readers: "v <hex x> <hex y> <hex z>", "f a b c"
+            std::vector<Point3f> v;
+            std::vector<int> idx;
+            if (mode == "ply3d") { plyInfo info(argv[2]); v = info.vertexArray; idx = info.vertexIndices; }
+            else { PlyMesh m = LoadPLY(argv[2]); v = m.vertices; idx = m.indices; }
+            for (const Point3f& p : v) {
+                uint32_t b[3];
+                std::memcpy(&b[0], &p.x, 4); std::memcpy(&b[1], &p.y, 4); std::memcpy(&b[2], &p.z, 4);
+                std::printf("v %08x %08x %08x\n", b[0], b[1], b[2]);
+            }
+            for (size_t k = 0; k + 2 < idx.size(); k += 3) std::printf("f %d %d %d\n", idx[k], idx[k + 1], idx[k + 2]);
+            return 0;
+        }
         if (mode == "tiles" && argc > 4) {   // tiles W H world: one "rank x0 y0 x1 y1" line per tile
             const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), world = std::atoi(argv[4]);
             for (int r = 0; r < world; ++r)

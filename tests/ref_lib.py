@@ -36,6 +36,7 @@ def load():
     lib.ref_build_bvh.argtypes = [P(capi.SceneDesc), C.c_void_p, P(C.c_int), P(C.c_int32), P(C.c_int)]
     lib.ref_intersect.argtypes = [P(capi.SceneDesc), C.c_int, P(C.c_float), P(C.c_float), C.c_int]
     lib.ref_camera_rays.argtypes = [P(capi.CameraDesc), C.c_int, P(C.c_float), P(C.c_float)]
+    lib.ref_ply_info.argtypes = [C.c_char_p, P(C.c_int), P(C.c_int), C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
 
@@ -94,3 +95,13 @@ def camera_rays(cam, pfilm):
     out = np.empty((pf.shape[0], 6), np.float32)
     assert load().ref_camera_rays(C.byref(cam), pf.shape[0], capi.fptr(pf), capi.fptr(out)) == 0
     return out
+
+
+def ply_info(path):
+    """The reference's .3d reader (Shape/plyRead.h plyInfo): (vertices float32 [n,3] ×20, indices int32 [m,3])."""
+    nv, nt = C.c_int(), C.c_int()
+    assert load().ref_ply_info(path.encode(), C.byref(nv), C.byref(nt), None, None) == 0
+    v = np.empty((nv.value, 3), np.float32)
+    i = np.empty((nt.value, 3), np.int32)
+    assert load().ref_ply_info(path.encode(), C.byref(nv), C.byref(nt), v.ctypes.data, i.ctypes.data) == 0
+    return v, i
