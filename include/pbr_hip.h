@@ -295,6 +295,22 @@ int pbr_hip_bounds(pbr_hip_ctx* ctx, int prim, float* out6);
 int pbr_hip_li(pbr_hip_ctx* ctx, const pbr_render_desc* desc, int n, const float* rays,
                const int32_t* px_py_sample_dim, int depth, float* rgb_out);
 
+/* ---- BVH construction (BVHAccel::BVHAccel, Accelerator/BVHAccel.cpp:57-87; SAH recursiveBuild
+ * :97-260; flattenBVHTree :262-283) ----
+ * Both builders produce the reference's node array and orderedPrims exactly (the host one is the
+ * sequential algorithm; the device one, pbr_bvh_build.hip, reproduces its partitions level by level). */
+enum pbr_bvh_build { PBR_BVH_BUILD_HOST = 0, PBR_BVH_BUILD_DEVICE = 1 };
+/* Which builder pbr_hip_upload_scene runs (default PBR_BVH_BUILD_DEVICE). */
+int pbr_hip_set_bvh_build(pbr_hip_ctx* ctx, int where);
+/* The last upload's build: builder, wall ms (device: incl. the bounds upload and node download),
+ * device kernel ms (0 for the host builder). */
+int pbr_hip_bvh_build_info(pbr_hip_ctx* ctx, int* where, double* ms, double* kernel_ms);
+/* Standalone build over n primitive world bounds (6 floats each, lo.xyz hi.xyz, prims order:
+ * GeometricPrimitive::WorldBound): nodes_out has room for 2n-1 32-B LinearBVHNodes, prim_ids_out for
+ * n ids; ms_out (optional, 2 doubles) = {wall ms, device kernel ms}. */
+int pbr_hip_build_bvh(pbr_hip_ctx* ctx, int where, int n, const float* prim_bounds, int max_prims,
+                      void* nodes_out, int* n_nodes, int32_t* prim_ids_out, double* ms_out);
+
 /* Device build info: ABI version, gfx arch string. */
 int pbr_hip_abi_version(void);
 const char* pbr_hip_build_info(void);

@@ -109,6 +109,30 @@ class HipRenderer:
                     "get_bvh")
         return nodes, ids
 
+    def set_bvh_build(self, where: int):
+        """Which SAH builder the next upload runs: capi.BVH_BUILD_DEVICE (default) or BVH_BUILD_HOST."""
+        self._check(self.lib.pbr_hip_set_bvh_build(self.ctx, where), "set_bvh_build")
+
+    def bvh_build_info(self) -> dict:
+        """The last upload's BVH build: builder, wall ms, device kernel ms (pbr_hip_bvh_build_info)."""
+        w, ms, kms = C.c_int(), C.c_double(), C.c_double()
+        self._check(self.lib.pbr_hip_bvh_build_info(self.ctx, C.byref(w), C.byref(ms), C.byref(kms)), "bvh_build_info")
+        return {"where": "device" if w.value == capi.BVH_BUILD_DEVICE else "host", "ms": ms.value,
+                "kernel_ms": kms.value}
+
+    def build_bvh(self, prim_bounds, where=capi.BVH_BUILD_DEVICE, max_prims=1):
+        """BVHAccel's SAH build over [n, 6] primitive world bounds (pbr_hip_build_bvh): returns
+        (LinearBVHNode bytes [n_nodes*32], ordered prim ids, {"ms", "kernel_ms"})."""
+        b = np.ascontiguousarray(prim_bounds, dtype=np.float32).reshape(-1, 6)
+        n = b.shape[0]
+        nodes = np.zeros(max(1, 2 * n - 1) * 32, dtype=np.uint8)
+        ids = np.zeros(max(1, n), dtype=np.int32)
+        nn = C.c_int()
+        ms = (C.c_double * 2)()
+        self._check(self.lib.pbr_hip_build_bvh(self.ctx, where, n, capi.fptr(b), max_prims, nodes.ctypes.data,
+                                                C.byref(nn), capi.iptr(ids), ms), "build_bvh")
+        return nodes[:nn.value * 32], ids[:n], {"ms": ms[0], "kernel_ms": ms[1]}
+
     def sampler_values(self, width, height, spp, queries, sampler=capi.SAMPLER_HALTON):
         q = np.ascontiguousarray(queries, dtype=np.int32).reshape(-1, 4)
         out = np.empty(q.shape[0], dtype=np.float32)

@@ -23,6 +23,7 @@ LIGHT_POINT, LIGHT_DIFFUSE_AREA, LIGHT_SKYBOX, LIGHT_INFINITE_AREA = 0, 1, 2, 3
 INTEGRATOR_WHITTED, INTEGRATOR_PATH, INTEGRATOR_VOLPATH = 0, 1, 2
 SAMPLER_HALTON, SAMPLER_SOBOL = 0, 1
 LIGHTS_UNIFORM, LIGHTS_POWER = 0, 1
+BVH_BUILD_HOST, BVH_BUILD_DEVICE = 0, 1
 
 F3 = C.c_float * 3
 F16 = C.c_float * 16
@@ -208,6 +209,11 @@ EXPORTS = {
                              C.c_int, C.POINTER(C.c_float)]),
     "pbr_hip_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "pbr_hip_get_profile": (C.c_int, [C.c_void_p, C.POINTER(KernelProfile), C.c_int, C.POINTER(C.c_int)]),
+    "pbr_hip_set_bvh_build": (C.c_int, [C.c_void_p, C.c_int]),
+    "pbr_hip_bvh_build_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                         C.POINTER(C.c_double)]),
+    "pbr_hip_build_bvh": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_int, C.c_void_p,
+                                    C.POINTER(C.c_int), C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
 }
 
 PACKAGE_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -217,7 +223,7 @@ _lib = None
 
 
 OPTIONAL_FOR_AB = ("pbr_hip_sync", "pbr_hip_set_profiling", "pbr_hip_get_profile", "pbr_hip_query", "pbr_hip_bounds",
-                   "pbr_hip_li")
+                   "pbr_hip_li", "pbr_hip_set_bvh_build", "pbr_hip_bvh_build_info", "pbr_hip_build_bvh")
 
 
 def load_library(path: str | None = None) -> C.CDLL:

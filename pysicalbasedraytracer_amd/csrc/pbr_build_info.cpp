@@ -1,0 +1,8 @@
+// pbr_build_info.cpp — pbr_hip_build_info(): the content hash of the library's sources (Makefile
+// SRC_HASH), which ties PMC summaries and bench lines to a build.  Rebuilt whenever any source changes.
+#include "../../include/pbr_hip.h"
+
+#ifndef PBR_SRC_HASH
+#define PBR_SRC_HASH "unknown"
+#endif
+extern "C" const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 wavefront+megakernel src " PBR_SRC_HASH; }

@@ -818,6 +818,8 @@ struct pbr_hip_ctx {
     size_t profUsed = 0;
     DevBuf dProf;
     unsigned long long profHost[KP_COUNT][kProfFields] = {};
+    int bvhBuild = PBR_BVH_BUILD_DEVICE; // which SAH builder pbr_hip_upload_scene runs
+    double bvhMs = 0, bvhKernelMs = 0;   // the last upload's BVH build: wall / device time
     DevBuf dGuard;                       // DeviceScene::guard (kGuard* bits of tripped safety bounds)
     int* guardHost = nullptr;            // pinned copy, refreshed at the end of frames that can trip one
 };
@@ -1521,10 +1523,49 @@ int pbr_hip_li(pbr_hip_ctx* ctx, const pbr_render_desc* d, int n, const float* r
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return check_guard(ctx);
 }
-#ifndef PBR_SRC_HASH
-#define PBR_SRC_HASH "unknown"
-#endif
-const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 wavefront+megakernel src " PBR_SRC_HASH; }
+
+int pbr_hip_set_bvh_build(pbr_hip_ctx* ctx, int where) {
+    if (!ctx || (where != PBR_BVH_BUILD_HOST && where != PBR_BVH_BUILD_DEVICE)) return PBR_E_INVALID;
+    ctx->bvhBuild = where;
+    return PBR_OK;
+}
+
+int pbr_hip_bvh_build_info(pbr_hip_ctx* ctx, int* where, double* ms, double* kernel_ms) {
+    if (!ctx) return PBR_E_INVALID;
+    if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    if (where) *where = ctx->bvhBuild;
+    if (ms) *ms = ctx->bvhMs;
+    if (kernel_ms) *kernel_ms = ctx->bvhKernelMs;
+    return PBR_OK;
+}
+
+int pbr_hip_build_bvh(pbr_hip_ctx* ctx, int where, int n, const float* prim_bounds, int max_prims, void* nodes_out,
+                      int* n_nodes, int32_t* prim_ids_out, double* ms_out) {
+    if (!ctx || n < 0 || (n > 0 && !prim_bounds) || !nodes_out || !n_nodes || (n > 0 && !prim_ids_out) ||
+        (where != PBR_BVH_BUILD_HOST && where != PBR_BVH_BUILD_DEVICE))
+        return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    std::vector<float> pb(prim_bounds, prim_bounds + (size_t)n * 6);
+    std::vector<LinearBVHNode> nodes;
+    std::vector<int32_t> ids;
+    double kms = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        if (where == PBR_BVH_BUILD_DEVICE) device_build_bvh(ctx->stream, pb, max_prims > 0 ? max_prims : 1, &nodes, &ids, &kms);
+        else host_build_bvh(pb, max_prims > 0 ? max_prims : 1, &nodes, &ids);
+    } catch (const std::invalid_argument& e) {
+        return set_err(ctx, PBR_E_INVALID, e.what());
+    } catch (const std::exception& e) {
+        return set_err(ctx, PBR_E_HIP, e.what());
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms_out) { ms_out[0] = ms; ms_out[1] = kms; }
+    *n_nodes = (int)nodes.size();
+    if (!nodes.empty()) std::memcpy(nodes_out, nodes.data(), nodes.size() * sizeof(LinearBVHNode));
+    if (!ids.empty()) std::memcpy(prim_ids_out, ids.data(), ids.size() * 4);
+    return PBR_OK;
+}
 
 int pbr_hip_sobol_matrices(int dims, uint32_t* out) {
     if (dims < 1 || dims > kSobolMaxDims || !out) return PBR_E_INVALID;
@@ -1603,10 +1644,21 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = drain(ctx)) return rc;
     try {
-        build_host_scene(desc, &ctx->host);
-    } catch (const std::exception& e) {
+        ctx->bvhMs = ctx->bvhKernelMs = 0;
+        BvhBuildFn timed = [ctx](const std::vector<float>& pb, int maxPrims, std::vector<LinearBVHNode>* nodes,
+                                 std::vector<int32_t>* ids) {
+            const auto t0 = std::chrono::steady_clock::now();
+            if (ctx->bvhBuild == PBR_BVH_BUILD_DEVICE) device_build_bvh(ctx->stream, pb, maxPrims, nodes, ids, &ctx->bvhKernelMs);
+            else host_build_bvh(pb, maxPrims, nodes, ids);
+            ctx->bvhMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        };
+        build_host_scene(desc, &ctx->host, &timed);
+    } catch (const std::invalid_argument& e) {
         ctx->haveScene = false;
         return set_err(ctx, PBR_E_INVALID, e.what());
+    } catch (const std::exception& e) {
+        ctx->haveScene = false;
+        return set_err(ctx, PBR_E_HIP, e.what());
     }
     const HostScene& h = ctx->host;
     HIP_TRY(hipMemsetAsync(ctx->dGuard.p, 0, sizeof(int), ctx->stream));

@@ -439,7 +439,21 @@ void distribution1d(const std::vector<float>& f, std::vector<float>* cdf, float*
 
 }  // namespace
 
-void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
+void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
+                    std::vector<int32_t>* primIds) {
+    const size_t np = primBounds.size() / 6;
+    std::vector<Item> items(np);
+    for (size_t i = 0; i < np; ++i) {   // BVHPrimitiveInfo (BVHAccel.cpp:24-31)
+        const float* p = &primBounds[i * 6];
+        items[i].id = i;
+        items[i].box.lo = mk(p[0], p[1], p[2]);
+        items[i].box.hi = mk(p[3], p[4], p[5]);
+        items[i].c = .5f * items[i].box.lo + .5f * items[i].box.hi;
+    }
+    SahBuilder(items, maxPrims, nodes, primIds).run();
+}
+
+void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* bvh) {
     if (!d) fail("null scene");
     if (d->abi_version != PBR_HIP_ABI_VERSION) fail("abi_version mismatch");
     if (d->n_shapes < 0 || (d->n_shapes > 0 && !d->shapes)) fail("bad shapes");
@@ -492,7 +506,6 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
         return world[p.shape][sd.indices[3 * p.tri + k]];
     };
     // 2. SAH BVH over primitive world bounds
-    std::vector<Item> items(np);
     S->primBounds.clear();
     S->primBounds.reserve((size_t)np * 6);
     for (int i = 0; i < np; ++i) {
@@ -511,12 +524,12 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S) {
             b.lo = c0; b.hi = c0;
             for (int k = 1; k < 8; ++k) b.add(xf_point(r.o2w, corners[k]));
         }
-        items[i].id = (size_t)i;
-        items[i].box = b;
         S->primBounds.insert(S->primBounds.end(), {b.lo.x, b.lo.y, b.lo.z, b.hi.x, b.hi.y, b.hi.z});
-        items[i].c = .5f * b.lo + .5f * b.hi;
     }
-    SahBuilder(items, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1, &S->nodes, &S->primIds).run();
+    const int maxPrims = d->max_prims_in_node > 0 ? d->max_prims_in_node : 1;
+    if (bvh) (*bvh)(S->primBounds, maxPrims, &S->nodes, &S->primIds);
+    else host_build_bvh(S->primBounds, maxPrims, &S->nodes, &S->primIds);
+    if (S->primIds.size() != (size_t)np) fail("BVH build returned a wrong primitive count");
     // 3. primitive payloads in BVH order
     std::vector<int>& slotOf = S->slotOf;
     slotOf.assign(np, -1);

@@ -1,5 +1,6 @@
 // pbr_scene.h — host-side flattening of a pbr_scene_desc into the HBM layout of pbr_layout.h.
 #pragma once
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -61,8 +62,19 @@ struct HostScene {
 // to powers of two as Texture/MIPMap.h:86-150 does) and the Distribution2D over its luminance.
 void build_infinite_light(const pbr_light_desc& ld, const float worldMin[3], const float worldMax[3],
                           InfiniteHost* out, float power[3]);
-// Throws std::invalid_argument on a malformed descriptor.
-void build_host_scene(const pbr_scene_desc* desc, HostScene* out);
+// BVHAccel's SAH build (BVHAccel.cpp:57-283) over primitive world bounds (6 floats per primitive in
+// prims order): LinearBVHNode array in flatten order + orderedPrims ids.  The host builder
+// (pbr_scene.cpp) and the device builder (pbr_bvh_build.hip, on `stream`; device time in kernelMs;
+// throws std::runtime_error on a HIP failure) produce identical arrays.
+void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
+                    std::vector<int32_t>* primIds);
+void device_build_bvh(void* stream, const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
+                      std::vector<int32_t>* primIds, double* kernelMs);
+using BvhBuildFn = std::function<void(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
+                                      std::vector<int32_t>* primIds)>;
+
+// Throws std::invalid_argument on a malformed descriptor.  `bvh` replaces the host SAH build.
+void build_host_scene(const pbr_scene_desc* desc, HostScene* out, const BvhBuildFn* bvh = nullptr);
 
 // Light sampling distribution (Distribution1D over lights): uniform or power.
 void light_distribution(const HostScene& s, int strategy, std::vector<float>* cdf, std::vector<float>* func,

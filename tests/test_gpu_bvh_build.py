@@ -1,0 +1,110 @@
+"""The device SAH build (pbr_bvh_build.hip) against the host builder, which the reference pins
+(tests/test_ref_fixtures.py: node-array and orderedPrims hashes of the reference's own BVHAccel).
+
+Bit for bit: the LinearBVHNode array (BVHAccel.cpp:262-283) and orderedPrims (:107-112) — over random
+boxes, tie-heavy grids with +-0 coordinates (the first element of a tie wins Union's std::min/max),
+coincident centroids (the degenerate leaf, :121-130), two-element nodes (nth_element), leaf sizes
+1/4/255, the 100k-triangle C2 stand-in and an 871k-triangle (real-dragon-sized) one.
+"""
+import numpy as np
+import pytest
+
+from pysicalbasedraytracer_amd import HipRenderer, capi, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    r = HipRenderer(0)
+    yield r
+    r.close()
+
+
+def both(hip, b, max_prims=1):
+    dn, di, dt = hip.build_bvh(b, capi.BVH_BUILD_DEVICE, max_prims)
+    hn, hi, ht = hip.build_bvh(b, capi.BVH_BUILD_HOST, max_prims)
+    assert np.array_equal(di, hi), "orderedPrims differ"
+    assert np.array_equal(dn, hn), "LinearBVHNode arrays differ"
+    return dn, di, dt, ht
+
+
+def boxes_from_points(lo, ext):
+    return np.concatenate([lo, lo + ext], axis=1).astype(np.float32)
+
+
+def mesh_bounds(P, I):
+    v = P[I]                       # [n, 3, 3]
+    lo = np.minimum(np.minimum(v[:, 0], v[:, 1]), v[:, 2])
+    hi = np.maximum(np.maximum(v[:, 0], v[:, 1]), v[:, 2])
+    return np.concatenate([lo, hi], axis=1).astype(np.float32)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 17, 64, 65, 1000, 20000])
+def test_random_boxes(hip, n):
+    rng = np.random.default_rng(n)
+    b = boxes_from_points(rng.normal(size=(n, 3)), rng.random((n, 3)) * 0.1)
+    dn, di, _, _ = both(hip, b)
+    assert dn.size == max(0, 2 * n - 1) * 32
+    assert sorted(di.tolist()) == list(range(n))
+
+
+@pytest.mark.parametrize("max_prims", [1, 4, 255])
+def test_leaf_sizes(hip, max_prims):
+    rng = np.random.default_rng(7)
+    b = boxes_from_points(rng.random((5000, 3)) * 10, rng.random((5000, 3)))
+    both(hip, b, max_prims)
+
+
+def test_ties_and_signed_zeros(hip):
+    rng = np.random.default_rng(11)
+    n = 6000
+    lo = rng.integers(-2, 3, size=(n, 3)).astype(np.float32) * 0.5
+    ext = rng.integers(0, 3, size=(n, 3)).astype(np.float32) * 0.5
+    hi = lo + ext
+    # signed zeros: -0.0 and +0.0 compare equal, so which one a union keeps depends on the order
+    z = rng.random((n, 3)) < 0.5
+    lo[(lo == 0) & z] = -0.0
+    hi[(hi == 0) & ~z] = -0.0
+    b = np.concatenate([lo, hi], axis=1).astype(np.float32)
+    dn, _, _, _ = both(hip, b)
+    for mp in (2, 8):
+        both(hip, b, mp)
+
+
+def test_coincident_centroids(hip):
+    # all centroids equal → one leaf holding everything (BVHAccel.cpp:121-130)
+    b = np.tile(np.array([[-1, -1, -1, 1, 1, 1]], np.float32), (200, 1))
+    b[::3, :3] -= 0.25
+    b[::3, 3:] += 0.25
+    dn, di, _, _ = both(hip, b)
+    nodes = dn.view(np.int32).reshape(-1, 8)
+    assert nodes.shape[0] == 1 and (nodes[0, 7] & 0xffff) == 200
+    # a cluster of coincident centroids inside a larger set
+    rng = np.random.default_rng(3)
+    c = boxes_from_points(rng.random((300, 3)), rng.random((300, 3)) * 0.01)
+    c[100:180] = c[100]
+    both(hip, c)
+
+
+@pytest.mark.parametrize("n", [224, 660])
+def test_dragon_standins(hip, n):
+    P, I = scenes.dragon_standin(n=n)
+    b = mesh_bounds(P, I)
+    _, _, dt, ht = both(hip, b)
+    print(f"\n{I.shape[0]} triangles: host build {ht['ms']:.1f} ms, device build {dt['ms']:.1f} ms "
+          f"({dt['kernel_ms']:.1f} ms of kernels)")
+
+
+def test_upload_with_either_builder(hip):
+    s, _ = scenes.config_c2(64, 36, 1, sky=np.ones((8, 16, 3), np.float32))
+    got = {}
+    for where in (capi.BVH_BUILD_HOST, capi.BVH_BUILD_DEVICE):
+        hip.set_bvh_build(where)
+        hip.upload(s)
+        info = hip.bvh_build_info()
+        assert info["where"] == ("device" if where == capi.BVH_BUILD_DEVICE else "host")
+        assert info["ms"] > 0 and (info["kernel_ms"] > 0) == (where == capi.BVH_BUILD_DEVICE)
+        got[where] = hip.get_bvh()
+    hip.set_bvh_build(capi.BVH_BUILD_DEVICE)
+    assert np.array_equal(got[0][0], got[1][0]) and np.array_equal(got[0][1], got[1][1])
