@@ -188,6 +188,46 @@ class ConstantTexture : public Texture<T> {
     T value;
 };
 
+using RGBSpectrum = Spectrum;
+
+// Texture/Texture.h:9-27, Texture/MIPMap.h:21, Texture/ImageTexture.h:43-91
+enum class ImageWrap { Repeat, Black, Clamp };
+class TextureMapping2D {
+  public:
+    virtual ~TextureMapping2D() = default;
+};
+class UVMapping2D : public TextureMapping2D {
+  public:
+    UVMapping2D(float su = 1, float sv = 1, float du = 0, float dv = 0) : su(su), sv(sv), du(du), dv(dv) {}
+    const float su, sv, du, dv;
+};
+// The image of an ImageTexture, as its loadImage (stbi_loadf with flip-on-load) hands it over.
+struct ImageTextureData {
+    const UVMapping2D* mapping = nullptr;   // nullptr: a mapping other than UVMapping2D (refused by the GPU path)
+    int width = 0, height = 0, components = 0;
+    std::vector<float> data;                // empty → GetTexture's 0.5 grey image
+    bool doTrilinear = false, gamma = false, isFloat = false;
+    float maxAniso = 8.f, scale = 1.f;
+    ImageWrap wrapMode = ImageWrap::Repeat;
+};
+template <typename Tmemory, typename Treturn>
+class ImageTexture : public Texture<Treturn> {
+  public:
+    // Loads `filename` as loadImage does: a Radiance .hdr read the way stbi_loadf reads it, rows
+    // flipped (stbi_set_flip_vertically_on_load(true), ImageTexture.cpp:19); a missing or unreadable
+    // file gives the 0.5 grey image (ImageTexture.cpp:60-66).
+    ImageTexture(std::unique_ptr<TextureMapping2D> mapping, const std::string& filename, bool doTrilinear, float maxAniso,
+                 ImageWrap wrapMode, float scale, bool gamma);
+    // In-memory variant: data = width*height*components floats in stbi_loadf's (flipped) row order.
+    ImageTexture(std::unique_ptr<TextureMapping2D> mapping, int width, int height, int components, std::vector<float> data,
+                 bool doTrilinear, float maxAniso, ImageWrap wrapMode, float scale, bool gamma);
+    const ImageTextureData& Image() const { return img; }
+
+  private:
+    std::unique_ptr<TextureMapping2D> mapping;
+    ImageTextureData img;
+};
+
 // ---------------------------------------------------------------------------- Media/
 class Medium {
   public:

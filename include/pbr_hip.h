@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PBR_HIP_ABI_VERSION 2
+#define PBR_HIP_ABI_VERSION 3
 
 /* ---- status codes ---- */
 enum {
@@ -110,6 +110,40 @@ typedef struct pbr_shape_desc {
     int medium_outside;
 } pbr_shape_desc;
 
+/* ImageTexture<RGBSpectrum, Spectrum> / <float, float> (Texture/ImageTexture.h:43-91,
+ * ImageTexture.cpp:13-92) with a UVMapping2D (Texture/Texture.h:16-27).  The reference's ray
+ * differentials are zero (dudx = dvdx = 0, F5), so both MIPMap filters — trilinear (MIPMap.h:193-211)
+ * and EWA (:227-247) — reduce to the bilinear level-0 lookup triangle(0, st) (:240-252); the pyramid
+ * above level 0 is never read.  Level 0 is the image resampled to powers of two with the texture's
+ * wrap mode (MIPMap.h:86-150). */
+enum pbr_image_wrap { PBR_WRAP_REPEAT = 0, PBR_WRAP_BLACK = 1, PBR_WRAP_CLAMP = 2 };   /* ImageWrap, MIPMap.h:21 */
+typedef struct pbr_texture_desc {
+    int is_float;               /* 1: ImageTexture<float, float> (convertIn: scale * y()), 0: RGB */
+    int width, height, components;
+    const float* data;          /* as loadImage's stbi_loadf returns it (flip-on-load set); NULL →
+                                 * the 1x1 grey 0.5 image GetTexture substitutes (ImageTexture.cpp:60-66) */
+    float scale;
+    int gamma;                  /* convertIn applies InverseGammaCorrect (Core/PBR.h:126-129) */
+    int wrap;                   /* pbr_image_wrap */
+    int trilinear;              /* doTrilinear (no effect, see above) */
+    float max_aniso;            /* maxAniso (no effect, see above) */
+    float su, sv, du, dv;       /* UVMapping2D(su, sv, du, dv): st = (su·u + du, sv·v + dv) */
+} pbr_texture_desc;
+
+/* Material parameter slots that may hold an image texture instead of the constant below
+ * (pbr_material_desc.tex[slot] = index into pbr_scene_desc.textures + 1; 0 = the constant, so a
+ * zero-initialised descriptor has no textures).  RGB slots need an RGB texture, scalar slots a
+ * float one. */
+enum pbr_texture_slot {
+    PBR_TEX_KD = 0,             /* matte / plastic Kd (RGB) */
+    PBR_TEX_KS = 1,             /* plastic Ks (RGB) */
+    PBR_TEX_KR = 2,             /* mirror / glass Kr (RGB) */
+    PBR_TEX_KT = 3,             /* glass Kt (RGB) */
+    PBR_TEX_SIGMA = 4,          /* matte sigma (float) */
+    PBR_TEX_ROUGHNESS = 5,      /* plastic roughness (float) */
+    PBR_TEX_SLOTS = 6
+};
+
 typedef struct pbr_material_desc {
     int type;                   /* pbr_material_type */
     float Kd[3];                /* matte Kd, plastic Kd */
@@ -125,6 +159,7 @@ typedef struct pbr_material_desc {
     float vroughness;
     int has_uv_roughness;       /* metal: uRoughness/vRoughness textures present */
     int remap_roughness;
+    int tex[PBR_TEX_SLOTS];     /* pbr_texture_slot → texture index + 1, or 0 (triangle meshes only) */
 } pbr_material_desc;
 
 typedef struct pbr_light_desc {
@@ -161,6 +196,8 @@ typedef struct pbr_scene_desc {
     int n_media;
     const pbr_medium_desc* media;
     int max_prims_in_node;      /* BVHAccel maxPrimsInNode (main.cpp:385 uses 1) */
+    int n_textures;
+    const pbr_texture_desc* textures;
 } pbr_scene_desc;
 
 /* CreatePerspectiveCamera (Camera/Perspective.cpp:84-104) inputs. */

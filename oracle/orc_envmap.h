@@ -34,35 +34,41 @@ inline int RoundUpPow2I(int v) {   // PBR.h:262-270
 }
 inline int Log2IntI(uint32_t v) { return v ? 31 - __builtin_clz(v) : 0; }   // PBR.h:290-297
 
-class MIPMapS {
+enum class ImageWrapO { Repeat = 0, Black = 1, Clamp = 2 };   // MIPMap.h:21
+inline Spec ClampInf(const Spec& v) { return v.Clamp(0.f, Infinity); }
+inline float ClampInf(float v) { return Clampf(v, 0.f, Infinity); }
+
+// MIPMap<T> (T = Spectrum or float), Texture/MIPMap.h:37-252
+template <class T>
+class MIPMapT {
   public:
-    MIPMapS(int resX, int resY, const Spec* img) {   // MIPMap.h:86-155 (Repeat wrap)
-        std::vector<Spec> resampled;
-        const Spec* level0 = img;
+    MIPMapT(int resX, int resY, const T* img, ImageWrapO wrap = ImageWrapO::Repeat) : wrapMode(wrap) {   // MIPMap.h:86-155
+        std::vector<T> resampled;
+        const T* level0 = img;
         if (!IsPow2(resX) || !IsPow2(resY)) {
             int rx = RoundUpPow2I(resX), ry = RoundUpPow2I(resY);
             std::vector<RW> sW = Weights(resX, rx);
-            resampled.assign((size_t)rx * ry, Spec(0.f));
+            resampled.assign((size_t)rx * ry, T(0.f));
             for (int t = 0; t < resY; ++t)
                 for (int s = 0; s < rx; ++s) {
                     resampled[(size_t)t * rx + s] = 0.f;
                     for (int j = 0; j < 4; ++j) {
-                        int origS = ModI(sW[s].firstTexel + j, resX);
+                        int origS = WrapI(sW[s].firstTexel + j, resX);
                         if (origS >= 0 && origS < resX)
                             resampled[(size_t)t * rx + s] += sW[s].weight[j] * img[(size_t)t * resX + origS];
                     }
                 }
             std::vector<RW> tW = Weights(resY, ry);
-            std::vector<Spec> work(ry);
+            std::vector<T> work(ry);
             for (int s = 0; s < rx; ++s) {
                 for (int t = 0; t < ry; ++t) {
                     work[t] = 0.f;
                     for (int j = 0; j < 4; ++j) {
-                        int offset = ModI(tW[t].firstTexel + j, resY);
+                        int offset = WrapI(tW[t].firstTexel + j, resY);
                         if (offset >= 0 && offset < resY) work[t] += tW[t].weight[j] * resampled[(size_t)offset * rx + s];
                     }
                 }
-                for (int t = 0; t < ry; ++t) resampled[(size_t)t * rx + s] = work[t].Clamp(0.f, Infinity);
+                for (int t = 0; t < ry; ++t) resampled[(size_t)t * rx + s] = ClampInf(work[t]);
             }
             resX = rx;
             resY = ry;
@@ -79,7 +85,7 @@ class MIPMapS {
             int sRes = std::max(1, us[i - 1] / 2), tRes = std::max(1, vs[i - 1] / 2);
             us[i] = sRes;
             vs[i] = tRes;
-            pyr[i].assign((size_t)sRes * tRes, Spec(0.f));
+            pyr[i].assign((size_t)sRes * tRes, T(0.f));
             for (int t = 0; t < tRes; ++t)
                 for (int s = 0; s < sRes; ++s)
                     pyr[i][(size_t)t * sRes + s] = .25f * (Texel(i - 1, 2 * s, 2 * t) + Texel(i - 1, 2 * s + 1, 2 * t) +
@@ -89,12 +95,17 @@ class MIPMapS {
     int Width() const { return us[0]; }
     int Height() const { return vs[0]; }
     int Levels() const { return (int)pyr.size(); }
-    const Spec& Texel(int level, int s, int t) const {   // MIPMap.h:166-190
-        s = ModI(s, us[level]);
-        t = ModI(t, vs[level]);
+    T Texel(int level, int s, int t) const {   // MIPMap.h:166-190
+        switch (wrapMode) {
+        case ImageWrapO::Repeat: s = ModI(s, us[level]); t = ModI(t, vs[level]); break;
+        case ImageWrapO::Clamp: s = Clampi(s, 0, us[level] - 1); t = Clampi(t, 0, vs[level] - 1); break;
+        case ImageWrapO::Black:
+            if (s < 0 || s >= us[level] || t < 0 || t >= vs[level]) return T(0.f);
+            break;
+        }
         return pyr[level][(size_t)t * us[level] + s];
     }
-    Spec Lookup(P2 st, float width = 0.f) const {   // MIPMap.h:193-211
+    T Lookup(P2 st, float width = 0.f) const {   // MIPMap.h:193-211
         float level = Levels() - 1 + Log2(std::max(width, (float)1e-8));
         if (level < 0) return triangle(0, st);
         else if (level >= Levels() - 1) return Texel(Levels() - 1, 0, 0);
@@ -102,9 +113,17 @@ class MIPMapS {
         float delta = level - iLevel;
         return (1 - delta) * triangle(iLevel, st) + delta * triangle(iLevel + 1, st);   // Lerp
     }
+    // Lookup(st, dst0, dst1) (MIPMap.h:227-247) with the zero differentials every hit carries (F5):
+    // trilinear → Lookup(st, 0) → triangle(0, st); EWA → minorLength == 0 → triangle(0, st)
+    T LookupZeroDifferentials(P2 st, bool doTrilinear) const { return doTrilinear ? Lookup(st, 0.f) : triangle(0, st); }
 
   private:
     struct RW { int firstTexel; float weight[4]; };
+    int WrapI(int i, int res) const {
+        if (wrapMode == ImageWrapO::Repeat) return ModI(i, res);
+        if (wrapMode == ImageWrapO::Clamp) return Clampi(i, 0, res - 1);
+        return i;
+    }
     static bool IsPow2(int v) { return v && !(v & (v - 1)); }
     static float Log2(float x) {   // PBR.h:283-286
         const float invLog2 = 1.442695040888963387004650940071;
@@ -125,7 +144,7 @@ class MIPMapS {
         }
         return wt;
     }
-    Spec triangle(int level, P2 st) const {   // MIPMap.h:240-252
+    T triangle(int level, P2 st) const {   // MIPMap.h:240-252
         level = Clampi(level, 0, Levels() - 1);
         float s = st.x * us[level] - 0.5f;
         float t = st.y * vs[level] - 0.5f;
@@ -134,9 +153,11 @@ class MIPMapS {
         return (1 - ds) * (1 - dt) * Texel(level, s0, t0) + (1 - ds) * dt * Texel(level, s0, t0 + 1) +
                ds * (1 - dt) * Texel(level, s0 + 1, t0) + ds * dt * Texel(level, s0 + 1, t0 + 1);
     }
+    ImageWrapO wrapMode;
     std::vector<int> us, vs;
-    std::vector<std::vector<Spec>> pyr;
+    std::vector<std::vector<T>> pyr;
 };
+using MIPMapS = MIPMapT<Spec>;
 
 // Distribution1D::SampleContinuous (Sampling.h:117-131)
 inline float SampleContinuous(const Distribution1D& d, float u, float* pdf, int* off) {

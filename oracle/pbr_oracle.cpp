@@ -70,6 +70,13 @@ struct Light {
 };
 struct Medium { Spec sigma_a, sigma_s, sigma_t; float g; };
 struct MaterialO { pbr_material_desc d; float ua, va, ra; };   // pre-remapped roughness
+// ImageTexture<RGBSpectrum, Spectrum> / <float, float> with its UVMapping2D (Texture/ImageTexture.h)
+struct TextureO {
+    bool isFloat = false, trilinear = false;
+    float su = 1, sv = 1, du = 0, dv = 0;
+    std::shared_ptr<MIPMapT<Spec>> ms;
+    std::shared_ptr<MIPMapT<float>> mf;
+};
 
 }  // namespace orc
 
@@ -93,6 +100,7 @@ struct Scene {
     std::vector<int> primIds;       // original prims-vector index per ordered slot
     std::vector<OrcLinearBVHNode> nodes;
     std::vector<MaterialO> materials;
+    std::vector<TextureO> textures;
     std::vector<Light> lights;
     std::vector<int> infinite;
     std::vector<Medium> media;
@@ -278,6 +286,7 @@ struct Interaction {
 };
 struct SurfaceInteraction : Interaction {
     int prim = -1;          // ordered primitive slot
+    P2 uv;                  // Triangle.cpp:170 uvHit
     V3 dpdu;                // shading.dpdu (== dpdu without shading normals)
     V3 sn;                  // shading.n
 };
@@ -356,6 +365,7 @@ static void TriangleSI(const Mesh& m, int tri, const Ray& ray, float b0, float b
     if (m.reverse ^ m.swaps) n = -n;
     si->n = n; si->sn = n;
     si->dpdu = dpdu;
+    si->uv = P2(b0 * uv[0].x + b1 * uv[1].x + b2 * uv[2].x, b0 * uv[0].y + b1 * uv[1].y + b2 * uv[2].y);   // b0*uv0 + b1*uv1 + b2*uv2
 }
 
 // Sphere: the reference's is a stub (F2). This is the pbrt-v3 full-sphere algorithm with the
@@ -880,6 +890,25 @@ static Lobe MakeTR(Lobe l, float ax, float ay) {   // TrowbridgeReitzDistributio
 }
 static Spec S3(const float* v) { return Spec(v[0], v[1], v[2]); }
 
+// Texture<Spectrum/float>::Evaluate of a material slot: ConstantTexture (the descriptor's value) or
+// ImageTexture::Evaluate (ImageTexture.h:52-60): UVMapping2D::Map (Texture.cpp:8-14), then the MIPMap
+// lookup with the zero differentials every hit carries (F5).
+static const TextureO* SlotTex(const Scene& s, const pbr_material_desc& m, int slot) {
+    return m.tex[slot] ? &s.textures[m.tex[slot] - 1] : nullptr;
+}
+static Spec EvalSpec(const Scene& s, const pbr_material_desc& m, int slot, const float* constant, const SurfaceInteraction& si) {
+    const TextureO* t = SlotTex(s, m, slot);
+    if (!t) return S3(constant);
+    P2 st(t->su * si.uv.x + t->du, t->sv * si.uv.y + t->dv);
+    return t->ms->LookupZeroDifferentials(st, t->trilinear);
+}
+static float EvalFloat(const Scene& s, const pbr_material_desc& m, int slot, float constant, const SurfaceInteraction& si) {
+    const TextureO* t = SlotTex(s, m, slot);
+    if (!t) return constant;
+    P2 st(t->su * si.uv.x + t->du, t->sv * si.uv.y + t->dv);
+    return t->mf->LookupZeroDifferentials(st, t->trilinear);
+}
+
 // Material::ComputeScatteringFunctions for each material (Material/*.cpp)
 static void ComputeBSDF(const Scene& s, const SurfaceInteraction& si, bool allowMultipleLobes, BSDF* bsdf) {
     const Prim& pr = s.prims[si.prim];
@@ -896,8 +925,8 @@ static void ComputeBSDF(const Scene& s, const SurfaceInteraction& si, bool allow
     bsdf->ts = Cross(bsdf->ns, bsdf->ss);
     switch (m.type) {
     case PBR_MAT_MATTE: {                               // MatteMaterial.cpp:13-28
-        Spec r = S3(m.Kd).Clamp();
-        float sig = Clampf(m.sigma, 0, 90);
+        Spec r = EvalSpec(s, m, PBR_TEX_KD, m.Kd, si).Clamp();
+        float sig = Clampf(EvalFloat(s, m, PBR_TEX_SIGMA, m.sigma, si), 0, 90);
         if (!r.IsBlack()) {
             Lobe l; l.R = r; l.type = BSDF_REFLECTION | BSDF_DIFFUSE;
             if (sig == 0) l.kind = L_LAMBERT;
@@ -913,13 +942,13 @@ static void ComputeBSDF(const Scene& s, const SurfaceInteraction& si, bool allow
         break;
     }
     case PBR_MAT_MIRROR: {                              // Mirror.cpp:5-15
-        Spec R = S3(m.Kr).Clamp();
+        Spec R = EvalSpec(s, m, PBR_TEX_KR, m.Kr, si).Clamp();
         if (!R.IsBlack()) { Lobe l; l.kind = L_SPEC_R; l.type = BSDF_REFLECTION | BSDF_SPECULAR; l.R = R; l.fresnel = FR_NOOP; bsdf->Add(l); }
         break;
     }
     case PBR_MAT_GLASS: {                               // GlassMaterial.cpp:9-57
         float eta = m.eta, urough = m.uroughness, vrough = m.vroughness;
-        Spec R = S3(m.Kr).Clamp(), T = S3(m.Kt).Clamp();
+        Spec R = EvalSpec(s, m, PBR_TEX_KR, m.Kr, si).Clamp(), T = EvalSpec(s, m, PBR_TEX_KT, m.Kt, si).Clamp();
         if (R.IsBlack() && T.IsBlack()) break;
         bool isSpecular = urough == 0 && vrough == 0;
         if (isSpecular && allowMultipleLobes) {
@@ -952,12 +981,12 @@ static void ComputeBSDF(const Scene& s, const SurfaceInteraction& si, bool allow
         break;
     }
     case PBR_MAT_PLASTIC: {                             // PlasticMaterial.cpp:8-30
-        Spec kd = S3(m.Kd).Clamp();
+        Spec kd = EvalSpec(s, m, PBR_TEX_KD, m.Kd, si).Clamp();
         if (!kd.IsBlack()) { Lobe l; l.kind = L_LAMBERT; l.type = BSDF_REFLECTION | BSDF_DIFFUSE; l.R = kd; bsdf->Add(l); }
-        Spec ks = S3(m.Ks).Clamp();
+        Spec ks = EvalSpec(s, m, PBR_TEX_KS, m.Ks, si).Clamp();
         if (!ks.IsBlack()) {
-            float rough = m.roughness;
-            if (m.remap_roughness) rough = mo.ra;
+            float rough = EvalFloat(s, m, PBR_TEX_ROUGHNESS, m.roughness, si);
+            if (m.remap_roughness) rough = m.tex[PBR_TEX_ROUGHNESS] ? RoughnessToAlpha(rough) : mo.ra;
             Lobe l; l.kind = L_MF_R; l.type = BSDF_REFLECTION | BSDF_GLOSSY; l.R = ks;
             l.fresnel = FR_DIEL; l.fEtaI = 1.5f; l.fEtaT = 1.f;
             bsdf->Add(MakeTR(l, rough, rough));
@@ -1538,6 +1567,37 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
         mo.ra = RoughnessToAlpha(mo.d.roughness);
         if (mo.d.type == PBR_MAT_METAL && !mo.d.has_uv_roughness) { mo.ua = mo.va = mo.ra; }
         s->materials.push_back(mo);
+    }
+    // ImageTexture::GetTexture (ImageTexture.cpp:46-92): loadImage's texels (or a 0.5 grey 1x1
+    // image), convertIn (ImageTexture.h:69-78), MIPMap(res, texels, doTrilinear, maxAniso, wrap)
+    for (int i = 0; i < d->n_textures; ++i) {
+        const pbr_texture_desc& td = d->textures[i];
+        TextureO t;
+        t.isFloat = td.is_float != 0;
+        t.trilinear = td.trilinear != 0;
+        t.su = td.su; t.sv = td.sv; t.du = td.du; t.dv = td.dv;
+        int w = 1, h = 1;
+        std::vector<Spec> texels;
+        if (td.data && td.width > 0 && td.height > 0) {
+            w = td.width; h = td.height;
+            for (int j = 0; j < w * h; ++j)
+                texels.push_back(Spec(td.data[(size_t)j * td.components], td.data[(size_t)j * td.components + 1], td.data[(size_t)j * td.components + 2]));
+        } else {
+            texels.push_back(Spec(0.5f));
+        }
+        auto igc = [](float v) { return v <= 0.04045f ? v * 1.f / 12.92f : t_pow((v + 0.055f) * 1.f / 1.055f, (float)2.4f); };
+        const ImageWrapO wrap = (ImageWrapO)td.wrap;
+        if (t.isFloat) {
+            std::vector<float> conv(texels.size());
+            for (size_t j = 0; j < texels.size(); ++j) conv[j] = td.scale * (td.gamma ? igc(texels[j].y()) : texels[j].y());
+            t.mf = std::make_shared<MIPMapT<float>>(w, h, conv.data(), wrap);
+        } else {
+            std::vector<Spec> conv(texels.size());
+            for (size_t j = 0; j < texels.size(); ++j)
+                for (int k = 0; k < 3; ++k) conv[j].c[k] = td.scale * (td.gamma ? igc(texels[j].c[k]) : texels[j].c[k]);
+            t.ms = std::make_shared<MIPMapT<Spec>>(w, h, conv.data(), wrap);
+        }
+        s->textures.push_back(t);
     }
     for (int i = 0; i < d->n_media; ++i) {
         const pbr_medium_desc& md = d->media[i];

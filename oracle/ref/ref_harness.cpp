@@ -65,6 +65,7 @@
 #include "Material\MetalMaterial.h"
 #include "Material\Mirror.h"
 #include "Material\PlasticMaterial.h"
+#include "Texture\ImageTexture.h"
 #include "Media\HomogeneousMedium.h"
 #include "Sampler\Halton.h"
 #include "Shape\Triangle.h"
@@ -191,24 +192,52 @@ std::unique_ptr<RefScene> build(const pbr_scene_desc* d) {
     std::unique_ptr<RefScene> r(new RefScene);
     for (int i = 0; i < d->n_media; ++i)
         r->media.emplace_back(new HomogeneousMedium(spec(d->media[i].sigma_a), spec(d->media[i].sigma_s), d->media[i].g));
+    // ImageTextures as main.cpp / ModelLoad.cpp make them (main.cpp:63-78, ModelLoad.cpp:95-160): the
+    // image goes through a file that the texture's own loadImage (stbi_loadf, flip-on-load set,
+    // ImageTexture.cpp:13-37) reads back as exactly the descriptor's floats
+    auto image = [&](const pbr_texture_desc& td) {
+        std::string path;
+        if (td.data && td.width > 0 && td.height > 0) {
+            path = write_env(td.data, td.width, td.height, td.components, true);
+            r->tmpFiles.push_back(path);
+        }
+        return path;
+    };
+    auto texS = [&](const pbr_material_desc& m, int slot, const float* v) -> std::shared_ptr<Texture<Spectrum>> {
+        if (!m.tex[slot]) return cs(v);
+        const pbr_texture_desc& td = d->textures[m.tex[slot] - 1];
+        return std::make_shared<ImageTexture<RGBSpectrum, Spectrum>>(std::make_unique<UVMapping2D>(td.su, td.sv, td.du, td.dv),
+                                                                     image(td), td.trilinear != 0, td.max_aniso,
+                                                                     (ImageWrap)td.wrap, td.scale, td.gamma != 0);
+    };
+    auto texF = [&](const pbr_material_desc& m, int slot, float v) -> std::shared_ptr<Texture<float>> {
+        if (!m.tex[slot]) return cf(v);
+        const pbr_texture_desc& td = d->textures[m.tex[slot] - 1];
+        return std::make_shared<ImageTexture<float, float>>(std::make_unique<UVMapping2D>(td.su, td.sv, td.du, td.dv), image(td),
+                                                            td.trilinear != 0, td.max_aniso, (ImageWrap)td.wrap, td.scale,
+                                                            td.gamma != 0);
+    };
     for (int i = 0; i < d->n_materials; ++i) {   // Main/main.cpp:147-239
         const pbr_material_desc& m = d->materials[i];
         std::shared_ptr<Material> mat;
         auto bump = cf(0.f);
         switch (m.type) {
         case PBR_MAT_NONE: break;
-        case PBR_MAT_MATTE: mat = std::make_shared<MatteMaterial>(cs(m.Kd), cf(m.sigma), bump); break;
-        case PBR_MAT_MIRROR: mat = std::make_shared<MirrorMaterial>(cs(m.Kr), bump); break;
+        case PBR_MAT_MATTE: mat = std::make_shared<MatteMaterial>(texS(m, PBR_TEX_KD, m.Kd), texF(m, PBR_TEX_SIGMA, m.sigma), bump); break;
+        case PBR_MAT_MIRROR: mat = std::make_shared<MirrorMaterial>(texS(m, PBR_TEX_KR, m.Kr), bump); break;
         case PBR_MAT_GLASS:
-            mat = std::make_shared<GlassMaterial>(cs(m.Kr), cs(m.Kt), cf(m.uroughness), cf(m.vroughness), cf(m.eta), bump,
-                                                  m.remap_roughness != 0);
+            mat = std::make_shared<GlassMaterial>(texS(m, PBR_TEX_KR, m.Kr), texS(m, PBR_TEX_KT, m.Kt), cf(m.uroughness),
+                                                  cf(m.vroughness), cf(m.eta), bump, m.remap_roughness != 0);
             break;
         case PBR_MAT_METAL:
             mat = std::make_shared<MetalMaterial>(cs(m.metal_eta), cs(m.metal_k), cf(m.roughness),
                                                   m.has_uv_roughness ? cf(m.uroughness) : nullptr,
                                                   m.has_uv_roughness ? cf(m.vroughness) : nullptr, bump, m.remap_roughness != 0);
             break;
-        case PBR_MAT_PLASTIC: mat = std::make_shared<PlasticMaterial>(cs(m.Kd), cs(m.Ks), cf(m.roughness), bump, m.remap_roughness != 0); break;
+        case PBR_MAT_PLASTIC:
+            mat = std::make_shared<PlasticMaterial>(texS(m, PBR_TEX_KD, m.Kd), texS(m, PBR_TEX_KS, m.Ks),
+                                                    texF(m, PBR_TEX_ROUGHNESS, m.roughness), bump, m.remap_roughness != 0);
+            break;
         default: throw std::runtime_error("unknown material");
         }
         r->materials.push_back(mat);

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 PBR_OK = 0
 PBR_E_INVALID = -1
@@ -24,6 +24,8 @@ INTEGRATOR_WHITTED, INTEGRATOR_PATH, INTEGRATOR_VOLPATH = 0, 1, 2
 SAMPLER_HALTON, SAMPLER_SOBOL = 0, 1
 LIGHTS_UNIFORM, LIGHTS_POWER = 0, 1
 BVH_BUILD_HOST, BVH_BUILD_DEVICE = 0, 1
+WRAP_REPEAT, WRAP_BLACK, WRAP_CLAMP = 0, 1, 2
+TEX_KD, TEX_KS, TEX_KR, TEX_KT, TEX_SIGMA, TEX_ROUGHNESS = range(6)
 
 F3 = C.c_float * 3
 F16 = C.c_float * 16
@@ -68,6 +70,26 @@ class MaterialDesc(C.Structure):
         ("vroughness", C.c_float),
         ("has_uv_roughness", C.c_int),
         ("remap_roughness", C.c_int),
+        ("tex", C.c_int * 6),
+    ]
+
+
+class TextureDesc(C.Structure):
+    _fields_ = [
+        ("is_float", C.c_int),
+        ("width", C.c_int),
+        ("height", C.c_int),
+        ("components", C.c_int),
+        ("data", C.POINTER(C.c_float)),
+        ("scale", C.c_float),
+        ("gamma", C.c_int),
+        ("wrap", C.c_int),
+        ("trilinear", C.c_int),
+        ("max_aniso", C.c_float),
+        ("su", C.c_float),
+        ("sv", C.c_float),
+        ("du", C.c_float),
+        ("dv", C.c_float),
     ]
 
 
@@ -108,6 +130,8 @@ class SceneDesc(C.Structure):
         ("n_media", C.c_int),
         ("media", C.POINTER(MediumDesc)),
         ("max_prims_in_node", C.c_int),
+        ("n_textures", C.c_int),
+        ("textures", C.POINTER(TextureDesc)),
     ]
 
 

@@ -4,6 +4,7 @@
 // to it (see pbr_math.h for the numerics contract).
 #pragma once
 #include "pbr_layout.h"
+#include "pbr_material.h"
 #include "pbr_math.h"
 
 namespace pbr {
@@ -19,6 +20,7 @@ struct Isect {
     f3 sn, dpdu;               // shading normal and shading dpdu (surfaces)
     int slot;                  // BVH-ordered primitive slot (surfaces)
     int medIn, medOut;
+    float u, v;                // SurfaceInteraction::uv (Triangle.cpp:170), read by image textures
 };
 PBR_HD int get_medium(const Isect& it, f3 w) { return dot(w, it.n) > 0 ? it.medOut : it.medIn; }   // Interaction.h:48-50
 PBR_HD Ray spawn_ray(const Isect& it, f3 d) {   // Interaction.h:28-31
@@ -150,6 +152,8 @@ __device__ void triangle_si(const DeviceScene& S, int slot, const Ray& ray, floa
     si->n = n;
     si->sn = n;
     si->dpdu = dpdu;
+    si->u = b0 * u0x + b1 * u1x + b2 * u2x;   // uvHit = b0 * uv[0] + b1 * uv[1] + b2 * uv[2]
+    si->v = b0 * u0y + b1 * u1y + b2 * u2y;
 }
 __device__ void sphere_si(const SphereRec& s, const Ray& r, float t, Isect* si) {
     f3 o = xf_point(s.w2o, r.o), d = xf_vector(s.w2o, r.d);
@@ -175,6 +179,7 @@ __device__ void sphere_si(const SphereRec& s, const Ray& r, float t, Isect* si) 
     si->n = n;
     si->sn = n;
     si->dpdu = du;
+    si->u = si->v = 0.f;   // image textures are refused on spheres at upload
 }
 
 __device__ __forceinline__ bool prim_hit(const DeviceScene& S, int slot, const Ray& r, float* t, float* b0, float* b1, float* b2) {
@@ -667,6 +672,7 @@ PBR_HD float tr_pdf(const Lobe& l, f3 wo, f3 wh) { return tr_D(l, wh) * tr_G1(l,
 // K: bit mask of the LobeKinds the caller can meet (the scene's materials, or what a type filter
 // admits); kinds outside it compile out, which keeps the microfacet code out of simple kernels.
 constexpr int kAllLobes = 0x7f;
+constexpr int kTexturedLobes = 0x80;   // LOBES flag of the shading kernels: some material has image textures
 #define PBR_HAS(K, kind) (((K) >> (kind)) & 1)
 template <int K = kAllLobes>
 PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
@@ -888,13 +894,61 @@ PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float
     }
     return f;
 }
+// ImageTexture::Evaluate (ImageTexture.h:52-60) with zero differentials: MIPMap::triangle(0, st)
+// (MIPMap.h:240-252) on the level-0 texels, Texel's wrap modes (:166-190).
+__device__ __forceinline__ float4 tex_texel(const DeviceScene& S, const TexDev& t, int s, int u) {
+    if (t.wrap == 0) { s = s % t.w; if (s < 0) s += t.w; u = u % t.h; if (u < 0) u += t.h; }
+    else if (t.wrap == 2) { s = clampi(s, 0, t.w - 1); u = clampi(u, 0, t.h - 1); }
+    else if (s < 0 || s >= t.w || u < 0 || u >= t.h) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return S.texels[t.offset + (size_t)u * t.w + s];
+}
+__device__ __forceinline__ float4 tex_lookup(const DeviceScene& S, const TexDev& t, float su, float sv) {
+    const float s = su * t.w - 0.5f, u = sv * t.h - 0.5f;
+    const int s0 = (int)floorf(s), u0 = (int)floorf(u);
+    const float ds = s - s0, du = u - u0;
+    const float w00 = (1 - ds) * (1 - du), w01 = (1 - ds) * du, w10 = ds * (1 - du), w11 = ds * du;
+    const float4 a = tex_texel(S, t, s0, u0), b = tex_texel(S, t, s0, u0 + 1), c = tex_texel(S, t, s0 + 1, u0),
+                 d = tex_texel(S, t, s0 + 1, u0 + 1);
+    return make_float4(w00 * a.x + w01 * b.x + w10 * c.x + w11 * d.x, w00 * a.y + w01 * b.y + w10 * c.y + w11 * d.y,
+                       w00 * a.z + w01 * b.z + w10 * c.z + w11 * d.z, 0.f);
+}
+// A textured material's lobes at one hit: its textures evaluated through their UVMapping2D
+// (Texture.cpp:8-14), then the material's ComputeScatteringFunctions (pbr_material.h).  Out of line:
+// the untextured scenes' shading kernels pay no registers for it.
+__device__ __noinline__ void textured_template(const DeviceScene& S, int mat, float u, float v, bool multiLobe,
+                                               MatTemplate* out) {
+    const TexMat& tm = S.texMats[mat];
+    MatParams p = tm.p;
+    for (int k = 0; k < 6; ++k) {
+        const int ti = tm.tex[k];
+        if (ti < 0) continue;
+        const TexDev& t = S.textures[ti];
+        const float4 val = tex_lookup(S, t, t.su * u + t.du, t.sv * v + t.dv);
+        float* dst = k == 0 ? p.Kd : (k == 1 ? p.Ks : (k == 2 ? p.Kr : p.Kt));
+        if (k == 4) p.sigma = val.x;
+        else if (k == 5) p.roughness = val.x;
+        else { dst[0] = val.x; dst[1] = val.y; dst[2] = val.z; }
+    }
+    material_template(p, multiLobe, out);
+}
+
 // SurfaceInteraction::ComputeScatteringFunctions → BSDF(si, eta) frame (Reflection.h:105-110)
-// mats: S.materials, or a kernel's LDS copy of it
-__device__ __forceinline__ bool make_bsdf(const DeviceScene& S, const MatTemplate* mats, const Isect& si, bool multiLobe, BSDF* b) {
+// mats: S.materials, or a kernel's LDS copy of it; texLocal: where a textured material's per-hit
+// lobes go (the BSDF points at it)
+// TEX = false (scenes without image textures) keeps every template read on its known address space.
+template <bool TEX>
+__device__ __forceinline__ bool make_bsdf(const DeviceScene& S, const MatTemplate* mats, const Isect& si, bool multiLobe, BSDF* b,
+                                          MatTemplate* texLocal) {
     int mat = S.primInfo[si.slot].y;
     if (mat < 0) return false;
     const MatTemplate* mt = mats + 2 * mat + (multiLobe ? 1 : 0);
     if (!mt->valid) return false;
+    if constexpr (TEX) {
+        if (mt->textured) {
+            textured_template(S, mat, si.u, si.v, multiLobe, texLocal);
+            mt = texLocal;
+        }
+    }
     b->mt = mt;
     b->ns = si.sn;
     b->ng = si.n;

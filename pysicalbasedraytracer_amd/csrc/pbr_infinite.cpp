@@ -1,4 +1,5 @@
-// pbr_infinite.cpp — host half of the InfiniteAreaLight (Light/InfiniteAreaLight.cpp:7-68): the
+// pbr_infinite.cpp — host half of the InfiniteAreaLight (Light/InfiniteAreaLight.cpp:7-68) and of
+// ImageTexture (Texture/ImageTexture.cpp:13-92: its MIPMap's level 0, see build_image_texture): the
 // MIPMap<RGBSpectrum> built from the environment image (Texture/MIPMap.h:86-187), its level-0
 // texels for the device's bilinear Lookup(st, 0), the Distribution2D over luminance × sinθ
 // (Sampler/Sampling.h:76-171, Sampling.cpp:121-133) and Power() for the power light distribution.
@@ -157,7 +158,90 @@ void dist1d(const float* f, int n, std::vector<float>* cdf, float* funcInt) {
     else for (int i = 1; i < n + 1; ++i) (*cdf)[i] /= *funcInt;
 }
 
+float inverse_gamma(float v) {   // InverseGammaCorrect (Core/PBR.h:126-129)
+    if (v <= 0.04045f) return v * 1.f / 12.92f;
+    return t_pow((v + 0.055f) * 1.f / 1.055f, (float)2.4f);
+}
+
+// MIPMap<T> constructor's power-of-two resample (MIPMap.h:86-150) with the texture's wrap mode, for
+// T = RGBSpectrum (nc = 3) or float (nc = 1); img is row-major, nc floats per texel.
+void resample_pow2(int wrap, int nc, int* resW, int* resH, std::vector<float>* img) {
+    const int W0 = *resW, H0 = *resH;
+    if (is_pow2(W0) && is_pow2(H0)) return;
+    const int pw = round_up_pow2(W0), ph = round_up_pow2(H0);
+    auto wrapIdx = [wrap](int i, int res) {
+        if (wrap == PBR_WRAP_REPEAT) return imod(i, res);
+        if (wrap == PBR_WRAP_CLAMP) return i < 0 ? 0 : (i > res - 1 ? res - 1 : i);
+        return i;
+    };
+    std::vector<Weight> sw = resample_weights(W0, pw);
+    std::vector<float> re((size_t)pw * ph * nc, 0.f);
+    for (int t = 0; t < H0; ++t)
+        for (int s = 0; s < pw; ++s)
+            for (int j = 0; j < 4; ++j) {
+                const int os = wrapIdx(sw[s].first + j, W0);
+                if (os >= 0 && os < W0)
+                    for (int k = 0; k < nc; ++k)
+                        re[((size_t)t * pw + s) * nc + k] += sw[s].w[j] * (*img)[((size_t)t * W0 + os) * nc + k];
+            }
+    std::vector<Weight> tw = resample_weights(H0, ph);
+    std::vector<float> work((size_t)ph * nc);
+    for (int s = 0; s < pw; ++s) {
+        for (int t = 0; t < ph; ++t) {
+            for (int k = 0; k < nc; ++k) work[(size_t)t * nc + k] = 0.f;
+            for (int j = 0; j < 4; ++j) {
+                const int off = wrapIdx(tw[t].first + j, H0);
+                if (off >= 0 && off < H0)
+                    for (int k = 0; k < nc; ++k) work[(size_t)t * nc + k] += tw[t].w[j] * re[((size_t)off * pw + s) * nc + k];
+            }
+        }
+        for (int t = 0; t < ph; ++t)
+            for (int k = 0; k < nc; ++k) re[((size_t)t * pw + s) * nc + k] = clamp_inf(work[(size_t)t * nc + k]);
+    }
+    img->swap(re);
+    *resW = pw;
+    *resH = ph;
+}
+
 }  // namespace
+
+void build_image_texture(const pbr_texture_desc& td, TexDev* out, std::vector<float>* texels) {
+    // loadImage (ImageTexture.cpp:13-37) → GetTexture's substitute for a missing image (:60-66) →
+    // convertIn per texel (ImageTexture.h:69-78) → MIPMap level 0 (MIPMap.h:86-150)
+    int w = 1, h = 1;
+    std::vector<RGB> rgb;
+    if (td.data && td.width > 0 && td.height > 0) {
+        if (td.components < 3) throw std::invalid_argument("ImageTexture image needs >= 3 components");
+        w = td.width;
+        h = td.height;
+        rgb.resize((size_t)w * h);
+        for (size_t i = 0; i < rgb.size(); ++i)
+            for (int k = 0; k < 3; ++k) rgb[i].c[k] = td.data[i * td.components + k];
+    } else {
+        rgb.assign(1, RGB{{0.5f, 0.5f, 0.5f}});
+    }
+    if (td.wrap < PBR_WRAP_REPEAT || td.wrap > PBR_WRAP_CLAMP) throw std::invalid_argument("bad texture wrap mode");
+    const int nc = td.is_float ? 1 : 3;
+    std::vector<float> img((size_t)w * h * nc);
+    for (size_t i = 0; i < rgb.size(); ++i) {
+        if (td.is_float) {
+            const float y = lum(rgb[i]);
+            img[i] = td.scale * (td.gamma ? inverse_gamma(y) : y);
+        } else {
+            for (int k = 0; k < 3; ++k) img[i * 3 + k] = td.scale * (td.gamma ? inverse_gamma(rgb[i].c[k]) : rgb[i].c[k]);
+        }
+    }
+    resample_pow2(td.wrap, nc, &w, &h, &img);
+    std::memset(out, 0, sizeof(*out));
+    out->offset = (int)(texels->size() / 4);
+    out->w = w;
+    out->h = h;
+    out->wrap = td.wrap;
+    out->isFloat = td.is_float ? 1 : 0;
+    out->su = td.su; out->sv = td.sv; out->du = td.du; out->dv = td.dv;
+    for (size_t i = 0; i < (size_t)w * h; ++i)
+        for (int k = 0; k < 4; ++k) texels->push_back(k < nc ? img[i * nc + k] : 0.f);
+}
 
 void build_infinite_light(const pbr_light_desc& ld, const float worldMin[3], const float worldMax[3],
                           InfiniteHost* out, float power[3]) {

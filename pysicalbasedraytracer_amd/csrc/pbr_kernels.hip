@@ -349,7 +349,8 @@ __device__ rgb whitted_li(const KParams& P, Ray ray, SState& st, Counters* c) {
         if (STATS) c->shading++;
         f3 n = isect.sn, wo = isect.wo;
         BSDF bsdf;
-        if (!make_bsdf(S, S.materials, isect, false, &bsdf)) {
+        MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+        if (!make_bsdf<true>(S, S.materials, isect, false, &bsdf, &texLocal)) {
             if (guard > kMaxPassThrough) { atomicOr(S.guard, kGuardWhittedPassThrough); Llast = sp(0.f); break; }
             ray = spawn_ray(isect, ray.d);     // Li(isect.SpawnRay(ray.d), depth)
             continue;
@@ -405,7 +406,8 @@ __device__ rgb path_li(const KParams& P, Ray ray, SState& st, Counters* c) {
         if (!found || bounces >= P.maxDepth) break;
         if (STATS) c->shading++;
         BSDF bsdf;
-        if (!make_bsdf(S, S.materials, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
+        MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+        if (!make_bsdf<true>(S, S.materials, isect, true, &bsdf, &texLocal)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
         if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0) {
             rgb Ld = beta * uniform_sample_one_light<STATS>(P, isect, &bsdf, 0.f, st, false, c);
             L = L + Ld;
@@ -487,7 +489,8 @@ __device__ rgb volpath_li(const KParams& P, Ray ray, SState& st, Counters* c) {
             if (!found || bounces >= P.maxDepth) break;
             if (STATS) c->shading++;
             BSDF bsdf;
-            if (!make_bsdf(S, S.materials, isect, true, &bsdf)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
+            MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+            if (!make_bsdf<true>(S, S.materials, isect, true, &bsdf, &texLocal)) { ray = spawn_ray(isect, ray.d); bounces--; continue; }
             L = L + beta * uniform_sample_one_light<STATS>(P, isect, &bsdf, 0.f, st, true, c);
             f3 wo = -ray.d, wi = mk(0, 0, 0);
             float pdf = 0;
@@ -790,6 +793,7 @@ struct pbr_hip_ctx {
     HaltonTables halton;
     DevBuf dInfTex, dInfCF, dInfCC, dInfMF, dInfMC, dInfRec;
     DevBuf dLeafParent;
+    DevBuf dTexels, dTextures, dTexMats;   // ImageTextures and the textured materials' parameters
     DevBuf dNodes, dWide, dQuad, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
     DevBuf dSobol, dSobolHi, dSobolPix;  // active Sobol nibble tables (index bits 0-31, 32-51), pixel tables
@@ -825,6 +829,17 @@ struct pbr_hip_ctx {
 };
 
 namespace {
+
+// Lobe kinds the scene's BSDFs can hold (selects the shading kernels' specialisation); a textured
+// material's lobes are built per hit, so it may produce any kind.
+int scene_lobe_kinds(const HostScene& h) {
+    int lobes = 0;
+    for (const MatTemplate& m : h.materials) {
+        if (m.textured) lobes |= kAllLobes | kTexturedLobes;
+        for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
+    }
+    return lobes;
+}
 
 int set_err(pbr_hip_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -888,6 +903,9 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     S.media = (const float*)ctx->dMedia.p;
     S.nMedia = (int)h.media.size() / 10;
     S.inf = h.inf.light >= 0 ? (const InfDev*)ctx->dInfRec.p : nullptr;
+    S.texels = h.texTexels.empty() ? nullptr : (const float4*)ctx->dTexels.p;
+    S.textures = h.textures.empty() ? nullptr : (const TexDev*)ctx->dTextures.p;
+    S.texMats = h.texMats.empty() ? nullptr : (const TexMat*)ctx->dTexMats.p;
     return S;
 }
 
@@ -1086,10 +1104,9 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const size_t cap = ch.cap, qcap = ch.qcap;
     const int lightsPerShade = ml ? std::max(1, nL) : 1;
     const size_t sqcap = qcap * (size_t)lightsPerShade;   // shadow-queue entries
-    int lobes = 0;
-    for (const MatTemplate& m : ctx->host.materials)
-        for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
+    const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
+    const bool textured = (lobes & kTexturedLobes) != 0;
     // tuning switches (results are bit-identical either way): LDS short stack, shade occupancy
     const char* eStack = getenv("PBR_SHORT_STACK");
     const bool shortStack = !(eStack && eStack[0] == '0');
@@ -1194,7 +1211,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             }
             const int l0 = level == 0 ? 1 : 0;
             PROF_LAUNCH(KP_WF_SHADE, st,
-            if (ml) {
+            if (textured) {
+                if (ml) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes | kTexturedLobes, false>), gstride, blk, 0, st, W, l0);
+                else hipLaunchKernelGGL((k_wf_shade<kAllLobes | kTexturedLobes, false>), gstride, blk, 0, st, W, l0);
+            } else if (ml) {
                 if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
                 else if (simple) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
                 else if (matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, true>), gstride, blk, 0, st, W, l0);
@@ -1242,10 +1262,9 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     // C3 2^25 349.4 ms, 2^26 336.1, 2^27 340.4; C5 2^25 1979 ms, 2^26 1939, 2^27 1919
     const WfChunks ch = wf_chunks(P, 26);
     const size_t cap = ch.cap, qcap = ch.qcap;
-    int lobes = 0;
-    for (const MatTemplate& m : ctx->host.materials)
-        for (int i = 0; i < m.nLobes; ++i) lobes |= 1 << m.lobes[i].kind;
+    const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
+    const bool textured = (lobes & kTexturedLobes) != 0;
     const char* eMats = getenv("PBR_MATS_LDS");
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
     WfvParams VL[kWfLanes];
@@ -1340,13 +1359,15 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
             const int kShade = vol ? KP_WFV_SHADE : KP_WFP_SHADE;
             if (vol) {
                 PROF_LAUNCH(KP_WFV_SHADE, st,
-                    if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0);
+                    if (textured) hipLaunchKernelGGL((k_wfv_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, V, l0);
+                    else if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0);
                     else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, st, V, l0);
                     else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0);
                     else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0));
             } else {
                 PROF_LAUNCH(KP_WFP_SHADE, st,
-                    if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
+                    if (textured) hipLaunchKernelGGL((k_wfp_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, X, l0);
+                    else if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
                     else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0);
                     else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, st, X, l0);
                     else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, st, X, l0));
@@ -1697,6 +1718,9 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
         HIP_TRY(hipStreamSynchronize(ctx->stream));   // rec is a host temporary
     }
     HIP_TRY(ctx->dPrimIds.upload(h.primIds, ctx->stream));
+    HIP_TRY(ctx->dTexels.upload(h.texTexels, ctx->stream));
+    HIP_TRY(ctx->dTextures.upload(h.textures, ctx->stream));
+    HIP_TRY(ctx->dTexMats.upload(h.texMats, ctx->stream));
     int rc = upload_light_distribution(ctx, PBR_LIGHTS_UNIFORM);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -36,7 +36,7 @@ struct MatTemplate {              // what Material::ComputeScatteringFunctions a
     int valid;                    // 0: material == nullptr → no BSDF
     int nLobes;
     float eta;                    // BSDF::eta (glass index, else 1)
-    int pad;
+    int textured;                 // 1: some parameter is an image texture — the lobes are built per hit
     Lobe lobes[2];
 };
 
@@ -52,6 +52,14 @@ struct DLight {
     float p[3];                   // point position
     float area;                   // area light triangle area
     float worldRadius;            // skybox
+};
+
+// ImageTexture level 0 (pbr_infinite.cpp build_image_texture) + its UVMapping2D
+struct TexDev {
+    int offset;                   // first texel in DeviceScene::texels (float4; float textures use .x)
+    int w, h, wrap, isFloat;
+    float su, sv, du, dv;
+    int pad[3];
 };
 
 struct SphereRec { float o2w[16]; float w2o[16]; float radius; int flip; int pad[2]; };
@@ -95,6 +103,10 @@ struct DeviceScene {
     int nMedia;
     const InfDev* inf;             // the InfiniteAreaLight's tables (device memory), or null
     int* guard;                    // set (kGuard*) when a walk stops at a safety bound; the render then fails
+    // image textures (only scenes with textured materials)
+    const float4* texels;
+    const TexDev* textures;
+    const struct TexMat* texMats;  // per material (pbr_material.h)
 };
 // Safety bounds of walks the reference runs without limit; reaching one fails the render
 // (PBR_E_UNSUPPORTED) instead of returning a silently truncated result.

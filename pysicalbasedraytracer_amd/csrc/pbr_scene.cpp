@@ -8,6 +8,7 @@
 // the same std::partition / std::nth_element calls on the same element order, so the layout is
 // identical.
 #include "pbr_scene.h"
+#include "pbr_material.h"
 #include "pbr_sobol_jk.h"
 #include "pbr_xform.h"
 
@@ -299,130 +300,25 @@ class SahBuilder {
     std::vector<int32_t>* order_;
 };
 
-float roughness_to_alpha(float roughness) {   // Microfacet.h:78-83
-    roughness = mx(roughness, (float)1e-3);
-    float x = t_log(roughness);
-    return 1.62142f + 0.819955f * x + 0.1734f * x * x + 0.0171201f * x * x * x + 0.000640711f * x * x * x * x;
+// A material's constant parameters (ConstantTexture values, Material/*.cpp constructors).
+MatParams mat_params(const pbr_material_desc& m) {
+    MatParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.type = m.type;
+    for (int i = 0; i < 3; ++i) {
+        p.Kd[i] = m.Kd[i]; p.Kr[i] = m.Kr[i]; p.Kt[i] = m.Kt[i]; p.Ks[i] = m.Ks[i];
+        p.metal_eta[i] = m.metal_eta[i]; p.metal_k[i] = m.metal_k[i];
+    }
+    p.sigma = m.sigma; p.eta = m.eta;
+    p.roughness = m.roughness; p.uroughness = m.uroughness; p.vroughness = m.vroughness;
+    p.has_uv_roughness = m.has_uv_roughness; p.remap_roughness = m.remap_roughness;
+    return p;
 }
-void put3(float* d, const float* s) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
-bool is_black3(const float* v) { return v[0] == 0.f && v[1] == 0.f && v[2] == 0.f; }
-void clamp3(float* d, const float* s) { for (int i = 0; i < 3; ++i) d[i] = clampf(s[i], 0, PBR_INF); }
-
-Lobe lobe0() { Lobe l; std::memset(&l, 0, sizeof(l)); return l; }
-void set_tr(Lobe& l, float ax, float ay) { l.ax = mx(float(0.001), ax); l.ay = mx(float(0.001), ay); }
 
 // Material::ComputeScatteringFunctions with constant textures folded (Material/*.cpp)
 MatTemplate material_template(const pbr_material_desc& m, bool multi) {
     MatTemplate t;
-    std::memset(&t, 0, sizeof(t));
-    if (m.type == PBR_MAT_NONE) return t;
-    t.valid = 1;
-    t.eta = 1;
-    auto add = [&](const Lobe& l) { t.lobes[t.nLobes++] = l; };
-    switch (m.type) {
-    case PBR_MAT_MATTE: {
-        float r[3];
-        clamp3(r, m.Kd);
-        float sig = clampf(m.sigma, 0, 90);
-        if (!is_black3(r)) {
-            Lobe l = lobe0();
-            put3(l.R, r);
-            l.type = BSDF_REFLECTION | BSDF_DIFFUSE;
-            if (sig == 0) l.kind = L_LAMBERT;
-            else {
-                l.kind = L_OREN;
-                float s = (kPi / 180) * sig;
-                float s2 = s * s;
-                l.A = 1.f - (s2 / (2.f * (s2 + 0.33f)));
-                l.B = 0.45f * s2 / (s2 + 0.09f);
-            }
-            add(l);
-        }
-        break;
-    }
-    case PBR_MAT_MIRROR: {
-        float r[3];
-        clamp3(r, m.Kr);
-        if (!is_black3(r)) {
-            Lobe l = lobe0();
-            l.kind = L_SPEC_R; l.type = BSDF_REFLECTION | BSDF_SPECULAR; l.fresnel = FR_NOOP;
-            put3(l.R, r);
-            add(l);
-        }
-        break;
-    }
-    case PBR_MAT_GLASS: {
-        t.eta = m.eta;
-        float R[3], T[3];
-        clamp3(R, m.Kr);
-        clamp3(T, m.Kt);
-        float ur = m.uroughness, vr = m.vroughness;
-        if (is_black3(R) && is_black3(T)) break;
-        bool spec = ur == 0 && vr == 0;
-        if (spec && multi) {
-            Lobe l = lobe0();
-            l.kind = L_FRESNEL_SPEC; l.type = BSDF_REFLECTION | BSDF_TRANSMISSION | BSDF_SPECULAR;
-            put3(l.R, R); put3(l.T, T); l.etaA = 1.f; l.etaB = m.eta;
-            add(l);
-            break;
-        }
-        if (m.remap_roughness) { ur = roughness_to_alpha(ur); vr = roughness_to_alpha(vr); }
-        if (!is_black3(R)) {
-            Lobe l = lobe0();
-            put3(l.R, R); l.fresnel = FR_DIEL; l.fEtaI = 1.f; l.fEtaT = m.eta;
-            if (spec) { l.kind = L_SPEC_R; l.type = BSDF_REFLECTION | BSDF_SPECULAR; }
-            else { l.kind = L_MF_R; l.type = BSDF_REFLECTION | BSDF_GLOSSY; set_tr(l, ur, vr); }
-            add(l);
-        }
-        if (!is_black3(T)) {
-            Lobe l = lobe0();
-            put3(l.T, T); l.etaA = 1.f; l.etaB = m.eta;
-            if (spec) { l.kind = L_SPEC_T; l.type = BSDF_TRANSMISSION | BSDF_SPECULAR; }
-            else { l.kind = L_MF_T; l.type = BSDF_TRANSMISSION | BSDF_GLOSSY; set_tr(l, ur, vr); }
-            add(l);
-        }
-        break;
-    }
-    case PBR_MAT_METAL: {
-        float ur = m.has_uv_roughness ? m.uroughness : m.roughness;
-        float vr = m.has_uv_roughness ? m.vroughness : m.roughness;
-        if (m.remap_roughness) { ur = roughness_to_alpha(ur); vr = roughness_to_alpha(vr); }
-        Lobe l = lobe0();
-        l.kind = L_MF_R; l.type = BSDF_REFLECTION | BSDF_GLOSSY;
-        l.R[0] = l.R[1] = l.R[2] = 1.f;
-        l.fresnel = FR_COND;
-        l.cEtaI[0] = l.cEtaI[1] = l.cEtaI[2] = 1.f;
-        put3(l.cEtaT, m.metal_eta);
-        put3(l.cK, m.metal_k);
-        set_tr(l, ur, vr);
-        add(l);
-        break;
-    }
-    case PBR_MAT_PLASTIC: {
-        float kd[3], ks[3];
-        clamp3(kd, m.Kd);
-        if (!is_black3(kd)) {
-            Lobe l = lobe0();
-            l.kind = L_LAMBERT; l.type = BSDF_REFLECTION | BSDF_DIFFUSE;
-            put3(l.R, kd);
-            add(l);
-        }
-        clamp3(ks, m.Ks);
-        if (!is_black3(ks)) {
-            float r = m.roughness;
-            if (m.remap_roughness) r = roughness_to_alpha(r);
-            Lobe l = lobe0();
-            l.kind = L_MF_R; l.type = BSDF_REFLECTION | BSDF_GLOSSY;
-            put3(l.R, ks);
-            l.fresnel = FR_DIEL; l.fEtaI = 1.5f; l.fEtaT = 1.f;
-            set_tr(l, r, r);
-            add(l);
-        }
-        break;
-    }
-    default:
-        fail("unknown material type");
-    }
+    if (!pbr::material_template(mat_params(m), multi, &t)) fail("unknown material type");
     return t;
 }
 
@@ -581,6 +477,46 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* b
         S->materials.push_back(material_template(d->materials[m], false));
         S->materials.push_back(material_template(d->materials[m], true));
     }
+    // 4b. image textures (ImageTexture, Texture/ImageTexture.cpp) and the materials that read them:
+    //     those get their lobes per hit (pbr_device.h textured_template)
+    if (d->n_textures < 0 || (d->n_textures > 0 && !d->textures)) fail("bad textures");
+    S->textures.assign(d->n_textures, TexDev());
+    S->texTexels.clear();
+    for (int i = 0; i < d->n_textures; ++i) build_image_texture(d->textures[i], &S->textures[i], &S->texTexels);
+    S->texMats.clear();
+    bool anyTex = false;
+    for (int m = 0; m < d->n_materials; ++m)
+        for (int k = 0; k < PBR_TEX_SLOTS; ++k) anyTex |= d->materials[m].tex[k] != 0;
+    if (anyTex) {
+        // which slots each material type reads (Material/*.cpp ComputeScatteringFunctions)
+        static const int reads[6][PBR_TEX_SLOTS] = {
+            {0, 0, 0, 0, 0, 0}, {1, 0, 0, 0, 1, 0}, {0, 0, 1, 0, 0, 0}, {0, 0, 1, 1, 0, 0}, {0, 0, 0, 0, 0, 0}, {1, 1, 0, 0, 0, 1}};
+        static const int isFloatSlot[PBR_TEX_SLOTS] = {0, 0, 0, 0, 1, 1};
+        S->texMats.resize(d->n_materials);
+        for (int m = 0; m < d->n_materials; ++m) {
+            const pbr_material_desc& md = d->materials[m];
+            TexMat& tm = S->texMats[m];
+            tm.p = mat_params(md);
+            bool textured = false;
+            for (int k = 0; k < PBR_TEX_SLOTS; ++k) {
+                tm.tex[k] = -1;
+                if (!md.tex[k]) continue;
+                const int ti = md.tex[k] - 1;
+                if (ti < 0 || ti >= d->n_textures) fail("texture index out of range");
+                if (md.type < 0 || md.type > PBR_MAT_PLASTIC || !reads[md.type][k])
+                    fail("this material type has no such texture slot");
+                if ((d->textures[ti].is_float != 0) != (isFloatSlot[k] != 0))
+                    fail("texture slot needs a " + std::string(isFloatSlot[k] ? "float" : "RGB") + " texture");
+                tm.tex[k] = ti;
+                textured = true;
+            }
+            S->materials[2 * m].textured = S->materials[2 * m + 1].textured = textured ? 1 : 0;
+            if (!textured) continue;
+            for (int i = 0; i < ns; ++i)
+                if (d->shapes[i].material == m && d->shapes[i].type != PBR_SHAPE_TRIANGLE_MESH)
+                    fail("image textures are supported on triangle meshes only (the reference's sphere is a stub)");
+        }
+    }
     // 5. media (HomogeneousMedium.h: sigma_t = sigma_s + sigma_a)
     for (int m = 0; m < d->n_media; ++m) {
         const pbr_medium_desc& md = d->media[m];
@@ -601,7 +537,7 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* b
         if (ld.type == PBR_LIGHT_POINT) {
             f3 p = xf_point(ld.light_to_world.m, mk(0, 0, 0));
             L.p[0] = p.x; L.p[1] = p.y; L.p[2] = p.z;
-            put3(L.L, ld.I);
+            mt_put3(L.L, ld.I);
             float P[3];
             for (int k = 0; k < 3; ++k) P[k] = (4 * kPi) * ld.I[k];   // PointLight::Power
             S->lightPower.push_back(0.212671f * P[0] + 0.715160f * P[1] + 0.072169f * P[2]);
@@ -612,7 +548,7 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* b
             int orig = firstPrim[ld.shape] + ld.triangle;
             L.primSlot = slotOf[orig];
             L.twoSided = ld.two_sided;
-            put3(L.L, ld.Le);
+            mt_put3(L.L, ld.Le);
             f3 p0 = vert(prims[orig], 0), p1 = vert(prims[orig], 1), p2 = vert(prims[orig], 2);
             L.area = (float)(0.5 * (double)len(cross(p1 - p0, p2 - p0)));   // Triangle::Area
             float P[3];

@@ -7,6 +7,7 @@
 
 #include "../../include/pbr_hip.h"
 #include "pbr_layout.h"
+#include "pbr_material.h"
 #include "pbr_math.h"
 
 namespace pbr {
@@ -56,6 +57,9 @@ struct HostScene {
     std::vector<int32_t> slotOf;            // prims index → BVH slot
     std::vector<int32_t> leafParent;        // per primitive slot that starts a leaf: parentQuad << 2 | raw slot, -1 at the root
     InfiniteHost inf;                       // the InfiniteAreaLight, if any (pbr_infinite.cpp)
+    std::vector<TexDev> textures;           // ImageTextures (level 0 + mapping)
+    std::vector<float> texTexels;           // their texels, 4 floats each
+    std::vector<TexMat> texMats;            // per material, only when some material is textured
 };
 
 // InfiniteAreaLight tables (Light/InfiniteAreaLight.cpp:7-61): the level-0 MIPMap image (resampled
@@ -72,6 +76,9 @@ void device_build_bvh(void* stream, const std::vector<float>& primBounds, int ma
                       std::vector<int32_t>* primIds, double* kernelMs);
 using BvhBuildFn = std::function<void(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
                                       std::vector<int32_t>* primIds)>;
+
+// ImageTexture's MIPMap level 0 (pbr_infinite.cpp): appends the texels, fills the record.
+void build_image_texture(const pbr_texture_desc& td, TexDev* out, std::vector<float>* texels);
 
 // Throws std::invalid_argument on a malformed descriptor.  `bvh` replaces the host SAH build.
 void build_host_scene(const pbr_scene_desc* desc, HostScene* out, const BvhBuildFn* bvh = nullptr);

@@ -221,7 +221,8 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                 isect.slot = slot;
                 isect.medIn = isect.medOut = -1;
                 BSDF bsdf;
-                if (!make_bsdf(S, mats, isect, false, &bsdf)) {
+                MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+                if (!make_bsdf<(LOBES & kTexturedLobes) != 0>(S, mats, isect, false, &bsdf, &texLocal)) {
                     cont = spawn_ray(isect, ray.d);        // Li(isect.SpawnRay(ray.d), depth)
                     pushNext = true;
                 } else {
@@ -385,6 +386,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
         Ray ray, cont;
         Isect isect;
         BSDF bsdf;
+        MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
         rgb L = sp(0.f);
         SState st;
         st.index = 0; st.dim = 0; st.px = st.py = 0; st.sid = 0;
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
                 else triangle_si(S, slot, ray, hr.y, hr.z, hr.w, flags, &isect);
                 isect.slot = slot;
                 isect.medIn = isect.medOut = -1;
-                if (!make_bsdf(S, mats, isect, false, &bsdf)) {
+                if (!make_bsdf<(LOBES & kTexturedLobes) != 0>(S, mats, isect, false, &bsdf, &texLocal)) {
                     cont = spawn_ray(isect, ray.d);        // Li(isect.SpawnRay(ray.d), depth)
                     pushNext = true;
                 } else {

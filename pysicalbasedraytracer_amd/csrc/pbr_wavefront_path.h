@@ -124,7 +124,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
             }
             bool alive = found && bounces < P.maxDepth;
             BSDF bsdf;
-            if (alive && !make_bsdf(S, mats, isect, true, &bsdf)) {
+            MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+            if (alive && !make_bsdf<(LOBES & kTexturedLobes) != 0>(S, mats, isect, true, &bsdf, &texLocal)) {
                 cont = spawn_ray(isect, ray.d);   // isect.SpawnRay(ray.d); bounces-- then ++: same bounce
                 pushNext = true;
                 alive = false;

@@ -122,6 +122,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             }
             bool alive = !black(beta), doRR = false;
             BSDF bsdf;
+            MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
             const Isect* ip = mediumEvent ? &mi : &isect;
             bool estimate = false;
             if (alive && mediumEvent) {
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                     else for (int k = 0; k < S.nInfinite; ++k) L = L + beta * light_Le(S, S.lights[S.infinite[k]], ray);
                 }
                 if (!found || bounces >= P.maxDepth) alive = false;
-                else if (!make_bsdf(S, mats, isect, true, &bsdf)) {
+                else if (!make_bsdf<(LOBES & kTexturedLobes) != 0>(S, mats, isect, true, &bsdf, &texLocal)) {
                     cont = spawn_ray(isect, ray.d);   // bounces--; continue: no Russian roulette
                     pushNext = true;
                     alive = false;

@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include "../../include/pbr_hip.h"
+#include <type_traits>
 #include "../csrc/pbr_xform.h"
 
 // ============================================================================ FrameBuffer
@@ -413,6 +414,35 @@ bool load_hdr(const char* file, int* w, int* h, int* comp, std::vector<float>* d
 }
 }  // namespace
 
+// ============================================================================ ImageTexture
+template <typename Tmemory, typename Treturn>
+ImageTexture<Tmemory, Treturn>::ImageTexture(std::unique_ptr<TextureMapping2D> m, const std::string& filename, bool doTrilinear,
+                                             float maxAniso, ImageWrap wrapMode, float scale, bool gamma)
+    : mapping(std::move(m)) {
+    img.mapping = dynamic_cast<const UVMapping2D*>(mapping.get());
+    img.doTrilinear = doTrilinear; img.maxAniso = maxAniso; img.wrapMode = wrapMode; img.scale = scale; img.gamma = gamma;
+    img.isFloat = std::is_same<Tmemory, float>::value;
+    g_stbiFlip = true;   // loadImage: stbi_set_flip_vertically_on_load(true), left set
+    if (filename.empty() || !load_hdr(filename.c_str(), &img.width, &img.height, &img.components, &img.data, true)) {
+        img.width = img.height = img.components = 0;
+        img.data.clear();
+    }
+}
+template <typename Tmemory, typename Treturn>
+ImageTexture<Tmemory, Treturn>::ImageTexture(std::unique_ptr<TextureMapping2D> m, int width, int height, int components,
+                                             std::vector<float> data, bool doTrilinear, float maxAniso, ImageWrap wrapMode,
+                                             float scale, bool gamma)
+    : mapping(std::move(m)) {
+    if (!data.empty() && (width <= 0 || height <= 0 || components < 3 || data.size() != (size_t)width * height * components))
+        throw std::invalid_argument("ImageTexture: bad image");
+    img.mapping = dynamic_cast<const UVMapping2D*>(mapping.get());
+    img.width = width; img.height = height; img.components = components; img.data = std::move(data);
+    img.doTrilinear = doTrilinear; img.maxAniso = maxAniso; img.wrapMode = wrapMode; img.scale = scale; img.gamma = gamma;
+    img.isFloat = std::is_same<Tmemory, float>::value;
+}
+template class ImageTexture<RGBSpectrum, Spectrum>;
+template class ImageTexture<float, float>;
+
 SkyBoxLight::SkyBoxLight(const Transform& LightToWorld, const Point3f& worldCenter, float worldRadius, const char* file, int nSamples)
     : Light(LightToWorld, MediumInterface(), nSamples), worldCenter(worldCenter), worldRadius(worldRadius) {
     loadImage(file);   // as the reference: a missing file leaves a black sky
@@ -525,6 +555,8 @@ struct FlatScene {
     std::vector<pbr_material_desc> materials;
     std::vector<pbr_light_desc> lights;
     std::vector<pbr_medium_desc> media;
+    std::vector<pbr_texture_desc> textures;
+    std::map<const void*, int> textureIndex;                 // ImageTexture → index (shared textures once)
     std::vector<std::vector<int32_t>> indexRuns;
     std::vector<std::shared_ptr<TriangleMesh>> meshes;   // keep P/N/UV alive
     std::vector<std::shared_ptr<SkyBoxLight>> skies;     // keep env data alive
@@ -543,20 +575,53 @@ float flt(const FloatTexture& t, const char* what) {
 }
 void put(float* d, const Spectrum& s) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
 
-pbr_material_desc material_desc(const Material* m) {
+// An image texture in a material slot: registered once per scene, referenced as index + 1.
+template <typename T>
+const ImageTextureData* image_of(const std::shared_ptr<Texture<T>>& t) {
+    if (auto* a = dynamic_cast<const ImageTexture<RGBSpectrum, Spectrum>*>(t.get())) return &a->Image();
+    if (auto* b = dynamic_cast<const ImageTexture<float, float>*>(t.get())) return &b->Image();
+    return nullptr;
+}
+int texture_slot(FlatScene* F, const ImageTextureData* im) {
+    auto it = F->textureIndex.find(im);
+    if (it != F->textureIndex.end()) return it->second + 1;
+    if (!im->mapping) throw std::invalid_argument("ImageTexture: only UVMapping2D is on the GPU path");
+    pbr_texture_desc t;
+    std::memset(&t, 0, sizeof(t));
+    t.is_float = im->isFloat;
+    t.width = im->width; t.height = im->height; t.components = im->components;
+    t.data = im->data.empty() ? nullptr : im->data.data();
+    t.scale = im->scale; t.gamma = im->gamma; t.wrap = (int)im->wrapMode;
+    t.trilinear = im->doTrilinear; t.max_aniso = im->maxAniso;
+    t.su = im->mapping->su; t.sv = im->mapping->sv; t.du = im->mapping->du; t.dv = im->mapping->dv;
+    F->textureIndex[im] = (int)F->textures.size();
+    F->textures.push_back(t);
+    return (int)F->textures.size();
+}
+
+pbr_material_desc material_desc(FlatScene* F, const Material* m) {
     pbr_material_desc d;
     std::memset(&d, 0, sizeof(d));
+    // a slot holding an ImageTexture is flattened as a texture reference, else as its constant
+    auto sl = [&](const SpectrumTexture& t, int slot, float* out, const char* what) {
+        if (const ImageTextureData* im = image_of(t)) d.tex[slot] = texture_slot(F, im);
+        else put(out, spec(t, what));
+    };
+    auto fl = [&](const FloatTexture& t, int slot, float* out, const char* what) {
+        if (const ImageTextureData* im = image_of(t)) d.tex[slot] = texture_slot(F, im);
+        else *out = flt(t, what);
+    };
     if (auto* x = dynamic_cast<const MatteMaterial*>(m)) {
         d.type = PBR_MAT_MATTE;
-        put(d.Kd, spec(x->Kd, "Kd"));
-        d.sigma = flt(x->sigma, "sigma");
+        sl(x->Kd, PBR_TEX_KD, d.Kd, "Kd");
+        fl(x->sigma, PBR_TEX_SIGMA, &d.sigma, "sigma");
     } else if (auto* x = dynamic_cast<const MirrorMaterial*>(m)) {
         d.type = PBR_MAT_MIRROR;
-        put(d.Kr, spec(x->Kr, "Kr"));
+        sl(x->Kr, PBR_TEX_KR, d.Kr, "Kr");
     } else if (auto* x = dynamic_cast<const GlassMaterial*>(m)) {
         d.type = PBR_MAT_GLASS;
-        put(d.Kr, spec(x->Kr, "Kr"));
-        put(d.Kt, spec(x->Kt, "Kt"));
+        sl(x->Kr, PBR_TEX_KR, d.Kr, "Kr");
+        sl(x->Kt, PBR_TEX_KT, d.Kt, "Kt");
         d.uroughness = flt(x->uRoughness, "uRoughness");
         d.vroughness = flt(x->vRoughness, "vRoughness");
         d.eta = flt(x->index, "index");
@@ -572,9 +637,9 @@ pbr_material_desc material_desc(const Material* m) {
         d.remap_roughness = x->remapRoughness;
     } else if (auto* x = dynamic_cast<const PlasticMaterial*>(m)) {
         d.type = PBR_MAT_PLASTIC;
-        put(d.Kd, spec(x->Kd, "Kd"));
-        put(d.Ks, spec(x->Ks, "Ks"));
-        d.roughness = flt(x->roughness, "roughness");
+        sl(x->Kd, PBR_TEX_KD, d.Kd, "Kd");
+        sl(x->Ks, PBR_TEX_KS, d.Ks, "Ks");
+        fl(x->roughness, PBR_TEX_ROUGHNESS, &d.roughness, "roughness");
         d.remap_roughness = x->remapRoughness;
     } else {
         throw std::invalid_argument("material type not on the GPU path");
@@ -624,7 +689,7 @@ std::shared_ptr<FlatScene> FlattenScene(const Scene& scene, const Medium* camera
         const Material* m = gp->material.get();
         if (!m || matIndex.count(m)) continue;
         matIndex[m] = (int)F->materials.size();
-        F->materials.push_back(material_desc(m));
+        F->materials.push_back(material_desc(F.get(), m));
     }
     // lights: scene.lights order; area lights are bound to their shape below
     std::unordered_map<const Light*, int> lightIndex;
@@ -764,6 +829,8 @@ std::shared_ptr<FlatScene> FlattenScene(const Scene& scene, const Medium* camera
     d.n_media = (int)F->media.size();
     d.media = F->media.data();
     d.max_prims_in_node = bvh->maxPrimsInNode;
+    d.n_textures = (int)F->textures.size();
+    d.textures = F->textures.data();
     return F;
 }
 

@@ -282,7 +282,7 @@ class Scene:
     """Reference-shaped scene: shapes are appended in `prims` order (main.cpp:247-348)."""
 
     def __init__(self):
-        self.shapes, self.materials, self.lights, self.media = [], [], [], []
+        self.shapes, self.materials, self.lights, self.media, self.textures = [], [], [], [], []
         self._keep = []
         self.max_prims_in_node = 1
         self.info = {}
@@ -325,6 +325,28 @@ class Scene:
         m.Ks[:] = list(ks)
         self.materials.append(m)
         return len(self.materials) - 1
+
+    def image_texture(self, image=None, is_float=False, scale=1.0, gamma=False, wrap=capi.WRAP_REPEAT,
+                      trilinear=False, max_aniso=8.0, mapping=(1.0, 1.0, 0.0, 0.0)):
+        """ImageTexture<RGBSpectrum, Spectrum> (or <float, float>) with UVMapping2D(su, sv, du, dv)
+        (Texture/ImageTexture.h:43-91): `image` [h, w, c>=3] float32 as loadImage's stbi_loadf
+        returns it (rows bottom-up), None → the 0.5 grey image GetTexture substitutes.  Returns its
+        index for set_texture()."""
+        t = capi.TextureDesc(is_float=int(is_float), scale=scale, gamma=int(gamma), wrap=wrap,
+                             trilinear=int(trilinear), max_aniso=max_aniso)
+        t.su, t.sv, t.du, t.dv = mapping
+        if image is not None:
+            img = np.ascontiguousarray(image, dtype=f32)
+            t.height, t.width, t.components = img.shape
+            t.data = capi.fptr(img)
+            self._keep.append(img)
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    def set_texture(self, material, slot, texture):
+        """Make a material parameter (capi.TEX_KD / KS / KR / KT / SIGMA / ROUGHNESS) read an image texture."""
+        self.materials[material].tex[slot] = texture + 1
+        return material
 
     def homogeneous_medium(self, sigma_a, sigma_s, g):
         md = capi.MediumDesc(g=g)
@@ -419,10 +441,12 @@ class Scene:
             (capi.MaterialDesc * max(1, len(self.materials)))(*self.materials),
             (capi.LightDesc * max(1, len(self.lights)))(*self.lights),
             (capi.MediumDesc * max(1, len(self.media)))(*self.media),
+            (capi.TextureDesc * max(1, len(self.textures)))(*self.textures),
         )
         d = capi.SceneDesc(abi_version=capi.ABI_VERSION, n_shapes=len(self.shapes), n_materials=len(self.materials),
                            n_lights=len(self.lights), n_media=len(self.media),
-                           max_prims_in_node=self.max_prims_in_node)
+                           max_prims_in_node=self.max_prims_in_node, n_textures=len(self.textures))
+        d.textures = C.cast(self._arrays[4], C.POINTER(capi.TextureDesc))
         d.shapes = C.cast(self._arrays[0], C.POINTER(capi.ShapeDesc))
         d.materials = C.cast(self._arrays[1], C.POINTER(capi.MaterialDesc))
         d.lights = C.cast(self._arrays[2], C.POINTER(capi.LightDesc))

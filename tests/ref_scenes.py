@@ -57,6 +57,16 @@ def box(lo, hi):
     return P, I
 
 
+def texture_image(w, h, seed):
+    """A deterministic RGB image with structure at texel scale (checks + gradients), rows as stbi_loadf
+    returns them."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    base = rng.random(3) * 0.6 + 0.2
+    img = np.stack([base[0] + 0.3 * ((x // 3 + y // 2) % 2), base[1] * (0.5 + x / w), base[2] * (0.4 + 0.6 * y / h)], -1)
+    return (img + rng.random((h, w, 3)) * 0.15).astype(np.float32)
+
+
 def inf_xform():   # main.cpp's InfinityLightToWorld = RotateX(-90) * RotateY(-0) * RotateZ(-50)
     return scenes.compose(scenes.compose(scenes.rotate_x(-90), scenes.rotate_y(-0.0)), scenes.rotate_z(-50))
 
@@ -121,6 +131,39 @@ def render_cases():
     Pl, Il = scenes.quad(2.45, 1.4, flip=True)
     s.area_light_mesh(Pl, Il, (6.0, 6.0, 6.0), s.matte((0.5, 0.5, 0.5)), n_samples=2)
     out["volpath_medium_box_interface"] = (s, scenes.render_desc(scenes.camera(40, 24, **CAM_C), capi.INTEGRATOR_VOLPATH, 16, 8))
+
+    # ImageTexture (Texture/ImageTexture.cpp): RGB and float textures, non-power-of-two images
+    # (Lanczos resample), the three wrap modes, gamma / scale, UVMapping2D offsets, mesh UVs and the
+    # default triangle UVs, and GetTexture's grey substitute for a missing image
+    for integ, name, spp, depth in ((capi.INTEGRATOR_WHITTED, "whitted", 4, 5), (capi.INTEGRATOR_PATH, "path", 8, 5)):
+        s = scenes.Scene()
+        P, I, UV = uv_patch()
+        img_a = scenes.rgbe_roundtrip(texture_image(37, 23, seed=1))
+        img_b = scenes.rgbe_roundtrip(texture_image(16, 8, seed=2))
+        img_c = scenes.rgbe_roundtrip(texture_image(21, 30, seed=3))
+        ta = s.image_texture(img_a, wrap=capi.WRAP_REPEAT, mapping=(2.0, 1.5, 0.1, -0.2))
+        tb = s.image_texture(img_b, wrap=capi.WRAP_CLAMP, gamma=True, scale=0.8)
+        tc = s.image_texture(img_c, wrap=capi.WRAP_BLACK, mapping=(1.3, 1.1, -0.15, 0.05))
+        tr = s.image_texture(img_c, is_float=True, scale=0.3, wrap=capi.WRAP_REPEAT, mapping=(3.0, 2.0, 0.0, 0.0))
+        ts = s.image_texture(img_b, is_float=True, scale=25.0, wrap=capi.WRAP_CLAMP, trilinear=True)
+        tg = s.image_texture(None, scale=1.6, gamma=True)
+        floor = s.set_texture(s.matte((0.5, 0.5, 0.5)), capi.TEX_KD, ta)
+        s.set_texture(floor, capi.TEX_SIGMA, ts)
+        s.mesh(P, I, floor, uv=UV)
+        dragon = s.set_texture(s.plastic((0.3, 0.3, 0.3), (0.2, 0.2, 0.2), rough=0.2, remap=True), capi.TEX_KD, tb)
+        s.set_texture(dragon, capi.TEX_KS, tc)
+        s.set_texture(dragon, capi.TEX_ROUGHNESS, tr)
+        s.mesh(m[0], m[1], dragon)
+        Pm, Im = scenes.quad(1.9, 4.0, flip=True)
+        s.mesh(Pm, Im, s.set_texture(s.mirror((0.9, 0.9, 0.9)), capi.TEX_KR, tc))
+        Pg, Ig = box((0.9, -0.9, 0.4), (1.4, -0.2, 0.9))
+        glass = s.set_texture(s.glass(eta=1.5, urough=0.0, vrough=0.0), capi.TEX_KT, tg)
+        s.mesh(Pg, Ig, s.set_texture(glass, capi.TEX_KR, tb))
+        if integ == capi.INTEGRATOR_PATH:
+            Pl, Il = scenes.quad(1.8, 0.8, flip=True)
+            s.area_light_mesh(Pl, Il, (5.0, 5.0, 5.0), s.matte((0.5, 0.5, 0.5)), n_samples=2)
+        s.point_light((1.0, 1.5, 1.8), (5.0, 5.0, 5.0))
+        out[f"{name}_image_textures"] = (s, scenes.render_desc(scenes.camera(40, 24, **CAM_C), integ, spp, depth))
 
     # two facing mirrors: deep Whitted recursion (maxDepth 12)
     s = scenes.Scene()
@@ -243,6 +286,10 @@ def scene_digest(scene, rd=None):
         h.update(_arr(ld.env_data, ld.env_width * ld.env_height * ld.env_components, C.c_float))
     for i in range(d.n_media):
         _fields(h, d.media[i])
+    for i in range(d.n_textures):
+        td = d.textures[i]
+        _fields(h, td)
+        h.update(_arr(td.data, td.width * td.height * td.components, C.c_float))
     if rd is not None:
         for f in ("integrator", "spp", "max_depth", "rr_threshold", "light_strategy", "sampler"):
             h.update(f"{f}={getattr(rd, f)!r};".encode())

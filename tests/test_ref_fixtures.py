@@ -30,6 +30,7 @@ MIN_EXACT = 0.98
 # the InfiniteAreaLight's MIPMap (Lanczos sinc weights, MIPMap.h:86-150) and spherical mapping
 # (acos/atan2 per lookup), and the medium's exp per segment, touch libm on most pixels
 MIN_EXACT_CASE = {"whitted_infinite_area_light": 0.7, "path_infinite_area_light": 0.7,
+                  "whitted_image_textures": 0.7, "path_image_textures": 0.7,
                   "volpath_medium_box_interface": 0.95}
 ULPS_REL = 4e-6
 
