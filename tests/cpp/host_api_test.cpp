@@ -117,6 +117,42 @@ void add_infinite(Built& b) {
     b.scene = std::make_unique<Scene>(b.scene->GetAggregate(), lights);
 }
 
+// main.cpp's getSmileFacePlasticMaterial idiom (main.cpp:63-78): an ImageTexture<RGBSpectrum,
+// Spectrum> with UVMapping2D(1, 1, 0, 0) as both Kd and Ks of a PlasticMaterial, here on a UV-mapped
+// floor, plus a float ImageTexture as the roughness and a textured matte tetrahedron (default UVs).
+void build_textured(Built& b, int W, int H) {
+    std::vector<float> img(13 * 9 * 3), rough(6 * 5 * 3);
+    for (int y = 0; y < 9; ++y)
+        for (int x = 0; x < 13; ++x)
+            for (int c = 0; c < 3; ++c) img[(y * 13 + x) * 3 + c] = ((x / 2 + y / 2) % 2 ? 0.8f : 0.15f) * (c == 1 ? 0.7f : 1.f);
+    for (size_t i = 0; i < rough.size(); ++i) rough[i] = 0.05f + 0.5f * (float)(i % 7) / 7.f;
+    std::shared_ptr<Texture<Spectrum>> kd = std::make_shared<ImageTexture<RGBSpectrum, Spectrum>>(
+        std::make_unique<UVMapping2D>(1.f, 1.f, 0.f, 0.f), 13, 9, 3, img, false, 8.f, ImageWrap::Repeat, 1.f, false);
+    std::shared_ptr<Texture<float>> rg = std::make_shared<ImageTexture<float, float>>(
+        std::make_unique<UVMapping2D>(2.f, 2.f, 0.1f, 0.f), 6, 5, 3, rough, false, 8.f, ImageWrap::Clamp, 1.f, false);
+    auto plastic = std::make_shared<PlasticMaterial>(kd, kd, rg, nullptr, true);
+    auto matte = std::make_shared<MatteMaterial>(std::make_shared<ImageTexture<RGBSpectrum, Spectrum>>(
+                                                     std::make_unique<UVMapping2D>(3.f, 3.f, 0.f, 0.f), 13, 9, 3, img, true, 8.f,
+                                                     ImageWrap::Black, 0.9f, true),
+                                                 fTex(0.f), nullptr);
+    std::vector<std::shared_ptr<Primitive>> prims;
+    const Transform* id = keep(b, Transform());
+    const Point3f fp[4] = {Point3f(-3, -1, -3), Point3f(3, -1, -3), Point3f(3, -1, 3), Point3f(-3, -1, 3)};
+    const Point2f fuv[4] = {Point2f(0, 0), Point2f(2.5f, 0), Point2f(2.5f, 2.f), Point2f(0, 2.f)};
+    const int fi[6] = {0, 2, 1, 0, 3, 2};
+    for (auto& s : CreateTriangleMesh(id, id, false, 2, fi, 4, fp, nullptr, nullptr, fuv))
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, plastic, nullptr, MediumInterface()));
+    const Point3f tp[4] = {Point3f(-0.8f, -0.9f, -0.5f), Point3f(0.8f, -0.9f, -0.5f), Point3f(0.f, -0.9f, 0.8f), Point3f(0.f, 0.6f, 0.f)};
+    const int ti[12] = {0, 2, 1, 0, 1, 3, 1, 2, 3, 2, 0, 3};
+    for (auto& s : CreateTriangleMesh(id, id, false, 4, ti, 4, tp, nullptr, nullptr, nullptr))
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, matte, nullptr, MediumInterface()));
+    std::vector<std::shared_ptr<Light>> lights;
+    lights.push_back(std::make_shared<PointLight>(Translate(Vector3f(0.5f, 2.f, 1.5f)), MediumInterface(), Spectrum(8.f)));
+    b.scene = std::make_unique<Scene>(std::make_shared<BVHAccel>(prims, 1), lights);
+    Transform lookat = LookAt(Point3f(0.f, 0.8f, 3.2f), Point3f(0.f, -0.5f, 0.f), Vector3f(0.f, 1.f, 0.f));
+    b.cam = std::shared_ptr<Camera>(CreatePerspectiveCamera(W, H, Inverse(lookat), nullptr));
+}
+
 // The same camera/render settings as SamplerIntegrator::Render builds, for the oracle.
 pbr_render_desc oracle_desc(const Built& b, const FlatScene& flat, int integrator, int spp, int depth, float rr) {
     auto* cam = dynamic_cast<const PerspectiveCamera*>(b.cam.get());
@@ -199,6 +235,15 @@ int run_cpu() {
     expect(d3->n_lights == 3 && d3->lights[2].type == PBR_LIGHT_INFINITE_AREA && d3->lights[2].env_width == 60 &&
                d3->lights[2].env_data != nullptr && a.scene->infiniteLights.size() == 1,
            "InfiniteAreaLight flattens with its image and is an infinite light");
+    Built t;
+    build_textured(t, 16, 16);
+    auto flat4 = FlattenScene(*t.scene, nullptr);
+    const pbr_scene_desc* d4 = SceneDesc(*flat4);
+    expect(d4->n_textures == 3 && d4->n_materials == 2 && d4->materials[0].tex[PBR_TEX_KD] == 1 &&
+               d4->materials[0].tex[PBR_TEX_KS] == 1 && d4->materials[0].tex[PBR_TEX_ROUGHNESS] == 2 &&
+               d4->textures[1].is_float == 1 && d4->textures[1].wrap == PBR_WRAP_CLAMP && d4->textures[2].gamma == 1 &&
+               d4->textures[0].width == 13 && d4->textures[0].data != nullptr,
+           "ImageTextures flatten once per texture, referenced from their material slots");
     // Render must fail loudly without a device (no CPU fallback)
     FrameBuffer fb;
     fb.InitBuffer(32, 32, 4);
@@ -434,6 +479,16 @@ int run_gpu() {
         auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
         auto v = std::make_shared<VolPathIntegrator>(10, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 1.f, "uniform", &fb);
         compare("VolPath homogeneous medium", b, v, fb, PBR_INTEGRATOR_VOLPATH, spp, 10, 1.f);
+    }
+    {
+        Built b;
+        const int W = 48, H = 36, spp = 8;
+        build_textured(b, W, H);
+        FrameBuffer fb;
+        fb.InitBuffer(W, H, 4);
+        auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        auto p = std::make_shared<PathIntegrator>(5, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 1.f, "uniform", &fb);
+        compare("Path ImageTexture plastic + matte", b, p, fb, PBR_INTEGRATOR_PATH, spp, 5, 1.f);
     }
     {   // main.cpp's own configuration: VolPath d10 "uniform" + the rotated InfiniteAreaLight
         Built b;
