@@ -842,6 +842,7 @@ void device_build_bvh(void* stream_, const std::vector<float>& primBounds, int m
     BVH_TRY(hipMemcpyAsync(nodes->data(), dNodes, (size_t)nRecs * sizeof(LinearBVHNode), hipMemcpyDeviceToHost, st));
     BVH_TRY(hipMemcpyAsync(primIds->data(), dIds, (size_t)N * 4, hipMemcpyDeviceToHost, st));
     BVH_TRY(hipStreamSynchronize(st));
+    interior_bounds_from_children(nodes);   // InitInterior's Union(c0, c1): the sign of a zero (pbr_scene.cpp)
     float ms = 0;
     BVH_TRY(hipEventElapsedTime(&ms, ev0, ev1));
     if (kernelMs) *kernelMs = ms;

@@ -335,6 +335,23 @@ void distribution1d(const std::vector<float>& f, std::vector<float>* cdf, float*
 
 }  // namespace
 
+// InitInterior (BVHAccel.cpp:33-38) overwrites an interior node's box with Union(c0->bounds,
+// c1->bounds).  The builders reduce the range before partitioning it, which gives the same values;
+// only the sign of a zero can differ (Union keeps its first operand on ties, -0 == +0), so the
+// boxes are rebuilt from the children, children first (reverse preorder).
+void interior_bounds_from_children(std::vector<LinearBVHNode>* nodes) {
+    std::vector<LinearBVHNode>& L = *nodes;
+    for (size_t i = L.size(); i-- > 0;) {
+        if (L[i].nPrimitives > 0) continue;
+        const LinearBVHNode& c0 = L[i + 1];
+        const LinearBVHNode& c1 = L[L[i].offset];
+        for (int a = 0; a < 3; ++a) {
+            L[i].pMin[a] = mn(c0.pMin[a], c1.pMin[a]);
+            L[i].pMax[a] = mx(c0.pMax[a], c1.pMax[a]);
+        }
+    }
+}
+
 void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
                     std::vector<int32_t>* primIds) {
     const size_t np = primBounds.size() / 6;
@@ -347,6 +364,7 @@ void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vec
         items[i].c = .5f * items[i].box.lo + .5f * items[i].box.hi;
     }
     SahBuilder(items, maxPrims, nodes, primIds).run();
+    interior_bounds_from_children(nodes);
 }
 
 void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* bvh) {

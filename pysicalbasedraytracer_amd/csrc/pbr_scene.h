@@ -74,6 +74,8 @@ void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vec
                     std::vector<int32_t>* primIds);
 void device_build_bvh(void* stream, const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
                       std::vector<int32_t>* primIds, double* kernelMs);
+// Interior boxes as InitInterior sets them: Union(first child, second child) (both builders end with it).
+void interior_bounds_from_children(std::vector<LinearBVHNode>* nodes);
 using BvhBuildFn = std::function<void(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
                                       std::vector<int32_t>* primIds)>;
 

@@ -108,3 +108,27 @@ def test_upload_with_either_builder(hip):
         got[where] = hip.get_bvh()
     hip.set_bvh_build(capi.BVH_BUILD_DEVICE)
     assert np.array_equal(got[0][0], got[1][0]) and np.array_equal(got[0][1], got[1][1])
+
+
+def test_signed_zero_bounds_match_the_oracle(hip):
+    """World vertices with -0 and +0 coordinates (-0 survives a transform only when every term is -0,
+    hence the -0 translation): interior boxes are InitInterior's Union(c0, c1), whose first operand
+    wins a -0/+0 tie (BVHAccel.cpp:33-38) — device and host builders against the oracle, bit for bit."""
+    import oracle_lib as O
+    rng = np.random.default_rng(5)
+    n = 400
+    P = rng.choice(np.array([-1.0, -0.5, 0.0, -0.0, 0.5], np.float32), size=(3 * n, 3)).astype(np.float32)
+    P[:, 1:] = -np.abs(P[:, 1:]) - 0.25      # y, z < 0: 0*y and 0*z are -0
+    I = np.arange(3 * n, dtype=np.int32).reshape(n, 3)
+    s = scenes.Scene()
+    s.mesh(P, I, s.matte((0.5, 0.5, 0.5)), xform=scenes.translate(-0.0, -0.0, -0.0))
+    s.point_light((0, 2, 0), (1, 1, 1))
+    cn, ci = O.build_bvh(s)
+    box = cn.view(np.float32).reshape(-1, 8)[:, :6]
+    assert ((box == 0) & np.signbit(box)).any() and ((box == 0) & ~np.signbit(box)).any()
+    for where in (capi.BVH_BUILD_HOST, capi.BVH_BUILD_DEVICE):
+        hip.set_bvh_build(where)
+        hip.upload(s)
+        gn, gi = hip.get_bvh()
+        assert np.array_equal(gi, ci) and np.array_equal(gn, cn), where
+    hip.set_bvh_build(capi.BVH_BUILD_DEVICE)
