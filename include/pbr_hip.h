@@ -81,6 +81,8 @@ enum pbr_integrator_type {
 };
 enum pbr_sampler_type { PBR_SAMPLER_HALTON = 0, PBR_SAMPLER_SOBOL = 1 };
 enum pbr_light_strategy { PBR_LIGHTS_UNIFORM = 0, PBR_LIGHTS_POWER = 1 };
+/* BVHAccel::SplitMethod (Accelerator/BVHAccel.h:18); HLBVH falls through to SAH (BVHAccel.cpp:135-160). */
+enum pbr_split_method { PBR_SPLIT_SAH = 0, PBR_SPLIT_HLBVH = 1, PBR_SPLIT_MIDDLE = 2, PBR_SPLIT_EQUAL_COUNTS = 3 };
 
 /* A reference Transform holds both m and mInv (Core/Transform.h:49-60); so do we. Row-major. */
 typedef struct pbr_transform {
@@ -198,6 +200,7 @@ typedef struct pbr_scene_desc {
     int max_prims_in_node;      /* BVHAccel maxPrimsInNode (main.cpp:385 uses 1) */
     int n_textures;
     const pbr_texture_desc* textures;
+    int split_method;           /* pbr_split_method (BVHAccel.h:18); Middle / EqualCounts build on the host */
 } pbr_scene_desc;
 
 /* CreatePerspectiveCamera (Camera/Perspective.cpp:84-104) inputs. */

@@ -147,9 +147,10 @@ struct BucketInfo { int count = 0; Bounds3 bounds; };
 struct Builder {
     const std::vector<Prim>& in;
     int maxPrimsInNode;
+    int splitMethod;                 // BVHAccel::SplitMethod (BVHAccel.h:18)
     std::vector<std::unique_ptr<BuildNode>> pool;
     std::vector<int> ordered;
-    Builder(const std::vector<Prim>& p, int m) : in(p), maxPrimsInNode(std::min(255, m)) {}
+    Builder(const std::vector<Prim>& p, int m, int split) : in(p), maxPrimsInNode(std::min(255, m)), splitMethod(split) {}
 
     BuildNode* leaf(BuildNode* node, std::vector<PrimInfo>& pi, int start, int end, const Bounds3& bounds) {
         int first = (int)ordered.size();
@@ -172,7 +173,21 @@ struct Builder {
         int dim = centroidBounds.MaximumExtent();
         int mid = (start + end) / 2;
         if (centroidBounds.pMax[dim] == centroidBounds.pMin[dim]) return leaf(node, pi, start, end, bounds);
-        if (nPrimitives <= 2) {
+        auto cmp = [dim](const PrimInfo& a, const PrimInfo& b) { return a.centroid[dim] < b.centroid[dim]; };
+        bool done = false;
+        if (splitMethod == PBR_SPLIT_MIDDLE) {   // BVHAccel.cpp:136-148
+            float pmid = (centroidBounds.pMin[dim] + centroidBounds.pMax[dim]) / 2;
+            PrimInfo* midPtr = std::partition(&pi[start], &pi[end - 1] + 1, [dim, pmid](const PrimInfo& p) { return p.centroid[dim] < pmid; });
+            mid = midPtr - &pi[0];
+            done = mid != start && mid != end;
+        }
+        if (!done && (splitMethod == PBR_SPLIT_MIDDLE || splitMethod == PBR_SPLIT_EQUAL_COUNTS)) {   // :149-158
+            mid = (start + end) / 2;
+            std::nth_element(&pi[start], &pi[mid], &pi[end - 1] + 1, cmp);
+            done = true;
+        }
+        if (done) {
+        } else if (nPrimitives <= 2) {
             mid = (start + end) / 2;
             std::nth_element(&pi[start], &pi[mid], &pi[end - 1] + 1,
                              [dim](const PrimInfo& a, const PrimInfo& b) { return a.centroid[dim] < b.centroid[dim]; });
@@ -243,7 +258,7 @@ struct Builder {
     }
 };
 
-static void BuildBVH(Scene& s, std::vector<Prim>& prims, int maxPrimsInNode) {
+static void BuildBVH(Scene& s, std::vector<Prim>& prims, int maxPrimsInNode, int splitMethod) {
     if (prims.empty()) return;
     std::vector<PrimInfo> pi(prims.size());
     for (size_t i = 0; i < prims.size(); ++i) {
@@ -252,7 +267,7 @@ static void BuildBVH(Scene& s, std::vector<Prim>& prims, int maxPrimsInNode) {
         pi[i].bounds = b;
         pi[i].centroid = .5f * b.pMin + .5f * b.pMax;
     }
-    Builder bld(prims, maxPrimsInNode);
+    Builder bld(prims, maxPrimsInNode, splitMethod);
     int total = 0;
     BuildNode* root = bld.build(pi, 0, (int)prims.size(), &total);
     s.nodes.assign(total, OrcLinearBVHNode());
@@ -1646,7 +1661,7 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
         }
         s->lights.push_back(std::move(l));
     }
-    BuildBVH(*s, prims, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1);
+    BuildBVH(*s, prims, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1, d->split_method);
     for (Light& l : s->lights)
         if (l.type == PBR_LIGHT_DIFFUSE_AREA) l.area = TriangleArea(*s, s->prims[s->primOfOriginal[l.prim]]);
     for (Light& l : s->lights)

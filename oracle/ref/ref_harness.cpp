@@ -311,7 +311,8 @@ std::unique_ptr<RefScene> build(const pbr_scene_desc* d) {
             r->primIndex[r->prims[k].get()] = k;
         }
     }
-    r->bvh = std::make_shared<BVHAccel>(r->prims, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1, BVHAccel::SplitMethod::SAH);
+    r->bvh = std::make_shared<BVHAccel>(r->prims, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1,
+                                        (BVHAccel::SplitMethod)d->split_method);
     r->scene.reset(new Scene(r->bvh, r->lights));
     return r;
 }

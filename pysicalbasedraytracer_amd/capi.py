@@ -24,6 +24,7 @@ INTEGRATOR_WHITTED, INTEGRATOR_PATH, INTEGRATOR_VOLPATH = 0, 1, 2
 SAMPLER_HALTON, SAMPLER_SOBOL = 0, 1
 LIGHTS_UNIFORM, LIGHTS_POWER = 0, 1
 BVH_BUILD_HOST, BVH_BUILD_DEVICE = 0, 1
+SPLIT_SAH, SPLIT_HLBVH, SPLIT_MIDDLE, SPLIT_EQUAL_COUNTS = 0, 1, 2, 3
 WRAP_REPEAT, WRAP_BLACK, WRAP_CLAMP = 0, 1, 2
 TEX_KD, TEX_KS, TEX_KR, TEX_KT, TEX_SIGMA, TEX_ROUGHNESS = range(6)
 
@@ -132,6 +133,7 @@ class SceneDesc(C.Structure):
         ("max_prims_in_node", C.c_int),
         ("n_textures", C.c_int),
         ("textures", C.POINTER(TextureDesc)),
+        ("split_method", C.c_int),
     ]
 
 

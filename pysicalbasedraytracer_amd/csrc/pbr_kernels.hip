@@ -824,6 +824,7 @@ struct pbr_hip_ctx {
     unsigned long long profHost[KP_COUNT][kProfFields] = {};
     int bvhBuild = PBR_BVH_BUILD_DEVICE; // which SAH builder pbr_hip_upload_scene runs
     double bvhMs = 0, bvhKernelMs = 0;   // the last upload's BVH build: wall / device time
+    int bvhWhereLast = PBR_BVH_BUILD_HOST;   // ... and where it ran (Middle / EqualCounts: always the host)
     DevBuf dGuard;                       // DeviceScene::guard (kGuard* bits of tripped safety bounds)
     int* guardHost = nullptr;            // pinned copy, refreshed at the end of frames that can trip one
 };
@@ -1554,7 +1555,7 @@ int pbr_hip_set_bvh_build(pbr_hip_ctx* ctx, int where) {
 int pbr_hip_bvh_build_info(pbr_hip_ctx* ctx, int* where, double* ms, double* kernel_ms) {
     if (!ctx) return PBR_E_INVALID;
     if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
-    if (where) *where = ctx->bvhBuild;
+    if (where) *where = ctx->bvhWhereLast;
     if (ms) *ms = ctx->bvhMs;
     if (kernel_ms) *kernel_ms = ctx->bvhKernelMs;
     return PBR_OK;
@@ -1666,9 +1667,11 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     if (int rc = drain(ctx)) return rc;
     try {
         ctx->bvhMs = ctx->bvhKernelMs = 0;
+        ctx->bvhWhereLast = PBR_BVH_BUILD_HOST;
         BvhBuildFn timed = [ctx](const std::vector<float>& pb, int maxPrims, std::vector<LinearBVHNode>* nodes,
                                  std::vector<int32_t>* ids) {
             const auto t0 = std::chrono::steady_clock::now();
+            ctx->bvhWhereLast = ctx->bvhBuild;
             if (ctx->bvhBuild == PBR_BVH_BUILD_DEVICE) device_build_bvh(ctx->stream, pb, maxPrims, nodes, ids, &ctx->bvhKernelMs);
             else host_build_bvh(pb, maxPrims, nodes, ids);
             ctx->bvhMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -183,8 +183,8 @@ void build_wide_nodes(HostScene* S) {
 // Bucketed SAH builder writing LinearBVHNodes in depth-first preorder.
 class SahBuilder {
   public:
-    SahBuilder(std::vector<Item>& items, int maxPrims, std::vector<LinearBVHNode>* nodes, std::vector<int32_t>* order)
-        : it_(items), maxPrims_(std::min(255, maxPrims)), nodes_(nodes), order_(order) {}
+    SahBuilder(std::vector<Item>& items, int maxPrims, int splitMethod, std::vector<LinearBVHNode>* nodes, std::vector<int32_t>* order)
+        : it_(items), maxPrims_(std::min(255, maxPrims)), split_(splitMethod), nodes_(nodes), order_(order) {}
 
     void run() {
         nodes_->clear();
@@ -254,6 +254,18 @@ class SahBuilder {
         if (get(cb.hi, dim) == get(cb.lo, dim)) return false;
         Item* first = it_.data() + s;
         Item* last = it_.data() + e;
+        auto byCentroid = [dim](const Item& a, const Item& c) { return get(a.c, dim) < get(c.c, dim); };
+        if (split_ == PBR_SPLIT_MIDDLE) {   // BVHAccel.cpp:136-148, falling through to EqualCounts
+            float pmid = (get(cb.lo, dim) + get(cb.hi, dim)) / 2;
+            Item* pm = std::partition(first, last, [dim, pmid](const Item& p) { return get(p.c, dim) < pmid; });
+            *mid = (int)(pm - it_.data());
+            if (*mid != s && *mid != e) return true;
+        }
+        if (split_ == PBR_SPLIT_MIDDLE || split_ == PBR_SPLIT_EQUAL_COUNTS) {   // :149-158
+            *mid = (s + e) / 2;
+            std::nth_element(first, it_.data() + *mid, last, byCentroid);
+            return true;
+        }
         if (n <= 2) {
             *mid = (s + e) / 2;
             std::nth_element(first, it_.data() + *mid, last,
@@ -296,6 +308,7 @@ class SahBuilder {
     std::vector<Leaf> leaves_;
     std::vector<Item>& it_;
     int maxPrims_;
+    int split_;
     std::vector<LinearBVHNode>* nodes_;
     std::vector<int32_t>* order_;
 };
@@ -353,7 +366,7 @@ void interior_bounds_from_children(std::vector<LinearBVHNode>* nodes) {
 }
 
 void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
-                    std::vector<int32_t>* primIds) {
+                    std::vector<int32_t>* primIds, int splitMethod) {
     const size_t np = primBounds.size() / 6;
     std::vector<Item> items(np);
     for (size_t i = 0; i < np; ++i) {   // BVHPrimitiveInfo (BVHAccel.cpp:24-31)
@@ -363,7 +376,7 @@ void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vec
         items[i].box.hi = mk(p[3], p[4], p[5]);
         items[i].c = .5f * items[i].box.lo + .5f * items[i].box.hi;
     }
-    SahBuilder(items, maxPrims, nodes, primIds).run();
+    SahBuilder(items, maxPrims, splitMethod, nodes, primIds).run();
     interior_bounds_from_children(nodes);
 }
 
@@ -441,8 +454,11 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* b
         S->primBounds.insert(S->primBounds.end(), {b.lo.x, b.lo.y, b.lo.z, b.hi.x, b.hi.y, b.hi.z});
     }
     const int maxPrims = d->max_prims_in_node > 0 ? d->max_prims_in_node : 1;
-    if (bvh) (*bvh)(S->primBounds, maxPrims, &S->nodes, &S->primIds);
-    else host_build_bvh(S->primBounds, maxPrims, &S->nodes, &S->primIds);
+    if (d->split_method < PBR_SPLIT_SAH || d->split_method > PBR_SPLIT_EQUAL_COUNTS) fail("unknown split method");
+    // the device builder is the SAH one (HLBVH is SAH in the reference); Middle / EqualCounts build here
+    const bool sah = d->split_method == PBR_SPLIT_SAH || d->split_method == PBR_SPLIT_HLBVH;
+    if (bvh && sah) (*bvh)(S->primBounds, maxPrims, &S->nodes, &S->primIds);
+    else host_build_bvh(S->primBounds, maxPrims, &S->nodes, &S->primIds, d->split_method);
     if (S->primIds.size() != (size_t)np) fail("BVH build returned a wrong primitive count");
     // 3. primitive payloads in BVH order
     std::vector<int>& slotOf = S->slotOf;

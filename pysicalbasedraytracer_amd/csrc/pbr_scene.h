@@ -71,7 +71,7 @@ void build_infinite_light(const pbr_light_desc& ld, const float worldMin[3], con
 // (pbr_scene.cpp) and the device builder (pbr_bvh_build.hip, on `stream`; device time in kernelMs;
 // throws std::runtime_error on a HIP failure) produce identical arrays.
 void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
-                    std::vector<int32_t>* primIds);
+                    std::vector<int32_t>* primIds, int splitMethod = PBR_SPLIT_SAH);
 void device_build_bvh(void* stream, const std::vector<float>& primBounds, int maxPrims, std::vector<LinearBVHNode>* nodes,
                       std::vector<int32_t>* primIds, double* kernelMs);
 // Interior boxes as InitInterior sets them: Union(first child, second child) (both builders end with it).

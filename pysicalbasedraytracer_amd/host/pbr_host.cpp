@@ -476,10 +476,8 @@ InfiniteAreaLight::InfiniteAreaLight(const Transform& LightToWorld, const Spectr
 // ============================================================================ aggregate, scene, camera, sampler
 BVHAccel::BVHAccel(std::vector<std::shared_ptr<Primitive>> p, int maxPrimsInNode, SplitMethod splitMethod)
     : maxPrimsInNode(std::min(255, maxPrimsInNode)), splitMethod(splitMethod), primitives(std::move(p)) {
-    // BVHAccel.cpp:131-160: the reference's switch has no HLBVH branch, so HLBVH builds with SAH
-    if (splitMethod == SplitMethod::Middle || splitMethod == SplitMethod::EqualCounts)
-        throw std::invalid_argument("BVHAccel: only SplitMethod::SAH (and HLBVH, which the reference builds with SAH) "
-                                    "is on the GPU path");
+    // BVHAccel.cpp:131-160: the reference's switch has no HLBVH branch, so HLBVH builds with SAH;
+    // Middle and EqualCounts are flattened as such (pbr_scene_desc.split_method) and built on the host
 }
 
 Bounds3f::Bounds3f() {
@@ -829,6 +827,7 @@ std::shared_ptr<FlatScene> FlattenScene(const Scene& scene, const Medium* camera
     d.n_media = (int)F->media.size();
     d.media = F->media.data();
     d.max_prims_in_node = bvh->maxPrimsInNode;
+    d.split_method = (int)bvh->splitMethod;   // SAH, HLBVH, Middle, EqualCounts = pbr_split_method
     d.n_textures = (int)F->textures.size();
     d.textures = F->textures.data();
     return F;

@@ -285,6 +285,7 @@ class Scene:
         self.shapes, self.materials, self.lights, self.media, self.textures = [], [], [], [], []
         self._keep = []
         self.max_prims_in_node = 1
+        self.split_method = capi.SPLIT_SAH
         self.info = {}
 
     # materials (Main/main.cpp:147-239 recipes)
@@ -445,7 +446,8 @@ class Scene:
         )
         d = capi.SceneDesc(abi_version=capi.ABI_VERSION, n_shapes=len(self.shapes), n_materials=len(self.materials),
                            n_lights=len(self.lights), n_media=len(self.media),
-                           max_prims_in_node=self.max_prims_in_node, n_textures=len(self.textures))
+                           max_prims_in_node=self.max_prims_in_node, n_textures=len(self.textures),
+                           split_method=self.split_method)
         d.textures = C.cast(self._arrays[4], C.POINTER(capi.TextureDesc))
         d.shapes = C.cast(self._arrays[0], C.POINTER(capi.ShapeDesc))
         d.materials = C.cast(self._arrays[1], C.POINTER(capi.MaterialDesc))

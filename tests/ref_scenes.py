@@ -200,6 +200,17 @@ def bvh_cases():
     s.mesh(m[0], m[1], s.matte((0.5, 0.5, 0.5)))
     s.max_prims_in_node = 4
     out["dragon_1152_max4"] = s
+    # the other SplitMethods (BVHAccel.cpp:136-158): Middle (std::partition at the centroid midpoint,
+    # falling through to EqualCounts when one side is empty) and EqualCounts (std::nth_element);
+    # HLBVH builds with SAH.  A grid of duplicated triangles makes Middle fall through.
+    for name, split in (("middle", capi.SPLIT_MIDDLE), ("equal_counts", capi.SPLIT_EQUAL_COUNTS), ("hlbvh", capi.SPLIT_HLBVH)):
+        s = scenes.Scene()
+        s.mesh(m[0], m[1], s.matte((0.5, 0.5, 0.5)))
+        Pq, Iq = scenes.quad(-1.2, 2.0)
+        for k in range(3):
+            s.mesh(Pq, Iq, s.matte((0.5, 0.5, 0.5)))
+        s.split_method = split
+        out[f"dragon_1152_{name}"] = s
     return out
 
 
