@@ -6,11 +6,11 @@
  * bench.py's cpu_baseline leg may load liboracle.so; the product path (pysicalbasedraytracer_amd)
  * never links or calls it.
  *
- * Parity pinning: the reference itself is unbuildable in this image
- * (MSVC-only: backslash include paths, the _BitScanReverse intrinsic, __declspec, and a
- * double-destroy crash that needs a source patch), so this restatement is pinned by the reference
- * outputs recorded in SURVEY.md §4 (Halton bit patterns, the single-pixel Li capture, struct
- * sizes) and by analytic known-answer tests.
+ * Parity pinning: this restatement is checked against outputs of the reference
+ * itself — oracle/_ref/libpbr_ref.so, compiled from the reference's unmodified sources by
+ * oracle/ref/Makefile — recorded in tests/golden/ref_fixtures.json (renders, whole frames, BVH
+ * node-array hashes, hit records, camera rays), plus the Halton / Li captures of SURVEY.md §4 and
+ * analytic known-answer tests where the reference cannot speak (its sphere is a stub).
  *
  * Deliberate, documented deviations from the reference (all listed in DESIGN.md):
  *   F1  the Render loop iterates x∈[0,W), y∈[0,H) (the reference swaps its axes)
