@@ -36,7 +36,9 @@ constexpr float gamma_n(int n) {
     return (float)((n * (1.1920928955078125e-07 * 0.5)) / (1 - n * (1.1920928955078125e-07 * 0.5)));
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PBR_INLINE_TRANS)
+#define PBR_TRANS PBR_HD
+#elif defined(__HIP_DEVICE_COMPILE__)
 #define PBR_TRANS __host__ __device__ __attribute__((noinline))
 #else
 #define PBR_TRANS PBR_HD

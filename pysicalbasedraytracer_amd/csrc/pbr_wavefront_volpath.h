@@ -35,7 +35,10 @@ __device__ __forceinline__ void set_interface(const DeviceScene& S, Isect* it, i
 }
 
 // Waves per SIMD (C5: 2 → 1940 ms, 3 → 1832-1846, 4 → 1898)
-template <int LOBES, bool MATS_LDS, int OCC = 3>
+#ifndef PBR_WFV_OCC
+#define PBR_WFV_OCC 3
+#endif
+template <int LOBES, bool MATS_LDS, int OCC = PBR_WFV_OCC>
 __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0) {
     WfpParams& X = V.X;
     WfParams& W = X.W;
