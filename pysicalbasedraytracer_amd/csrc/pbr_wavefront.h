@@ -73,6 +73,31 @@ struct WfParams {
     unsigned long long* prof;   // profile counters (ProfKind rows) while profiling, else null
 };
 
+// XCD-aware workgroup order: the dispatcher deals workgroup b to XCD b % 8, each XCD with its own
+// L2.  Kernels whose grid is a whole number of rounds of 8 runs of K = PBR_XCD_RUN workgroups (the
+// camera kernels, the kWfBlocks-wide shade kernels, resolve) work on a logical workgroup such
+// that K consecutive logical workgroups — consecutive queue entries, so neighbouring pixels — run on
+// one XCD, the runs dealt round-robin over the XCDs; that XCD's L2 then holds the part of the BVH,
+// mesh and sky the run touches.  Queue segments are numbered by the logical workgroup, so queue
+// order is unchanged, and records are indexed by sample, so frames are bit-identical either way.
+// Measured (profiles/r2_xcd_ab.log): K = 128 C2 -1.2..-1.6%, C3 -3.0..-3.9%, C5 ±0.3%; one
+// contiguous band per XCD C2 +5.6% (unbalanced); runs of 32 in the resident-size traversal grids
+// (1792 = 7 × 256 workgroups, not a multiple of 8 × 128, so left in dispatch order here) C2 +1%.
+#ifndef PBR_XCD_RUN
+#define PBR_XCD_RUN 128
+#endif
+constexpr int kXcds = 8;
+__device__ __forceinline__ int wf_block() {
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    constexpr int K = PBR_XCD_RUN;
+    if constexpr (K == 0) return b;
+    else {
+        if (G % (kXcds * K) != 0) return b;
+        const int x = b % kXcds, k = b / kXcds;   // the k-th workgroup dealt to XCD x
+        return ((k / K) * kXcds + x) * K + k % K;
+    }
+}
+
 // LDS counter; the wave's lanes must be converged
 __device__ __forceinline__ int wave_push(int* counter, bool pred) {
     unsigned long long m = __ballot(pred);
@@ -121,7 +146,7 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams W) {
     const KParams& P = W.P;
-    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    int q = wf_block() * blockDim.x + threadIdx.x;
     if (q >= W.nSamples) return;
     int lp = q / P.spp, s = q - lp * P.spp;
     int x, y;
@@ -149,7 +174,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_extend(WfParams W) {
     const int n = seg_scan(W.cur.segCount);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
         float4 o = W.cur.o[q], d = W.cur.d[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -189,9 +214,9 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;   // <= segCap / 256: a segment holds all pushes
-    const int base = blockIdx.x * W.segCap, sbase = blockIdx.x * W.shadowSegCap;
+    const int base = wf_block() * W.segCap, sbase = wf_block() * W.shadowSegCap;
     for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
-        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
         const bool active = i < n;
         const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
         bool pushShadow = false, pushNext = false;
@@ -317,14 +342,14 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) { W.shadowSeg[blockIdx.x] = s_push[0]; W.next.segCount[blockIdx.x] = s_push[1]; }
+    if (threadIdx.x == 0) { W.shadowSeg[wf_block()] = s_push[0]; W.next.segCount[wf_block()] = s_push[1]; }
 }
 
 // any-hit for the shadow queue; a visible light adds its contribution to the emitting level
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.shadowSegCap, i);
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -375,10 +400,10 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
     const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;
-    const int base = blockIdx.x * W.segCap, sbase = blockIdx.x * W.shadowSegCap;
+    const int base = wf_block() * W.segCap, sbase = wf_block() * W.shadowSegCap;
     const int nL = W.nLightsML;
     for (int it = 0; it < nIter; ++it) {
-        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
         const bool active = i < n;
         const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
         bool pushNext = false, shading = false, nonSpecular = false;
@@ -487,14 +512,14 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) { W.shadowSeg[blockIdx.x] = s_push[0]; W.next.segCount[blockIdx.x] = s_push[1]; }
+    if (threadIdx.x == 0) { W.shadowSeg[wf_block()] = s_push[0]; W.next.segCount[wf_block()] = s_push[1]; }
 }
 
 // any-hit for the multi-light shadow queue: the ray's (level, light) record turns visible
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow_ml(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.shadowSegCap, i);
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -536,7 +561,7 @@ __global__ __launch_bounds__(256) void k_wf_finish(WfParams W) {
     const KParams& P = W.P;
     const int spp = P.spp, pitch = min(spp, kFinishSamples) + 1;
     const int pb = finish_pixels(spp);
-    const int lp0 = blockIdx.x * pb;
+    const int lp0 = blockIdx.x * pb;   // dispatch order: the XCD-run order made finish 28% slower
     const int npx = min(pb, W.chunkPix - lp0);
     // spp > kFinishSamples: one pixel per block, folded and summed in slices of kFinishSamples
     const int slice = min(spp, kFinishSamples);

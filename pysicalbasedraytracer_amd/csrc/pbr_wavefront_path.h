@@ -42,7 +42,7 @@ template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpParams X) {
     WfParams& W = X.W;
     const KParams& P = W.P;
-    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    int q = wf_block() * blockDim.x + threadIdx.x;
     if (q >= W.nSamples) return;
     int lp = q / P.spp, s = q - lp * P.spp;
     int x, y;
@@ -88,9 +88,9 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
     const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;
-    const int base = blockIdx.x * W.segCap;
+    const int base = wf_block() * W.segCap;
     for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
-        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
         const bool active = i < n;
         const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
         bool pushShadow = false, pushProbe = false, pushDirect = false, pushNext = false;
@@ -259,10 +259,10 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        W.shadowSeg[blockIdx.x] = s_push[0];
-        X.probeSeg[blockIdx.x] = s_push[1];
-        X.directSeg[blockIdx.x] = s_push[2];
-        W.next.segCount[blockIdx.x] = s_push[3];
+        W.shadowSeg[wf_block()] = s_push[0];
+        X.probeSeg[wf_block()] = s_push[1];
+        X.directSeg[wf_block()] = s_push[2];
+        W.next.segCount[wf_block()] = s_push[3];
     }
 }
 
@@ -271,7 +271,7 @@ template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_shadow(WfpParams X) {
     WfParams& W = X.W;
     const int n = seg_scan(W.shadowSeg);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_probe(WfpParams X) {
     WfParams& W = X.W;
     const DeviceScene& S = W.P.S;
     const int n = seg_scan(X.probeSeg);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
         float4 o = X.po[q], d = X.pd[q];
         Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_probe(WfpParams X) {
 __global__ __launch_bounds__(256) void k_wfp_resolve(WfpParams X) {
     WfParams& W = X.W;
     const int n = seg_scan(X.directSeg);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int id = X.directId[seg_pos(W.segCap, i)];
         const int fl = X.dFlags[id];
         const float4 a = X.dA[id], bt = X.dBeta[id];
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256) void k_wfp_finish(WfpParams X) {
     const KParams& P = W.P;
     const int spp = P.spp, pitch = min(spp, kFinishSamples) + 1;
     const int pb = finish_pixels(spp);
-    const int lp0 = blockIdx.x * pb;
+    const int lp0 = blockIdx.x * pb;   // dispatch order: the XCD-run order made finish 28% slower
     const int npx = min(pb, W.chunkPix - lp0);
     const int slice = min(spp, kFinishSamples);
     float acc = 0.f;

@@ -60,9 +60,9 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
     const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;
-    const int base = blockIdx.x * W.segCap;
+    const int base = wf_block() * W.segCap;
     for (int it = 0; it < nIter; ++it) {
-        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
         const bool active = i < n;
         const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
         bool pushTr = false, pushProbe = false, pushDirect = false, pushNext = false;
@@ -292,10 +292,10 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        V.trSeg[blockIdx.x] = s_push[0];
-        X.probeSeg[blockIdx.x] = s_push[1];
-        X.directSeg[blockIdx.x] = s_push[2];
-        W.next.segCount[blockIdx.x] = s_push[3];
+        V.trSeg[wf_block()] = s_push[0];
+        X.probeSeg[wf_block()] = s_push[1];
+        X.directSeg[wf_block()] = s_push[2];
+        W.next.segCount[wf_block()] = s_push[3];
     }
 }
 
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfv_tr(WfvParams V) {
     WfpParams& X = V.X;
     const DeviceScene& S = X.W.P.S;
     const int n = seg_scan(V.trSeg);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(X.W.segCap, i);
         float4 o = V.to[q], d = V.td[q], tp = V.tp[q], te = V.te[q], tn = V.tn[q];
         const f3 p1 = mk(tp.x, tp.y, tp.z), e1 = mk(te.x, te.y, te.z), n1 = mk(tn.x, tn.y, tn.z);
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfv_tr(WfvParams V) {
 __global__ __launch_bounds__(256) void k_wfv_resolve(WfvParams V) {
     WfpParams& X = V.X;
     const int n = seg_scan(X.directSeg);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int id = X.directId[seg_pos(X.W.segCap, i)];
         const int fl = X.dFlags[id];
         const float4 a = X.dA[id], bt = X.dBeta[id];
