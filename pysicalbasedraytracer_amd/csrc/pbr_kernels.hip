@@ -776,7 +776,8 @@ struct WfBufs {
     DevBuf wsO2, wsD2, wsC2, wsId2;   // Whitted: second shadow queue (levels alternate)
     DevBuf wRecC, wRecV;              // multi-light Whitted: per-light contributions, visibility
     // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
-    DevBuf wpO, wpD, wpId, wdId, sL, sBeta, rA, rB, rBeta, rLi, rFlags, rLight;
+    DevBuf wqS0[2], wqS1[2];          // Path/VolPath: the path state carried with the ray
+    DevBuf wpO, wpD, wpId, sL, rA, rB, rBeta, rLi, rFlags, rLight, rTgt;
     DevBuf wtO, wtD, wtP, wtE, wtN, wtId, rLiA, rTr, rWA;   // VolPath transmittance walk
 };
 // Chunks alternate between two lanes (own buffers, own stream) so one chunk's launch tails overlap
@@ -859,14 +860,30 @@ int drain(pbr_hip_ctx* ctx) {
     return PBR_OK;
 }
 
+// Every stream of the context idle: the caller's stream, the lane-1 stream and the shadow streams.
+// Used after a schedule fails part-way (a side lane may still write lane buffers, dGuard or dProf)
+// and where profiling state is reset or read — instead of a device-wide synchronisation, which
+// would stall other contexts sharing the GPU.
+void quiesce(pbr_hip_ctx* ctx, hipStream_t s) {
+    if (s) (void)hipStreamSynchronize(s);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    for (int l = 0; l < kWfLanes; ++l)
+        if (ctx->shadowStream[l]) (void)hipStreamSynchronize(ctx->shadowStream[l]);
+    ctx->inFlight = false;
+}
+
 // A frame whose walk reached a safety bound fails instead of returning a truncated image.  Frames
 // that can trip one (scenes with material-less primitives) copy the flag to pinned memory at their
 // end; synchronous renders check it before returning, asynchronous ones at the next call.
+// The caller has made ctx->device current and drained the context (the pinned copy of an
+// asynchronous frame lands only when that frame ends); the reset is ordered on the context's stream.
 int check_guard(pbr_hip_ctx* ctx) {
     const int g = ctx->guardHost ? *(volatile int*)ctx->guardHost : 0;
     if (!g) return PBR_OK;
     *ctx->guardHost = 0;
-    HIP_TRY(hipMemset(ctx->dGuard.p, 0, sizeof(int)));
+    HIP_TRY(hipMemsetAsync(ctx->dGuard.p, 0, sizeof(int), ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     std::string what;
     if (g & kGuardWhittedPassThrough) what += "a Whitted path crossed more than 1024 material-less surfaces; ";
     if (g & kGuardTransmittance) what += "a transmittance walk crossed more than 256 medium interfaces; ";
@@ -1171,6 +1188,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         WfBufs& B = ctx->wb[l];
         WfQueue q;
         q.o = (float4*)B.wqO[k].p; q.d = (float4*)B.wqD[k].p; q.id = (int*)B.wqId[k].p; q.hit = (float4*)B.wqHit[k].p;
+        q.s0 = (float4*)B.wqS0[k].p; q.s1 = (float4*)B.wqS1[k].p;
         q.segCount = cntL[l] + k * kWfBlocks;
         return q;
     };
@@ -1275,13 +1293,15 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         for (int k = 0; k < 2; ++k) {
             HIP_TRY(B.wqO[k].ensure(qcap * 16)); HIP_TRY(B.wqD[k].ensure(qcap * 16));
             HIP_TRY(B.wqId[k].ensure(qcap * 4)); HIP_TRY(B.wqHit[k].ensure(qcap * 16));
+            HIP_TRY(B.wqS0[k].ensure(qcap * 16)); HIP_TRY(B.wqS1[k].ensure(qcap * 16));
         }
         HIP_TRY(B.wsO.ensure(qcap * 16)); HIP_TRY(B.wsD.ensure(qcap * 16)); HIP_TRY(B.wsId.ensure(qcap * 4));
         HIP_TRY(B.wpO.ensure(qcap * 16)); HIP_TRY(B.wpD.ensure(qcap * 16)); HIP_TRY(B.wpId.ensure(qcap * 4));
-        HIP_TRY(B.wdId.ensure(qcap * 4));
-        HIP_TRY(B.sL.ensure(cap * 16)); HIP_TRY(B.sBeta.ensure(cap * 16));
-        HIP_TRY(B.rA.ensure(cap * 16)); HIP_TRY(B.rB.ensure(cap * 16)); HIP_TRY(B.rBeta.ensure(cap * 16));
-        HIP_TRY(B.rLi.ensure(cap * 16)); HIP_TRY(B.rFlags.ensure(cap * 4)); HIP_TRY(B.rLight.ensure(cap * 4));
+        HIP_TRY(B.sL.ensure(cap * 16));
+        // direct records live at the direct queue's positions (segmented, like the ray queues)
+        HIP_TRY(B.rA.ensure(qcap * 16)); HIP_TRY(B.rB.ensure(qcap * 16)); HIP_TRY(B.rBeta.ensure(qcap * 16));
+        HIP_TRY(B.rLi.ensure(qcap * 16)); HIP_TRY(B.rFlags.ensure(qcap * 4)); HIP_TRY(B.rLight.ensure(qcap * 4));
+        HIP_TRY(B.rTgt.ensure(qcap * 4));
         HIP_TRY(B.wIndex.ensure(cap * 4));
         HIP_TRY(B.wCnt.ensure(6 * kWfBlocks * sizeof(int)));
         int* cnt = cntL[l] = (int*)B.wCnt.p;   // segment counts: ray queues 0/1, shadow, probe, direct, Tr walk
@@ -1293,7 +1313,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
             V.anyHitTr = ctx->host.anyNoMaterial ? 0 : 1;
             HIP_TRY(B.wtO.ensure(qcap * 16)); HIP_TRY(B.wtD.ensure(qcap * 16)); HIP_TRY(B.wtP.ensure(qcap * 16));
             HIP_TRY(B.wtE.ensure(qcap * 16)); HIP_TRY(B.wtN.ensure(qcap * 16)); HIP_TRY(B.wtId.ensure(qcap * 4));
-            HIP_TRY(B.rLiA.ensure(cap * 16)); HIP_TRY(B.rTr.ensure(cap * 16)); HIP_TRY(B.rWA.ensure(cap * 4));
+            HIP_TRY(B.rLiA.ensure(qcap * 16)); HIP_TRY(B.rTr.ensure(qcap * 16)); HIP_TRY(B.rWA.ensure(qcap * 4));
             V.to = (float4*)B.wtO.p; V.td = (float4*)B.wtD.p; V.tp = (float4*)B.wtP.p;
             V.te = (float4*)B.wtE.p; V.tn = (float4*)B.wtN.p; V.tid = (int*)B.wtId.p;
             V.trSeg = cnt + 5 * kWfBlocks;
@@ -1309,12 +1329,10 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         W.cap = (int)cap;
         X.po = (float4*)B.wpO.p; X.pd = (float4*)B.wpD.p; X.pid = (int*)B.wpId.p;
         X.probeSeg = cnt + 3 * kWfBlocks;
-        X.directId = (int*)B.wdId.p;
         X.directSeg = cnt + 4 * kWfBlocks;
-        X.stL = (float4*)B.sL.p; X.stBeta = (float4*)B.sBeta.p;
+        X.stL = (float4*)B.sL.p;
         X.dA = (float4*)B.rA.p; X.dB = (float4*)B.rB.p; X.dBeta = (float4*)B.rBeta.p; X.dLi = (float4*)B.rLi.p;
-        X.dFlags = (int*)B.rFlags.p; X.dLight = (int*)B.rLight.p;
-        HIP_TRY(hipMemsetAsync(X.dFlags, 0, cap * 4, s));
+        X.dFlags = (int*)B.rFlags.p; X.dLight = (int*)B.rLight.p; X.dTgt = (int*)B.rTgt.p;
         // Path: 5 camera dims + per bounce 1 + 2 + 2 (light) + 2 (BSDF) + 1 (RR)
         W.P.smp.ldsDims = std::min(kLdsDims, 5 + 8 * std::max(1, P.maxDepth) + 2);
         if (const char* e = getenv("PBR_HALTON_LDS")) if (e[0] == '0') W.P.smp.ldsDims = 0;
@@ -1323,6 +1341,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         WfBufs& B = ctx->wb[l];
         WfQueue q;
         q.o = (float4*)B.wqO[k].p; q.d = (float4*)B.wqD[k].p; q.id = (int*)B.wqId[k].p; q.hit = (float4*)B.wqHit[k].p;
+        q.s0 = (float4*)B.wqS0[k].p; q.s1 = (float4*)B.wqS1[k].p;
         q.segCount = cntL[l] + k * kWfBlocks;
         return q;
     };
@@ -1358,6 +1377,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
             W.next = queue(l, cur ^ 1);
             const int l0 = level == 0 ? 1 : 0;
             const int kShade = vol ? KP_WFV_SHADE : KP_WFP_SHADE;
+            X.lastLevel = level + 1 >= maxLevels && !ctx->host.anyNoMaterial;
             if (vol) {
                 PROF_LAUNCH(KP_WFV_SHADE, st,
                     if (textured) hipLaunchKernelGGL((k_wfv_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, V, l0);
@@ -1432,6 +1452,9 @@ int make_params(pbr_hip_ctx* ctx, const pbr_render_desc* d, KParams* out) {
         while (res < std::max(d->camera.width, d->camera.height)) { res <<= 1; ++m; }
         // pbrt-v3's SobolSampleFloat reads one 52-column matrix per dimension: indices below 2^52
         if (2 * m + 31 - __builtin_clz((unsigned)spp) > kSobolMatrixSize) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol sample index beyond 52 bits");
+        // the device index keeps (px << m) | py and its low 32 bits in 32-bit words, and bits >= 32
+        // come from frame >> (32 - 2m): rasters of 2^16 or more (max(w, h) > 32768) are refused
+        if (m >= 16) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol raster above 32768 pixels per side");
     } else if ((long long)spp * (long long)31104 >= (1ll << 32)) {
         return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
     }
@@ -1513,9 +1536,9 @@ int pbr_hip_li(pbr_hip_ctx* ctx, const pbr_render_desc* d, int n, const float* r
                float* rgb_out) {
     if (!ctx || !d || n < 0 || (n > 0 && (!rays || !q || !rgb_out)) || depth < 0) return PBR_E_INVALID;
     if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
-    if (int rc = check_guard(ctx)) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = drain(ctx)) return rc;
+    if (int rc = check_guard(ctx)) return rc;
     KParams P;
     if (int rc = make_params(ctx, d, &P)) return rc;
     // Whitted recurses while depth + 1 < maxDepth: starting at `depth` is starting at 0 with
@@ -1643,6 +1666,11 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
     if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
     if (ctx->evJoin) (void)hipEventDestroy(ctx->evJoin);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    for (auto& e : ctx->profEv) {
+        if (e.a) (void)hipEventDestroy(e.a);
+        if (e.b) (void)hipEventDestroy(e.b);
+    }
+    ctx->profEv.clear();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->guardHost) (void)hipHostFree(ctx->guardHost);
@@ -1735,9 +1763,15 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (!ctx) return PBR_E_INVALID;
     if (!d) return set_err(ctx, PBR_E_INVALID, "null render desc");
     if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
-    if (int rc = check_guard(ctx)) return rc;   // an earlier asynchronous frame stopped at a bound
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(ctx->device));
+    // An earlier asynchronous frame that stopped at a safety bound fails this call.  Only scenes with
+    // material-less primitives can trip one (and copy the flag out at the end of their frames), so
+    // only those wait for the previous frame here; every other frame stays queued back to back.
+    if (ctx->host.anyNoMaterial) {
+        if (int rc = drain(ctx)) return rc;
+    }
+    if (int rc = check_guard(ctx)) return rc;
     hipStream_t s = d->stream ? (hipStream_t)d->stream : ctx->stream;
     KParams P;
     if (int rc = make_params(ctx, d, &P)) return rc;
@@ -1813,12 +1847,12 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     else if (occ >= 4) hipLaunchKernelGGL((k_render<I, false, 4>), grid, block, 0, s, P);            \
     else if (occ >= 2) hipLaunchKernelGGL((k_render<I, false, 2>), grid, block, 0, s, P);            \
     else hipLaunchKernelGGL((k_render<I, false, 1>), grid, block, 0, s, P);
-        if (wavefront) {
-            int rc = render_wavefront(ctx, P, s);
-            if (rc) return rc;
-        } else if (wavefrontPath) {
-            int rc = render_wavefront_path(ctx, P, s, d->integrator == PBR_INTEGRATOR_VOLPATH);
-            if (rc) return rc;
+        if (wavefront || wavefrontPath) {
+            int rc = wavefront ? render_wavefront(ctx, P, s) : render_wavefront_path(ctx, P, s, d->integrator == PBR_INTEGRATOR_VOLPATH);
+            if (rc) {   // stopped part-way: the forked lane / shadow streams may still run
+                quiesce(ctx, s);
+                return rc;
+            }
         } else {
             PROF_LAUNCH(KP_MEGA, s,
                 switch (d->integrator) {
@@ -1870,7 +1904,7 @@ int pbr_hip_set_profiling(pbr_hip_ctx* ctx, int on) {
     if (!ctx) return PBR_E_INVALID;
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = drain(ctx)) return rc;
-    HIP_TRY(hipDeviceSynchronize());
+    quiesce(ctx, nullptr);
     ctx->profOn = on != 0;
     ctx->profCount = on >= 2;
     ctx->profUsed = 0;
@@ -1878,7 +1912,8 @@ int pbr_hip_set_profiling(pbr_hip_ctx* ctx, int on) {
     if (ctx->profOn) {
         const size_t bytes = (size_t)KP_COUNT * kProfFields * sizeof(unsigned long long);
         HIP_TRY(ctx->dProf.ensure(bytes));
-        HIP_TRY(hipMemset(ctx->dProf.p, 0, bytes));
+        HIP_TRY(hipMemsetAsync(ctx->dProf.p, 0, bytes, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     return PBR_OK;
 }
@@ -1887,7 +1922,7 @@ int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int*
     if (!ctx || !n || (max > 0 && !out)) return PBR_E_INVALID;
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = drain(ctx)) return rc;
-    HIP_TRY(hipDeviceSynchronize());
+    quiesce(ctx, nullptr);
     static const char* kNames[KP_COUNT] = {
         "k_wf_camera_extend", "k_wf_shade", "k_wf_shadow", "k_wf_extend", "k_wf_finish",
         "k_wfp_camera_extend", "k_wfp_shade", "k_wfp_shadow", "k_wfp_probe", "k_wfp_resolve", "k_wfp_finish",
@@ -1915,17 +1950,19 @@ int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int*
         case KP_WF_CAMERA: return 52 * f[0];                                   // o, d, hit, index
         case KP_WF_SHADE: return 72 * f[0] + 4 * f[5] + 52 * f[1] + 52 * f[4]; // ray + index + recA + depth; shadow; next + recF/P
         case KP_WF_SHADOW: return 52 * f[0] + 32 * f[1];                       // o, d, contribution, id; recA RMW
-        case KP_WF_EXTEND: return 52 * f[0];                                   // o, d read; tMax, hit written
+        case KP_WF_EXTEND: return 64 * f[0];                                   // o, d read; o, hit written
         case KP_WF_FINISH: return 16 * f[0] + 4 * f[1] + 16 * c[KP_WF_SHADE][0] + 20 * c[KP_WF_SHADE][4];
-        case KP_WFP_CAMERA: return 84 * f[0];                                  // + L, beta
-        case KP_WFP_SHADE: return 116 * f[0] + 4 * f[5] + 36 * f[1] + 36 * f[2] + 60 * f[3] + 36 * f[4];
+        case KP_WFP_CAMERA: return 52 * f[0];                                  // o, d, hit, index
+        // ray + hit + index (level 0) or id + carried state (queued); stL of the paths that end;
+        // shadow, probe, direct record, continuation with its state
+        case KP_WFP_SHADE: return 52 * f[0] + 32 * f[5] + 16 * (f[0] - f[4]) + 36 * f[1] + 36 * f[2] + 60 * f[3] + 68 * f[4];
         case KP_WFP_SHADOW: return 36 * f[0] + 8 * f[1];
         case KP_WFP_PROBE: return 56 * f[0];
-        case KP_WFP_RESOLVE: return 108 * f[0];
+        case KP_WFP_RESOLVE: return 104 * f[0];                                // record 72 + L RMW 32
         case KP_WFP_FINISH: return 16 * f[0] + 16 * f[1];
-        case KP_WFV_SHADE: return 116 * f[0] + 4 * f[5] + 84 * f[1] + 36 * f[2] + 80 * f[3] + 36 * f[4];
+        case KP_WFV_SHADE: return 52 * f[0] + 36 * f[5] + 16 * (f[0] - f[4]) + 84 * f[1] + 36 * f[2] + 80 * f[3] + 68 * f[4];
         case KP_WFV_TR: return 100 * f[0];
-        case KP_WFV_RESOLVE: return 144 * f[0];
+        case KP_WFV_RESOLVE: return 140 * f[0];
         default: return 16 * f[1];                                             // megakernel: the film output
         }
     };

@@ -41,10 +41,12 @@ __device__ __forceinline__ void prof_count(unsigned long long* ctr, bool pred) {
 }
 
 struct WfQueue {
-    float4* o;      // origin.xyz, tMax
+    float4* o;      // origin.xyz, tMax (the hit distance once a closest-hit kernel has traced the ray)
     float4* d;      // dir.xyz, packed (dim | depth << 16) as int bits
     int* id;        // sample index within the chunk
     float4* hit;    // slot (int bits, -1 = miss), b0, b1, b2
+    float4* s0;     // Path/VolPath state carried with the ray: L.rgb, beta.r
+    float4* s1;     //   beta.g, beta.b, etaScale, the sample's global index (bits)
     int* segCount;  // [kWfBlocks]; null for the dense level-0 queue
 };
 struct WfParams {
@@ -181,7 +183,11 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_extend(WfParams W) {
         HitRec h;
         Counters c;
         bool hit = traverse<false, false, SHORT>(W.P.S, r, &h, &c);
-        W.cur.o[q].w = r.tMax;
+        // the whole 16-B origin record is rewritten with the hit distance: full-line stores.  Measured
+        // (bit-identical; C3 / C5 / C2 frame ms): o.w alone 325 / 1642 / 17.66, the whole record
+        // 321 / 1646 / 17.73, a separate dense t[] array 349 / 1736 / 18.94 (the traversal loop's
+        // register allocation got worse: 13 scratch reloads instead of 9)
+        W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
         W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
     }
 }

@@ -12,26 +12,36 @@
 //   k_wf_extend    closest hit for the continuation queue (shared with Whitted)
 // then k_wfp_finish sums each pixel's per-sample L in sample order and runs the film.
 //
-// L and beta live per sample; every L update happens in the reference's order (emission of
-// bounce k, direct light of bounce k, emission of bounce k+1, ...), so the per-sample radiance is
-// bit-identical to the recursive megakernel's.  Sampler dimensions travel in the ray queue.
+// The path state — L, beta, etaScale and the sample's global index — travels with the ray in the
+// queues (WfQueue s0/s1, compacted with the ray), and the direct-light estimate of bounce k is a
+// record at its own position of the direct queue, which the shadow/probe entries point at: every
+// kernel reads and writes its queue entries densely instead of gathering per-sample state by
+// sample id from a compacted queue (which moved 3.5-8x the algorithmic bytes: partial lines).
+// A path's L leaves the queues once, when the path ends (stL[id], read by the finish).  The
+// estimate's record names where L is at resolve time — the continuation entry the same shade
+// pushed, or stL[id] — and resolve adds the direct term there.  Every L update therefore happens
+// in the reference's order (emission of bounce k, direct light of bounce k, emission of bounce
+// k+1, ...), so the per-sample radiance is bit-identical to the recursive megakernel's.  Sampler
+// dimensions travel in the ray queue.
 #pragma once
 
 constexpr int kWfpAPending = 1, kWfpBPending = 2, kWfpVisible = 4;
 
 struct WfpParams {
-    WfParams W;            // queues (cur/next rays, shadow), chunk geometry, sample index table
-    // probe queue (segmented): origin+tMax, dir, sample id
+    WfParams W;            // queues (cur/next rays with the path state, shadow), chunk geometry, sample index table
+    // probe queue (segmented): origin+tMax, dir, the direct record it fills
     float4* po; float4* pd; int* pid; int* probeSeg;
-    int* directId; int* directSeg;   // samples with a pending direct-light estimate
-    float4* stL;           // L.rgb
-    float4* stBeta;        // beta.rgb, etaScale
+    int* directSeg;        // direct-light records, segmented like the queues (at the shade's push position)
+    float4* stL;           // the finished path's L.rgb, per sample (the finish's input)
     float4* dA;            // light-sample term f·Li·w/lightPdf (if unoccluded), pmf
     float4* dB;            // BSDF-sample f (× |cos|), weight
     float4* dBeta;         // beta at the estimate, scatteringPdf
     float4* dLi;           // probe result: Li at the BSDF-sampled direction
     int* dFlags;           // kWfp* bits
     int* dLight;           // light index of the estimate
+    int* dTgt;             // where the path's L is when the estimate resolves: the continuation's
+                           // position in the next queue, or ~id (stL[id]) when the path ended
+    int lastLevel;         // this shade is the schedule's last: a continuation ends the path instead
 };
 
 __device__ __forceinline__ int pack_path(int dim, int bounces, bool specular) {
@@ -60,9 +70,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_path(st.dim, 0, false)));
     W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
-    W.sampleIndex[q] = st.index;
-    X.stL[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    X.stBeta[q] = make_float4(1.f, 1.f, 1.f, 1.f);
+    W.sampleIndex[q] = st.index;   // the level-0 state (L = 0, beta = 1, etaScale = 1) is implied
 }
 
 // One bounce of PathIntegrator::Li for every queued ray.
@@ -97,6 +105,10 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
         int id = 0, dim = 0, bounces = 0;
         bool specularBounce = false;
         Ray shadow, probe, cont;
+        rgb L, beta, A, fB, betaD;
+        float etaScale = 1.f, pmfD = 0.f, weightB = 1.f, scatPdfD = 0.f;
+        uint32_t sIndex = 0;
+        int dflagsD = 0, lightD = 0;
         if (active) {
             float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
             id = level0 ? q : W.cur.id[q];
@@ -107,9 +119,15 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
             Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
             const int slot = __float_as_int(hr.x);
             const bool found = slot >= 0;
-            float4 lv = X.stL[id], bv = X.stBeta[id];
-            rgb L = sp3(lv.x, lv.y, lv.z), beta = sp3(bv.x, bv.y, bv.z);
-            float etaScale = bv.w;
+            if (level0) {
+                L = sp(0.f); beta = sp(1.f); etaScale = 1.f;
+                sIndex = W.sampleIndex[q];
+            } else {
+                const float4 a = W.cur.s0[q], b = W.cur.s1[q];
+                L = sp3(a.x, a.y, a.z); beta = sp3(a.w, b.x, b.y);
+                etaScale = b.z;
+                sIndex = __float_as_uint(b.w);
+            }
             Isect isect;
             if (found) {
                 int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
@@ -131,7 +149,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                 alive = false;
             } else if (alive) {
                 SState st;
-                st.index = W.sampleIndex[id];
+                st.index = sIndex;
                 st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
                 st.dim = dim;
                 st.px = st.py = 0;
@@ -152,7 +170,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                         float lightPdf = 0, scatteringPdf = 0;
                         VisPt vis;
                         rgb Li = sample_li(S, light, isect, uL0, uL1, &wi, &lightPdf, &vis);
-                        rgb A = sp(0.f);
+                        A = sp(0.f);
                         if (lightPdf > 0 && !black(Li)) {
                             rgb f = bsdf_f<LOBES>(bsdf, wo, wi, flagsNS) * absdot(wi, isect.sn);
                             scatteringPdf = bsdf_pdf<LOBES>(bsdf, wo, wi, flagsNS);
@@ -168,8 +186,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                                 dflags |= kWfpAPending;
                             }
                         }
-                        rgb fB = sp(0.f);
-                        float weightB = 1.f;
+                        fB = sp(0.f);
+                        weightB = 1.f;
                         if (!delta) {
                             int stype = 0;
                             fB = bsdf_sample<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
@@ -192,16 +210,16 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                                 }
                             }
                         }
-                        if (dflags) {
-                            X.dA[id] = make_float4(A.r, A.g, A.b, pmf);
-                            X.dB[id] = make_float4(fB.r, fB.g, fB.b, weightB);
-                            X.dBeta[id] = make_float4(beta.r, beta.g, beta.b, scatteringPdf);
-                            X.dFlags[id] = dflags;
-                            X.dLight[id] = li;
+                        if (dflags) {   // the record is written at its queue position below
+                            pmfD = pmf;
+                            scatPdfD = scatteringPdf;
+                            dflagsD = dflags;
+                            lightD = li;
                             pushDirect = true;
                         }
                     }
                 }
+                betaD = beta;   // beta at the estimate (the direct record's)
                 // BSDF sample for the path (PathIntegrator.cpp:80-105): wo is -ray.d here, not the
                 // normalised isect.wo the light estimate uses
                 const f3 woPath = -ray.d;
@@ -232,29 +250,38 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                     }
                 }
                 dim = st.dim;
-                X.stBeta[id] = make_float4(beta.r, beta.g, beta.b, etaScale);
             }
-            X.stL[id] = make_float4(L.r, L.g, L.b, 0.f);
+            if (X.lastLevel) pushNext = false;   // never taken: no bounce is left at the last level
+            if (!pushNext) X.stL[id] = make_float4(L.r, L.g, L.b, 0.f);   // the path ends here
         }
-        const int si = base + wave_push(&s_push[0], pushShadow);
-        if (pushShadow) {
-            W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
-            W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, 0.f);
-            W.sid[si] = id;
-        }
-        const int pi = base + wave_push(&s_push[1], pushProbe);
-        if (pushProbe) {
-            X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
-            X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
-            X.pid[pi] = id;
-        }
-        const int di = base + wave_push(&s_push[2], pushDirect);
-        if (pushDirect) X.directId[di] = id;
         const int ni = base + wave_push(&s_push[3], pushNext);
         if (pushNext) {
             W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
             W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_path(dim, bounces, specularBounce)));
             W.next.id[ni] = id;
+            W.next.s0[ni] = make_float4(L.r, L.g, L.b, beta.r);
+            W.next.s1[ni] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
+        }
+        const int di = base + wave_push(&s_push[2], pushDirect);
+        if (pushDirect) {
+            X.dA[di] = make_float4(A.r, A.g, A.b, pmfD);
+            X.dB[di] = make_float4(fB.r, fB.g, fB.b, weightB);
+            X.dBeta[di] = make_float4(betaD.r, betaD.g, betaD.b, scatPdfD);
+            X.dFlags[di] = dflagsD;
+            X.dLight[di] = lightD;
+            X.dTgt[di] = pushNext ? ni : ~id;
+        }
+        const int si = base + wave_push(&s_push[0], pushShadow);
+        if (pushShadow) {
+            W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
+            W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, 0.f);
+            W.sid[si] = di;
+        }
+        const int pi = base + wave_push(&s_push[1], pushProbe);
+        if (pushProbe) {
+            X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
+            X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
+            X.pid[pi] = di;
         }
     }
     __syncthreads();
@@ -279,10 +306,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_shadow(WfpParams X) {
         Counters c;
         const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
         if (W.prof) prof_count(W.prof + KP_WFP_SHADOW * kProfFields + 1, visible);
-        if (visible) {
-            const int id = W.sid[q];
-            X.dFlags[id] |= kWfpVisible;   // the only writer of this sample's record in this launch
-        }
+        if (visible) X.dFlags[W.sid[q]] |= kWfpVisible;   // the only writer of this record in this launch
     }
 }
 
@@ -297,8 +321,8 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_probe(WfpParams X) {
         const int q = seg_pos(W.segCap, i);
         float4 o = X.po[q], d = X.pd[q];
         Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
-        const int id = X.pid[q];
-        const int li = X.dLight[id];
+        const int di = X.pid[q];
+        const int li = X.dLight[di];
         HitRec h;
         Counters c;
         rgb Li2 = sp(0.f);
@@ -314,8 +338,16 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_probe(WfpParams X) {
         } else {
             Li2 = light_Le(S, S.lights[li], ray);
         }
-        X.dLi[id] = make_float4(Li2.r, Li2.g, Li2.b, 0.f);
+        X.dLi[di] = make_float4(Li2.r, Li2.g, Li2.b, 0.f);
     }
+}
+
+// the path's L where the estimate resolves: its continuation entry, or stL[id] if the path ended
+__device__ __forceinline__ void add_direct(const WfpParams& X, int tgt, rgb direct) {
+    float4* p = tgt >= 0 ? &X.W.next.s0[tgt] : &X.stL[~tgt];
+    float4 L = *p;
+    L.x = L.x + direct.r; L.y = L.y + direct.g; L.z = L.z + direct.b;
+    *p = L;
 }
 
 // Ld = [A if the light sample is unoccluded] + [f·Li·weight/scatteringPdf if Li is not black];
@@ -324,22 +356,18 @@ __global__ __launch_bounds__(256) void k_wfp_resolve(WfpParams X) {
     WfParams& W = X.W;
     const int n = seg_scan(X.directSeg);
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int id = X.directId[seg_pos(W.segCap, i)];
-        const int fl = X.dFlags[id];
-        const float4 a = X.dA[id], bt = X.dBeta[id];
+        const int di = seg_pos(W.segCap, i);
+        const int fl = X.dFlags[di];
+        const float4 a = X.dA[di], bt = X.dBeta[di];
         rgb Ld = sp(0.f);
         if ((fl & kWfpAPending) && (fl & kWfpVisible)) Ld = Ld + sp3(a.x, a.y, a.z);
         if (fl & kWfpBPending) {
-            const float4 li = X.dLi[id], b = X.dB[id];
+            const float4 li = X.dLi[di], b = X.dB[di];
             const rgb Li2 = sp3(li.x, li.y, li.z);
             if (!black(Li2)) Ld = Ld + sp3(b.x, b.y, b.z) * Li2 * b.w / bt.w;
         }
         const rgb beta = sp3(bt.x, bt.y, bt.z);
-        const rgb direct = beta * (Ld / a.w);
-        float4 L = X.stL[id];
-        L.x = L.x + direct.r; L.y = L.y + direct.g; L.z = L.z + direct.b;
-        X.stL[id] = L;
-        X.dFlags[id] = 0;
+        add_direct(X, X.dTgt[di], beta * (Ld / a.w));
     }
 }
 

@@ -14,8 +14,10 @@ constexpr int kWfvDelta = 8;   // dFlags: the estimate's light is a delta light
 
 struct WfvParams {
     WfpParams X;
-    // transmittance-walk queue (segmented): origin+tMax, dir + medium, target p, pError, n, id
+    // transmittance-walk queue (segmented): origin+tMax, dir + medium, target p, pError, n, the
+    // direct record it fills
     float4* to; float4* td; float4* tp; float4* te; float4* tn; int* tid; int* trSeg;
+    // direct records (at the direct queue position, like WfpParams' d*)
     float4* dLiA;          // light sample Li.rgb, lightPdf
     float4* dTr;           // transmittance to the light sample
     float* dWA;            // MIS weight of the light sample
@@ -70,6 +72,10 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
         bool specularBounce = false;
         Ray shadow, probe, cont;
         VisPt vis;
+        rgb L, beta, fA, fB, Li, betaD;
+        float etaScale = 1.f, pmfD = 0.f, weightA = 0.f, weightB = 1.f, lightPdf = 0.f, scatPdfD = 0.f;
+        uint32_t sIndex = 0;
+        int dflagsD = 0, lightD = 0;
         if (active) {
             float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
             id = level0 ? q : W.cur.id[q];
@@ -81,11 +87,17 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, medium);
             const int slot = __float_as_int(hr.x);
             const bool found = slot >= 0;
-            float4 lv = X.stL[id], bv = X.stBeta[id];
-            rgb L = sp3(lv.x, lv.y, lv.z), beta = sp3(bv.x, bv.y, bv.z);
-            float etaScale = bv.w;
+            if (level0) {
+                L = sp(0.f); beta = sp(1.f); etaScale = 1.f;
+                sIndex = W.sampleIndex[q];
+            } else {
+                const float4 a = W.cur.s0[q], b = W.cur.s1[q];
+                L = sp3(a.x, a.y, a.z); beta = sp3(a.w, b.x, b.y);
+                etaScale = b.z;
+                sIndex = __float_as_uint(b.w);
+            }
             SState st;
-            st.index = W.sampleIndex[id];
+            st.index = sIndex;
             st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
             st.dim = dim;
             st.px = st.py = 0;
@@ -159,9 +171,11 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                     const int flagsNS = BSDF_ALL & ~BSDF_SPECULAR;
                     int dflags = delta ? kWfvDelta : 0;
                     f3 wi = mk(0, 0, 0);
-                    float lightPdf = 0, scatteringPdf = 0, weightA = 0;
-                    rgb Li = sample_li(S, light, ref, uL0, uL1, &wi, &lightPdf, &vis);
-                    rgb fA = sp(0.f);
+                    float scatteringPdf = 0;
+                    lightPdf = 0;
+                    weightA = 0;
+                    Li = sample_li(S, light, ref, uL0, uL1, &wi, &lightPdf, &vis);
+                    fA = sp(0.f);
                     if (lightPdf > 0 && !black(Li)) {
                         if (!mediumEvent) {
                             fA = bsdf_f<LOBES>(bsdf, ref.wo, wi, flagsNS) * absdot(wi, ref.sn);
@@ -177,8 +191,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                             dflags |= kWfpAPending;
                         }
                     }
-                    rgb fB = sp(0.f);
-                    float weightB = 1.f;
+                    fB = sp(0.f);
+                    weightB = 1.f;
                     if (!delta) {
                         bool sampledSpecular = false;
                         if (!mediumEvent) {
@@ -208,14 +222,12 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                             }
                         }
                     }
-                    if (dflags & (kWfpAPending | kWfpBPending)) {
-                        X.dA[id] = make_float4(fA.r, fA.g, fA.b, pmf);
-                        V.dLiA[id] = make_float4(Li.r, Li.g, Li.b, lightPdf);
-                        V.dWA[id] = weightA;
-                        X.dB[id] = make_float4(fB.r, fB.g, fB.b, weightB);
-                        X.dBeta[id] = make_float4(beta.r, beta.g, beta.b, scatteringPdf);
-                        X.dFlags[id] = dflags;
-                        X.dLight[id] = li;
+                    if (dflags & (kWfpAPending | kWfpBPending)) {   // written at its queue position below
+                        pmfD = pmf;
+                        scatPdfD = scatteringPdf;
+                        betaD = beta;
+                        dflagsD = dflags;
+                        lightD = li;
                         pushDirect = true;
                     }
                 }
@@ -263,8 +275,27 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 }
             }
             dim = st.dim;
-            X.stBeta[id] = make_float4(beta.r, beta.g, beta.b, etaScale);
-            X.stL[id] = make_float4(L.r, L.g, L.b, 0.f);
+            if (X.lastLevel) pushNext = false;   // never taken: no bounce is left at the last level
+            if (!pushNext) X.stL[id] = make_float4(L.r, L.g, L.b, 0.f);   // the path ends here
+        }
+        const int ni = base + wave_push(&s_push[3], pushNext);
+        if (pushNext) {
+            W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
+            W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_vol(dim, bounces, specularBounce, cont.medium)));
+            W.next.id[ni] = id;
+            W.next.s0[ni] = make_float4(L.r, L.g, L.b, beta.r);
+            W.next.s1[ni] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
+        }
+        const int di = base + wave_push(&s_push[2], pushDirect);
+        if (pushDirect) {
+            X.dA[di] = make_float4(fA.r, fA.g, fA.b, pmfD);
+            V.dLiA[di] = make_float4(Li.r, Li.g, Li.b, lightPdf);
+            V.dWA[di] = weightA;
+            X.dB[di] = make_float4(fB.r, fB.g, fB.b, weightB);
+            X.dBeta[di] = make_float4(betaD.r, betaD.g, betaD.b, scatPdfD);
+            X.dFlags[di] = dflagsD;
+            X.dLight[di] = lightD;
+            X.dTgt[di] = pushNext ? ni : ~id;
         }
         const int ti = base + wave_push(&s_push[0], pushTr);
         if (pushTr) {
@@ -273,21 +304,13 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             V.tp[ti] = make_float4(vis.p.x, vis.p.y, vis.p.z, 0.f);
             V.te[ti] = make_float4(vis.pError.x, vis.pError.y, vis.pError.z, 0.f);
             V.tn[ti] = make_float4(vis.n.x, vis.n.y, vis.n.z, 0.f);
-            V.tid[ti] = id;
+            V.tid[ti] = di;
         }
         const int pi = base + wave_push(&s_push[1], pushProbe);
         if (pushProbe) {
             X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
             X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
-            X.pid[pi] = id;
-        }
-        const int di = base + wave_push(&s_push[2], pushDirect);
-        if (pushDirect) X.directId[di] = id;
-        const int ni = base + wave_push(&s_push[3], pushNext);
-        if (pushNext) {
-            W.next.o[ni] = make_float4(cont.o.x, cont.o.y, cont.o.z, cont.tMax);
-            W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_vol(dim, bounces, specularBounce, cont.medium)));
-            W.next.id[ni] = id;
+            X.pid[pi] = di;
         }
     }
     __syncthreads();
@@ -348,29 +371,25 @@ __global__ __launch_bounds__(256) void k_wfv_resolve(WfvParams V) {
     WfpParams& X = V.X;
     const int n = seg_scan(X.directSeg);
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int id = X.directId[seg_pos(X.W.segCap, i)];
-        const int fl = X.dFlags[id];
-        const float4 a = X.dA[id], bt = X.dBeta[id];
+        const int di = seg_pos(X.W.segCap, i);
+        const int fl = X.dFlags[di];
+        const float4 a = X.dA[di], bt = X.dBeta[di];
         rgb Ld = sp(0.f);
         if (fl & kWfpAPending) {
-            const float4 la = V.dLiA[id], tr = V.dTr[id];
+            const float4 la = V.dLiA[di], tr = V.dTr[di];
             const rgb Lt = sp3(la.x, la.y, la.z) * sp3(tr.x, tr.y, tr.z);
             if (!black(Lt)) {
                 const rgb fA = sp3(a.x, a.y, a.z);
                 if (fl & kWfvDelta) Ld = Ld + fA * Lt / la.w;
-                else Ld = Ld + fA * Lt * V.dWA[id] / la.w;
+                else Ld = Ld + fA * Lt * V.dWA[di] / la.w;
             }
         }
         if (fl & kWfpBPending) {
-            const float4 li = X.dLi[id], b = X.dB[id];
+            const float4 li = X.dLi[di], b = X.dB[di];
             const rgb Li2 = sp3(li.x, li.y, li.z);
             if (!black(Li2)) Ld = Ld + sp3(b.x, b.y, b.z) * Li2 * b.w / bt.w;
         }
         const rgb beta = sp3(bt.x, bt.y, bt.z);
-        const rgb direct = beta * (Ld / a.w);
-        float4 L = X.stL[id];
-        L.x = L.x + direct.r; L.y = L.y + direct.g; L.z = L.z + direct.b;
-        X.stL[id] = L;
-        X.dFlags[id] = 0;
+        add_direct(X, X.dTgt[di], beta * (Ld / a.w));
     }
 }

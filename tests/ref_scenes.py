@@ -187,6 +187,50 @@ def frame_cases():
     return out
 
 
+def fullsize_pixels(width, height, n=64, seed=0):
+    """n distinct pixels of a width x height raster as one-pixel tiles (x0, y0, x1, y1): the four
+    corners, the centre, one on the area light, a jittered 4x4 grid over the whole frame and a
+    jittered 6x7 grid over the dragon's part of the frame (x 0.38-0.65, y 0.2-0.62 of the raster,
+    where the paths are longest), seeded."""
+    rng = np.random.default_rng(seed)
+    px = [(0, 0), (width - 1, 0), (0, height - 1), (width - 1, height - 1), (width // 2, height // 2),
+          (width // 2, height // 50)]
+
+    def grid(nx, ny, x0, x1, y0, y1):
+        for j in range(ny):
+            for i in range(nx):
+                x = (x0 + (i + rng.uniform(0.1, 0.9)) * (x1 - x0) / nx) * width
+                y = (y0 + (j + rng.uniform(0.1, 0.9)) * (y1 - y0) / ny) * height
+                px.append((min(int(x), width - 1), min(int(y), height - 1)))
+
+    grid(4, 4, 0.0, 1.0, 0.0, 1.0)
+    grid(6, 7, 0.38, 0.65, 0.2, 0.62)
+    out, seen = [], set()
+    for p in px:
+        if p not in seen:
+            seen.add(p)
+            out.append(p)
+    return [(x, y, x + 1, y + 1) for x, y in out[:n]]
+
+
+def fullsize_cases():
+    """name → (scene, render desc with one-pixel tiles): the BASELINE configs at their real size —
+    the 100,352-triangle dragon stand-in, full raster, full spp, full depth — on 64 pixels each.
+    C3 runs on the Halton sampler (the reference has no Sobol sampler, F3); C4 is 3840x2160 at
+    1024 spp.  The raster and spp fix the sample indices, so these are the benchmarked samples."""
+    mesh = scenes.dragon_standin()
+    mesh = (mesh[0], mesh[1], "standin:displaced-uv-sphere-224")
+    out = {}
+    for name, fn, seed in (("c2", scenes.config_c2, 2), ("c3_halton", scenes.config_c3, 3),
+                           ("c4", scenes.config_c4, 4), ("c5", scenes.config_c5, 5)):
+        s, rd = fn(mesh=mesh)
+        cam = rd.camera
+        tiles = fullsize_pixels(cam.width, cam.height, seed=seed)
+        out[name] = (s, scenes.render_desc(cam, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold,
+                                           rd.light_strategy, capi.SAMPLER_HALTON, tiles=tiles))
+    return out
+
+
 def bvh_cases():
     """name → scene for BVHAccel's node array and primitive order."""
     out = {}

@@ -163,3 +163,21 @@ def test_deep_whitted_mirror_box(hip, monkeypatch):
         assert np.array_equal(mk.view(np.uint32), g.view(np.uint32)), depth
     with pytest.raises(RuntimeError):
         hip.render(scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 1, 65))
+
+
+def test_sobol_raster_limit_is_refused(hip):
+    """The device keeps a Sobol sample's (px << m) | py and the low 32 index bits in 32-bit words,
+    with the higher bits from frame >> (32 - 2m): rasters of 2^16 and more per side (m >= 16,
+    max(width, height) > 32768) are refused with PBR_E_UNSUPPORTED instead of silently wrong
+    samples; 32768 is still accepted."""
+    s, _ = scenes.config_c1(8, 8, 1)
+    hip.upload(s)
+    for w, ok in ((40000, False), (32768, True)):
+        cam = scenes.camera(w, 2, (0.0, 0.0, 5.0), (0.0, 0.0, 0.0))
+        rd = scenes.render_desc(cam, capi.INTEGRATOR_PATH, 1, 1, sampler=capi.SAMPLER_SOBOL, tiles=[(0, 0, 4, 2)])
+        if ok:
+            g, _, _ = hip.render(rd)
+            assert np.isfinite(g).all()
+        else:
+            with pytest.raises(RuntimeError, match="32768"):
+                hip.render(rd)

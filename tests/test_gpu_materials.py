@@ -172,6 +172,14 @@ def test_transmittance_walk_bound_fails_loudly(hip, monkeypatch):
     with pytest.raises(RuntimeError, match="transmittance walk"):
         hip.sync()
     hip.sync()   # the failure is reported once
+    # ... or by the next render call, even one enqueued right behind the failing frame: the call
+    # waits for that frame before reading the flag, and blames the frame that tripped it
+    hip.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
+    with pytest.raises(RuntimeError, match="transmittance walk"):
+        hip.render_device(scenes.render_desc(cam, capi.INTEGRATOR_PATH, 2, 3), rgb.data_ptr(), rgba.data_ptr(),
+                          stream=stream.cuda_stream, sync=False)
+    g2, _, _ = hip.render(scenes.render_desc(cam, capi.INTEGRATOR_PATH, 2, 3))   # reported once
+    assert np.array_equal(g2.view(np.uint32), g.view(np.uint32))
     monkeypatch.setenv("PBR_WAVEFRONT", "0")
     with pytest.raises(RuntimeError, match="transmittance walk"):
         hip.render(rd)
