@@ -320,15 +320,24 @@ std::unique_ptr<RefScene> build(const pbr_scene_desc* d) {
 struct RefCamera {
     std::unique_ptr<Camera> cam;
 };
-std::shared_ptr<Camera> make_camera(const pbr_camera_desc& c) {   // CreatePerspectiveCamera (Perspective.cpp:84-104)
-    if (c.fov != 90.f || c.lens_radius != 0.f) throw std::runtime_error("the reference camera is fov 90, pinhole");
+// CreatePerspectiveCamera (Perspective.cpp:84-104) for pinhole cameras; a camera with an aperture
+// (lens_radius > 0) is the reference's PerspectiveCamera constructor (Perspective.cpp:7-9) called
+// with the screen window CreatePerspectiveCamera would pass, the descriptor's lens radius and focal
+// distance, and fov 90.
+std::shared_ptr<Camera> make_camera(const pbr_camera_desc& c) {
+    if (c.fov != 90.f || c.lens_radius < 0.f) throw std::runtime_error("the reference camera is fov 90");
     Transform c2w;
     if (c.use_look_at)
         c2w = Inverse(LookAt(Point3f(c.eye[0], c.eye[1], c.eye[2]), Point3f(c.look[0], c.look[1], c.look[2]),
                              Vector3f(c.up[0], c.up[1], c.up[2])));
     else
         c2w = xf(c.camera_to_world);
-    return std::shared_ptr<Camera>(CreatePerspectiveCamera(c.width, c.height, c2w, nullptr));
+    if (c.lens_radius == 0.f) return std::shared_ptr<Camera>(CreatePerspectiveCamera(c.width, c.height, c2w, nullptr));
+    const float frame = (float)c.width / (float)c.height;
+    Bounds2f screen;
+    if (frame > 1.f) { screen.pMin.x = -frame; screen.pMax.x = frame; screen.pMin.y = -1.f; screen.pMax.y = 1.f; }
+    else { screen.pMin.x = -1.f; screen.pMax.x = 1.f; screen.pMin.y = -1.f / frame; screen.pMax.y = 1.f / frame; }
+    return std::make_shared<PerspectiveCamera>(c.width, c.height, c2w, screen, c.lens_radius, c.focal_distance, 90.0f, nullptr);
 }
 
 std::shared_ptr<SamplerIntegrator> make_integrator(const pbr_render_desc* rd, std::shared_ptr<Camera> cam,
@@ -503,15 +512,15 @@ int ref_intersect(const pbr_scene_desc* sd, int n, const float* rays, float* out
     }
 }
 
-// PerspectiveCamera::GenerateRayDifferential for raster samples (pFilm; pLens (0.5, 0.5), time 0):
-// out = o.xyz, d.xyz.
-int ref_camera_rays(const pbr_camera_desc* cd, int n, const float* pfilm, float* out) {
+// PerspectiveCamera::GenerateRayDifferential for raster samples (pFilm; pLens (0.5, 0.5) or, with
+// plens, the given lens samples; time 0): out = o.xyz, d.xyz.
+int ref_camera_rays_lens(const pbr_camera_desc* cd, int n, const float* pfilm, const float* plens, float* out) {
     try {
         auto cam = make_camera(*cd);
         for (int i = 0; i < n; ++i) {
             CameraSample cs;
             cs.pFilm = Point2f(pfilm[2 * i], pfilm[2 * i + 1]);
-            cs.pLens = Point2f(0.5f, 0.5f);
+            cs.pLens = plens ? Point2f(plens[2 * i], plens[2 * i + 1]) : Point2f(0.5f, 0.5f);
             cs.time = 0.f;
             RayDifferential r;
             cam->GenerateRayDifferential(cs, &r);
@@ -522,6 +531,10 @@ int ref_camera_rays(const pbr_camera_desc* cd, int n, const float* pfilm, float*
     } catch (const std::exception& e) {
         return fail(e);
     }
+}
+
+int ref_camera_rays(const pbr_camera_desc* cd, int n, const float* pfilm, float* out) {
+    return ref_camera_rays_lens(cd, n, pfilm, nullptr, out);
 }
 
 // Shape/plyRead.h:22-47: the reference's ".3d" reader (vertices ×20); pass NULL arrays for counts.

@@ -120,7 +120,29 @@ __device__ __forceinline__ bool sphere_test(const SphereRec& s, const Ray& r, fl
     return true;
 }
 
+// PBR_TRAV_DIAG (diagnostic builds only): traversal loop steps per ray, reduced per wave by the queue
+// kernels into profile fields 6 (lane steps) and 7 (wave steps x 64): their ratio is the SIMD
+// utilisation of the traversal loop.
+#ifndef PBR_TRAV_DIAG
+#define PBR_TRAV_DIAG 0
+#endif
+#if PBR_TRAV_DIAG
+struct HitRec { int slot; float b0, b1, b2; int steps = 0; };
+#else
 struct HitRec { int slot; float b0, b1, b2; };
+#endif
+__device__ __forceinline__ void trav_diag(unsigned long long* prof, int kind, const HitRec& h) {
+#if PBR_TRAV_DIAG
+    if (!prof) return;
+    int sum = h.steps, mxs = h.steps;
+    for (int o = 32; o > 0; o >>= 1) { sum += __shfl_xor(sum, o); mxs = max(mxs, __shfl_xor(mxs, o)); }
+    const unsigned long long act = __ballot(1);
+    if ((int)__lane_id() == __ffsll((long long)act) - 1) {
+        atomicAdd(prof + kind * 8 + 6, (unsigned long long)sum);
+        atomicAdd(prof + kind * 8 + 7, (unsigned long long)mxs * 64ull);
+    }
+#endif
+}
 
 // Triangle::Intersect's SurfaceInteraction (Triangle.cpp:148-246), no shading normals
 // Hit-record and light-sampling helpers are inlined into the kernels: as calls, every live register
@@ -367,6 +389,9 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
     int from = -1;    // BT: re-entering node `cur` from its slot `from` (parent-link walk), else -1
     bool found = false;
     while (true) {
+#if PBR_TRAV_DIAG
+        h->steps++;
+#endif
         if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
             int slot = cur & 0x7fffffff;
             while (true) {
@@ -478,6 +503,9 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
     int cur = S.rootRef, sp = 0;
     bool found = false;
     while (true) {
+#if PBR_TRAV_DIAG
+        h->steps++;
+#endif
         if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
             int slot = cur & 0x7fffffff;
             while (true) {

@@ -1348,7 +1348,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     const dim3 blk(256), gshade(kWfBlocks);
     const dim3 gShadow = resident_grid(ctx, (const void*)k_wfp_shadow<kShortStack>);
     const dim3 gProbe = resident_grid(ctx, (const void*)k_wfp_probe<kShortStack>);
-    const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack>);
+    const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack, true>);
     const dim3 gResolve = resident_grid(ctx, (const void*)k_wfp_resolve);
     // Material-less primitives (medium interfaces) continue a path without a bounce
     // (PathIntegrator.cpp:70-75), one level per crossing.  With such primitives the schedule runs
@@ -1420,7 +1420,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
             }
             cur ^= 1;
             W.cur = queue(l, cur);
-            PROF_LAUNCH(KP_WF_EXTEND, st, hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W));
+            PROF_LAUNCH(KP_WF_EXTEND, st, hipLaunchKernelGGL((k_wf_extend<kShortStack, true>), gExtend, blk, 0, st, W));
             if (int rc = prof_sums(ctx, st, KP_WF_EXTEND, {W.cur.segCount})) return rc;
         }
         const int pb = finish_pixels(spp);

@@ -145,6 +145,182 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
     return lo * segCap + (q - s_seg_off[lo]);
 }
 
+// Queue traversal with lane refill (Aila & Laine's "replace terminated rays").  Incoherent rays
+// (Path/VolPath continuations, shadow and probe rays) need very different numbers of traversal steps,
+// and a wave that traces 64 of them at a time runs until its slowest lane is done: measured SIMD
+// utilisation of the traversal loop 0.27 (C3 continuations, 9.25 steps per ray), 0.29 (C3 shadow),
+// 0.33 (probe), against 0.96 for the coherent camera rays (tools/trav_diag.py).  Here every lane of a
+// wave keeps its own ray state, the loop runs one traversal step (a quad node, or a leaf and the pops
+// after it) per iteration, and once at least PBR_REFILL lanes are idle they take the wave's next rays.
+// The wave's rays are those the grid-stride loop would give it (batches of 64 consecutive queue
+// entries, `stride` apart), so the load balance over waves is unchanged.  Each ray's traversal — node
+// order, primitive order, ray.tMax updates — is exactly traverse_quad's, so results are identical.
+#ifndef PBR_REFILL
+#define PBR_REFILL 16
+#endif
+// Workgroups per CU the lane-refill traversal kernels are compiled for.  Keeping 64 lanes busy
+// needs more registers per lane (at 7 the closest-hit loop spilled 19 VGPRs).  Measured (C3 / C5
+// ms per frame of the family, bit-identical): closest hit (extend) 7: 175 / 610, 6: 163 / 587,
+// 5: 155 / 584; any hit (shadow) 7: 107, 6: 126, 5: 122; transmittance (C5) 7: 546, 6: 518, 5: 582.
+#ifndef PBR_REFILL_OCC
+#define PBR_REFILL_OCC 5
+#endif
+#ifndef PBR_REFILL_OCC_ANY
+#define PBR_REFILL_OCC_ANY 7
+#endif
+#ifndef PBR_REFILL_OCC_TR
+#define PBR_REFILL_OCC_TR 6
+#endif
+constexpr int kRefill = PBR_REFILL;
+// LDS entries of the closest-hit refill kernels' short stack (their 5 workgroups per CU leave LDS
+// room for more than the 6 of the other traversal kernels).  C3 / C5 frame ms: 6 entries 276.6 /
+// 1416, 10: 271.6 / 1386, 14 (4 workgroups per CU fit): 285.5 / 1403.
+#ifndef PBR_REFILL_SHORT
+#define PBR_REFILL_SHORT 10
+#endif
+constexpr int kRefillShort = PBR_REFILL_SHORT;
+__shared__ int s_trav_ref_r[kRefillShort * 256];
+__shared__ float s_trav_t_r[kRefillShort * 256];
+// load(i, &key) → the i-th ray of the queue (key: what store needs, e.g. its queue position);
+// store(key, hit, ray, h) → the ray's result (closest hit: ray.tMax and h; any hit: hit only).
+template <bool ANY, int SHORT, class Load, class Store>
+__device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store store, unsigned long long* diag = nullptr,
+                                int diagKind = 0) {
+    const int lane = (int)__lane_id();
+    const int stride = (int)(gridDim.x * blockDim.x);
+    const int wbase = wf_block() * (int)blockDim.x + ((int)threadIdx.x & ~63);
+    auto rayOf = [&](int j) { return (j >> 6) * stride + wbase + (j & 63); };   // increasing in j
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int* lref;
+    float* lt;
+    if constexpr (SHORT == kShortStack) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
+    else { static_assert(SHORT == kRefillShort, "short stack depth"); lref = s_trav_ref_r + threadIdx.x; lt = s_trav_t_r + threadIdx.x; }
+    constexpr int PRIV = 64 - SHORT;
+    int stackRef[PRIV];
+    float stackT[PRIV];
+    int cursor = 0;              // wave-uniform: the next ray of the wave's sequence
+    bool have = false;           // the lane holds a ray in flight
+    int key = 0, cur = 0, sp = 0;
+    bool found = false;
+    Ray r;
+    f3 inv = mk(0, 0, 0);
+    bool n0 = false, n1 = false, n2 = false;
+    HitRec h;
+    h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
+    unsigned long long laneSteps = 0, waveSteps = 0;
+    (void)laneSteps; (void)waveSteps;
+    while (true) {
+        const unsigned long long idle = __ballot(!have);
+        const int nIdle = __popcll(idle);
+        if (nIdle >= (kRefill > 0 ? kRefill : 64) && rayOf(cursor) < n) {   // wave-uniform
+            if (!have) {
+                const int i = rayOf(cursor + __popcll(idle & below));
+                if (i < n) {
+                    r = load(i, &key);
+                    found = false;
+                    h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
+                    // traverse(): the root is visited first (the binary root box)
+                    bool ok = S.nNodes > 0;
+                    if (ok) {
+                        inv = ANY ? mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z) : mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
+                        n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
+                        ok = node_hit(S.nodes[0], S.nodes[1], r, inv, n0, n1, n2);
+                    }
+                    if (ok) {
+                        cur = S.quadRootRef;
+                        sp = 0;
+                        have = true;
+                    } else {
+                        store(key, false, r, h);
+                    }
+                }
+            }
+            cursor += nIdle;
+        }
+        if (__ballot(have) == 0ull) {
+            if (rayOf(cursor) >= n) break;
+            continue;
+        }
+        if constexpr (PBR_TRAV_DIAG) { waveSteps += 64; laneSteps += have ? 1 : 0; }
+        if (!have) continue;
+        bool done = false;
+        bool descend = false;
+        if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
+            int slot = cur & 0x7fffffff;
+            while (true) {
+                float4 v0, v1, v2;
+                const int uslot = __builtin_amdgcn_readfirstlane(slot);
+                if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {
+                    const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
+                    v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
+                } else {
+                    const float4* tv = S.triVerts + 3 * (size_t)slot;
+                    v0 = tv[0]; v1 = tv[1]; v2 = tv[2];
+                }
+                const int flags = __float_as_int(v0.w);
+                float t, b0 = 0, b1 = 0, b2 = 0;
+                const bool hit = (flags & PRIM_SPHERE)
+                                     ? sphere_test(S.spheres[__float_as_int(v0.x)], r, &t)
+                                     : tri_test(mk(v0.x, v0.y, v0.z), mk(v1.x, v1.y, v1.z), mk(v2.x, v2.y, v2.z), r, &t, &b0, &b1, &b2);
+                if (hit) {
+                    found = true;
+                    if (ANY) { done = true; break; }
+                    r.tMax = t;   // GeometricPrimitive::Intersect (Primitive.cpp:26)
+                    h.slot = slot; h.b0 = b0; h.b1 = b1; h.b2 = b2;
+                }
+                if (flags & PRIM_LEAF_END) break;
+                ++slot;
+            }
+        } else {
+            QuadSlots q;
+            quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
+            const float tM = r.tMax;
+            const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
+                       p3 = q.k[3] && q.t[3] < tM;
+            if ((p0 | p1 | p2 | p3) && sp <= 64 - 3) {
+                const int first = p0 ? 0 : (p1 ? 1 : (p2 ? 2 : 3));
+                auto push = [&](int ref, float t) {
+                    if (SHORT && sp < SHORT) { lref[sp * 256] = ref; if (!ANY) lt[sp * 256] = t; }
+                    else { stackRef[sp - SHORT] = ref; if (!ANY) stackT[sp - SHORT] = t; }
+                    ++sp;
+                };
+                if (p3 && first < 3) push(q.ref[3], q.t[3]);
+                if (p2 && first < 2) push(q.ref[2], q.t[2]);
+                if (p1 && first < 1) push(q.ref[1], q.t[1]);
+                cur = first == 0 ? q.ref[0] : (first == 1 ? q.ref[1] : (first == 2 ? q.ref[2] : q.ref[3]));
+                descend = true;
+            }
+        }
+        if (!done && !descend) {   // pop until an entry passes its box test against the current tMax
+            bool more = false;
+            while (sp > 0) {
+                --sp;
+                if (ANY) { cur = (SHORT && sp < SHORT) ? lref[sp * 256] : stackRef[sp - SHORT]; more = true; break; }
+                int rr;
+                float tt;
+                if (SHORT && sp < SHORT) { rr = lref[sp * 256]; tt = lt[sp * 256]; }
+                else { rr = stackRef[sp - SHORT]; tt = stackT[sp - SHORT]; }
+                if (tt < r.tMax) { cur = rr; more = true; break; }
+            }
+            done = !more;
+        }
+        if (done) {
+            store(key, found, r, h);
+            have = false;
+        }
+    }
+#if PBR_TRAV_DIAG
+    if (diag) {
+        unsigned long long sum = laneSteps;
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        if (lane == 0) {
+            atomicAdd(diag + diagKind * 8 + 6, sum);
+            atomicAdd(diag + diagKind * 8 + 7, waveSteps);
+        }
+    }
+#endif
+}
+
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams W) {
     const KParams& P = W.P;
@@ -163,6 +339,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams
     HitRec h;
     Counters c;
     bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
+    trav_diag(W.prof, KP_WF_CAMERA, h);
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(st.dim, 0)));
     W.sampleIndex[q] = st.index;   // the level-0 queue is dense: queue slot == sample id
@@ -173,9 +350,28 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams
     W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
 }
 
-template <int SHORT>
-__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_extend(WfParams W) {
+// REFILL: the lane-refill traversal (Path/VolPath continuations: C3 204 → 179 ms/frame of extend,
+// C5 760 → 617).  Whitted's mirror continuations are coherent (SIMD utilisation 0.90 without
+// refill) and keep the plain loop: with refill C2's extend took 5.4 → 8.6 ms.
+template <int SHORT, bool REFILL = false>
+__global__ __launch_bounds__(256, REFILL ? PBR_REFILL_OCC : PBR_TRAV_OCC) void k_wf_extend(WfParams W) {
     const int n = seg_scan(W.cur.segCount);
+    if constexpr (REFILL && kRefill > 0 && SHORT > 0 && kQuadTraversal) {
+        traverse_stream<false, kRefillShort>(
+            W.P.S, n,
+            [&](int i, int* key) {
+                const int q = seg_pos(W.segCap, i);
+                *key = q;
+                const float4 o = W.cur.o[q], d = W.cur.d[q];
+                return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+            },
+            [&](int q, bool hit, const Ray& r, const HitRec& h) {
+                W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
+                W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
+            },
+            W.prof, KP_WF_EXTEND);
+        return;
+    }
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
         float4 o = W.cur.o[q], d = W.cur.d[q];
@@ -183,6 +379,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_extend(WfParams W) {
         HitRec h;
         Counters c;
         bool hit = traverse<false, false, SHORT>(W.P.S, r, &h, &c);
+        trav_diag(W.prof, KP_WF_EXTEND, h);
         // the whole 16-B origin record is rewritten with the hit distance: full-line stores.  Measured
         // (bit-identical; C3 / C5 / C2 frame ms): o.w alone 325 / 1642 / 17.66, the whole record
         // 321 / 1646 / 17.73, a separate dense t[] array 349 / 1736 / 18.94 (the traversal loop's
@@ -355,6 +552,31 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
+    // Whitted's shadow rays keep the plain loop: lane refill measured 5.45 → 5.90 ms/frame on C2
+    // (refill 16), 5.40 (refill 32)
+    if constexpr (false && kRefill > 0 && SHORT > 0 && kQuadTraversal) {
+        traverse_stream<true, SHORT>(
+            W.P.S, n,
+            [&](int i, int* key) {
+                const int q = seg_pos(W.shadowSegCap, i);
+                *key = q;
+                const float4 o = W.so[q], d = W.sd[q];
+                return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+            },
+            [&](int q, bool hit, const Ray&, const HitRec&) {
+                if (W.prof) atomicAdd(W.prof + KP_WF_SHADOW * kProfFields + 1, (unsigned long long)(hit ? 0 : 1));
+                if (!hit) {
+                    const int id = W.sid[q];
+                    const float4 cc = W.sc[q];
+                    const size_t ri = (size_t)__float_as_int(W.sd[q].w) * W.cap + id;
+                    float4 A = W.recA[ri];
+                    A.x = A.x + cc.x; A.y = A.y + cc.y; A.z = A.z + cc.z;
+                    W.recA[ri] = A;
+                }
+            },
+            W.prof, KP_WF_SHADOW);
+        return;
+    }
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.shadowSegCap, i);
         float4 o = W.so[q], d = W.sd[q];
@@ -362,6 +584,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
         HitRec h;
         Counters c;
         const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
+        trav_diag(W.prof, KP_WF_SHADOW, h);
         if (W.prof) prof_count(W.prof + KP_WF_SHADOW * kProfFields + 1, visible);
         if (visible) {
             int id = W.sid[q];
@@ -532,6 +755,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow_ml(WfParams W) 
         HitRec h;
         Counters c;
         const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
+        trav_diag(W.prof, KP_WF_SHADOW, h);
         if (W.prof) prof_count(W.prof + KP_WF_SHADOW * kProfFields + 1, visible);
         if (visible) {
             const int code = __float_as_int(d.w);

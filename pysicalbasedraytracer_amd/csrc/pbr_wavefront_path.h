@@ -67,6 +67,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
     HitRec h;
     Counters c;
     bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
+    trav_diag(W.prof, KP_WFP_CAMERA, h);
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_path(st.dim, 0, false)));
     W.cur.hit[q] = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
@@ -295,9 +296,25 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
 
 // VisibilityTester::Unoccluded for the light-sample rays
 template <int SHORT>
-__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_shadow(WfpParams X) {
+__global__ __launch_bounds__(256, PBR_REFILL_OCC_ANY) void k_wfp_shadow(WfpParams X) {
     WfParams& W = X.W;
     const int n = seg_scan(W.shadowSeg);
+    if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
+        traverse_stream<true, SHORT>(
+            W.P.S, n,
+            [&](int i, int* key) {
+                const int q = seg_pos(W.segCap, i);
+                *key = q;
+                const float4 o = W.so[q], d = W.sd[q];
+                return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+            },
+            [&](int q, bool hit, const Ray&, const HitRec&) {
+                if (W.prof) atomicAdd(W.prof + KP_WFP_SHADOW * kProfFields + 1, (unsigned long long)(hit ? 0 : 1));
+                if (!hit) X.dFlags[W.sid[q]] |= kWfpVisible;   // the only writer of this record in this launch
+            },
+            W.prof, KP_WFP_SHADOW);
+        return;
+    }
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
         float4 o = W.so[q], d = W.sd[q];
@@ -305,6 +322,7 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_shadow(WfpParams X) {
         HitRec h;
         Counters c;
         const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
+        trav_diag(W.prof, KP_WFP_SHADOW, h);
         if (W.prof) prof_count(W.prof + KP_WFP_SHADOW * kProfFields + 1, visible);
         if (visible) X.dFlags[W.sid[q]] |= kWfpVisible;   // the only writer of this record in this launch
     }
@@ -313,10 +331,40 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_shadow(WfpParams X) {
 // EstimateDirect's BSDF-sampled ray: closest hit; Li = the sampled light's emission if that is
 // what it hits (si.Le), light.Le(ray) if it escapes (Light::Le, F4 for non-infinite lights).
 template <int SHORT>
-__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_probe(WfpParams X) {
+__global__ __launch_bounds__(256, PBR_REFILL_OCC) void k_wfp_probe(WfpParams X) {
     WfParams& W = X.W;
     const DeviceScene& S = W.P.S;
     const int n = seg_scan(X.probeSeg);
+    if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
+        traverse_stream<false, kRefillShort>(
+            S, n,
+            [&](int i, int* key) {
+                const int q = seg_pos(W.segCap, i);
+                *key = q;
+                const float4 o = X.po[q], d = X.pd[q];
+                return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+            },
+            [&](int q, bool hit, const Ray& ray, const HitRec& h) {
+                const int di = X.pid[q];
+                const int li = X.dLight[di];
+                rgb Li2 = sp(0.f);
+                if (hit) {
+                    if (S.primInfo[h.slot].z == li) {
+                        Isect lightIsect;
+                        int flags = __float_as_int(S.triVerts[3 * (size_t)h.slot].w);
+                        if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)h.slot].x)], ray, ray.tMax, &lightIsect);
+                        else triangle_si(S, h.slot, ray, h.b0, h.b1, h.b2, flags, &lightIsect);
+                        lightIsect.slot = h.slot;
+                        Li2 = si_Le(S, lightIsect, -ray.d);
+                    }
+                } else {
+                    Li2 = light_Le(S, S.lights[li], ray);
+                }
+                X.dLi[di] = make_float4(Li2.r, Li2.g, Li2.b, 0.f);
+            },
+            W.prof, KP_WFP_PROBE);
+        return;
+    }
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
         float4 o = X.po[q], d = X.pd[q];
@@ -326,7 +374,9 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_probe(WfpParams X) {
         HitRec h;
         Counters c;
         rgb Li2 = sp(0.f);
-        if (traverse<false, false, SHORT>(S, ray, &h, &c)) {
+        const bool hitP = traverse<false, false, SHORT>(S, ray, &h, &c);
+        trav_diag(W.prof, KP_WFP_PROBE, h);
+        if (hitP) {
             if (S.primInfo[h.slot].z == li) {
                 Isect lightIsect;
                 int flags = __float_as_int(S.triVerts[3 * (size_t)h.slot].w);

@@ -324,10 +324,30 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
 
 // VisibilityTester::Tr (Light.cpp:31-47): walk to the light sample through medium interfaces
 template <int SHORT>
-__global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfv_tr(WfvParams V) {
+__global__ __launch_bounds__(256, PBR_REFILL_OCC_TR) void k_wfv_tr(WfvParams V) {
     WfpParams& X = V.X;
     const DeviceScene& S = X.W.P.S;
     const int n = seg_scan(V.trSeg);
+    if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
+        if (V.anyHitTr) {   // the walk is one any-hit query (below): lane-refill traversal
+            traverse_stream<true, SHORT>(
+                S, n,
+                [&](int i, int* key) {
+                    const int q = seg_pos(X.W.segCap, i);
+                    *key = q;
+                    const float4 o = V.to[q], d = V.td[q];
+                    return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, __float_as_int(d.w));
+                },
+                [&](int q, bool hit, const Ray& ray, const HitRec&) {
+                    rgb Tr = sp(1.f);
+                    if (hit) Tr = sp(0.0f);
+                    else if (ray.medium >= 0) Tr = Tr * medium_tr(S, ray.medium, ray);
+                    V.dTr[V.tid[q]] = make_float4(Tr.r, Tr.g, Tr.b, 0.f);
+                },
+                X.W.prof, KP_WFV_TR);
+            return;
+        }
+    }
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(X.W.segCap, i);
         float4 o = V.to[q], d = V.td[q], tp = V.tp[q], te = V.te[q], tn = V.tn[q];

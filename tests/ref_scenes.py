@@ -174,6 +174,17 @@ def render_cases():
     s.mesh(Pb, Ib, s.mirror((0.9, 0.95, 0.9)))
     s.point_light((0.3, 1.2, 1.5), (8.0, 8.0, 8.0))
     out["whitted_facing_mirrors_d12"] = (s, scenes.render_desc(scenes.camera(32, 20, **CAM_C), capi.INTEGRATOR_WHITTED, 4, 12))
+
+    # thin-lens cameras (Perspective.cpp:28-32,49-62): PerspectiveCamera with an aperture, pLens from
+    # the sampler's dimensions 3-4 through ConcentricSampleDisk, focused behind / in front of the dragon
+    for integ, name, spp, (lr, fd) in ((capi.INTEGRATOR_WHITTED, "whitted", 8, (0.08, 2.7)),
+                                       (capi.INTEGRATOR_PATH, "path", 8, (0.15, 1.6))):
+        s, rd = scenes.config_c2(40, 24, spp, mesh=m, sky=scenes.procedural_sky(64, 32)) if integ == capi.INTEGRATOR_WHITTED \
+            else scenes.config_c3(40, 24, spp, mesh=m)
+        cam = rd.camera
+        cam.lens_radius, cam.focal_distance = lr, fd
+        out[f"{name}_thin_lens"] = (s, scenes.render_desc(cam, integ, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                                                          capi.SAMPLER_HALTON))
     return out
 
 
