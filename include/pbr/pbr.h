@@ -560,30 +560,92 @@ class PerspectiveCamera : public Camera {   // Camera/Perspective.h
 PerspectiveCamera* CreatePerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& cam2world, Medium* media);
 
 // ---------------------------------------------------------------------------- Sampler/
-// GlobalSampler state (Sampler/Sampler.h:60-105): current pixel, sample number and the next
-// dimension; the values come from the device (pbr_hip_sampler_values).
+// Sampler (Sampler/Sampler.h:13-43) with the reference's interface — Get1D/Get2D/Clone pure
+// virtual, GetCameraSample from them (Sampler.cpp:10-21), the 1D/2D sample arrays — and
+// GlobalSampler's dimension bookkeeping (Sampler.h:62-82, Sampler.cpp:97-143).  The values come
+// from the device (pbr_hip_sampler_values), one query per block of kValueBlock dimensions of the
+// current sample, so the reference's per-pixel loop (Integrator.cpp:290-313) runs unchanged.
 class Sampler {
   public:
     explicit Sampler(int64_t samplesPerPixel) : samplesPerPixel(samplesPerPixel) {}
     virtual ~Sampler() = default;
-    virtual void StartPixel(const Point2i& p) { currentPixel = p; currentPixelSampleIndex = 0; dimension = 0; }
-    virtual bool StartNextSample() { dimension = 0; return ++currentPixelSampleIndex < samplesPerPixel; }
-    virtual bool SetSampleNumber(int64_t sampleNum) { dimension = 0; currentPixelSampleIndex = sampleNum; return sampleNum < samplesPerPixel; }
+    virtual void StartPixel(const Point2i& p);
+    virtual float Get1D() = 0;
+    virtual Point2f Get2D() = 0;
+    CameraSample GetCameraSample(const Point2i& pRaster);   // pFilm = pRaster + Get2D(), time = Get1D(), pLens = Get2D()
+    void Request1DArray(int n);
+    void Request2DArray(int n);
+    virtual int RoundCount(int n) const { return n; }
+    const float* Get1DArray(int n);
+    const Point2f* Get2DArray(int n);
+    virtual bool StartNextSample();
+    virtual std::unique_ptr<Sampler> Clone(int seed) = 0;
+    virtual bool SetSampleNumber(int64_t sampleNum);
     int64_t CurrentSampleNumber() const { return currentPixelSampleIndex; }
-    // Sampler.cpp:10-21: pFilm = pRaster + Get2D(), time = Get1D(), pLens = Get2D()
-    virtual CameraSample GetCameraSample(const Point2i& pRaster) = 0;
     const int64_t samplesPerPixel;
+    // Extensions: where the sampler stands — SamplerIntegrator::Li continues the sample on the
+    // device from (pixel, sample number, next dimension) — and which device sampler it is.
+    const Point2i& CurrentPixel() const { return currentPixel; }
+    virtual int CurrentDimension() const = 0;
+    virtual int DeviceSampler() const = 0;         // PBR_SAMPLER_HALTON / PBR_SAMPLER_SOBOL
+    virtual Point2i SampleRaster() const = 0;      // the raster the sample indices are defined on
+
+  protected:
     Point2i currentPixel;
     int64_t currentPixelSampleIndex = 0;
-    int dimension = 0;   // the next dimension a Get1D/Get2D would read
+    std::vector<int> samples1DArraySizes, samples2DArraySizes;
+    std::vector<std::vector<float>> sampleArray1D;
+    std::vector<std::vector<Point2f>> sampleArray2D;
+
+  private:
+    size_t array1DOffset = 0, array2DOffset = 0;
 };
-class HaltonSampler : public Sampler {   // Sampler/Halton.h
+class GlobalSampler : public Sampler {
+  public:
+    explicit GlobalSampler(int64_t samplesPerPixel) : Sampler(samplesPerPixel) {}
+    bool StartNextSample() override;
+    void StartPixel(const Point2i& p) override;
+    bool SetSampleNumber(int64_t sampleNum) override;
+    float Get1D() override;
+    Point2f Get2D() override;
+    int CurrentDimension() const override { return dimension; }
+    // The value of dimension `dim` for sample `sampleNum` of the current pixel —
+    // SampleDimension(GetIndexForSample(sampleNum), dim) — and a batch of them, on the device.
+    float SampleValue(int64_t sampleNum, int dim) const;
+    void SampleValues(const std::vector<int64_t>& sampleNums, const std::vector<int>& dims, float* out) const;
+    virtual int MaxDimensions() const = 0;
+    static constexpr int kValueBlock = 32;
+
+  private:
+    float value(int dim);
+    int dimension = 0;
+    static const int arrayStartDim = 5;
+    int arrayEndDim = 5;
+    int cacheBase = -1;                 // first dimension held in cache (-1: nothing cached)
+    float cache[kValueBlock];
+};
+class HaltonSampler : public GlobalSampler {   // Sampler/Halton.h
   public:
     HaltonSampler(int nsamp, const Bounds2i& sampleBounds, bool sampleAtCenter = false);
-    CameraSample GetCameraSample(const Point2i& pRaster) override;
+    std::unique_ptr<Sampler> Clone(int seed) override;   // Halton.cpp: a copy (the sequence has no seed)
+    int DeviceSampler() const override;
+    Point2i SampleRaster() const override;
+    int MaxDimensions() const override { return 1000; }   // PrimeTableSize
     const Bounds2i sampleBounds;
 };
 HaltonSampler* CreateHaltonSampler(const Bounds2i& sampleBounds);   // 16 spp, as Halton.cpp:98-104
+// pbrt-v3's SobolSampler (sobol.h/.cpp) over the reference's SobolMatrices32
+// (Sampler/SobolMatrices.cpp:69; F3 — the reference ships the tables, not the sampler): spp rounded
+// up to a power of two, resolution RoundUpPow2(max(width, height)) of the sample bounds.
+class SobolSampler : public GlobalSampler {
+  public:
+    SobolSampler(int64_t samplesPerPixel, const Bounds2i& sampleBounds);
+    std::unique_ptr<Sampler> Clone(int seed) override;
+    int DeviceSampler() const override;
+    Point2i SampleRaster() const override;
+    int MaxDimensions() const override { return 1024; }   // NumSobolDimensions
+    const Bounds2i sampleBounds;
+};
 
 // ---------------------------------------------------------------------------- Integrator/
 struct RenderStats {   // what the last Render measured (pbr_render_stats)
@@ -634,6 +696,8 @@ class SamplerIntegrator : public Integrator {
 
   private:
     void ensure_scene(const Scene& scene) const;   // context + upload (once per Scene)
+    std::vector<Spectrum> LiWith(const Sampler& s, const std::vector<Ray>& rays, const std::vector<Point2i>& pixels,
+                                 const std::vector<int64_t>& samples, int dimension, const Scene& scene, int depth) const;
     std::shared_ptr<Sampler> sampler;
     const Bounds2i pixelBounds;
     FrameBuffer* m_FrameBuffer;

@@ -541,10 +541,148 @@ PerspectiveCamera* CreatePerspectiveCamera(int RasterWidth, int RasterHeight, co
 }
 
 HaltonSampler::HaltonSampler(int nsamp, const Bounds2i& sampleBounds, bool sampleAtCenter)
-    : Sampler(nsamp), sampleBounds(sampleBounds) {
+    : GlobalSampler(nsamp), sampleBounds(sampleBounds) {
     if (sampleAtCenter) throw std::invalid_argument("HaltonSampler: sampleAtCenter is not on the GPU path");
 }
 HaltonSampler* CreateHaltonSampler(const Bounds2i& sampleBounds) { return new HaltonSampler(16, sampleBounds, false); }
+std::unique_ptr<Sampler> HaltonSampler::Clone(int) { return std::unique_ptr<Sampler>(new HaltonSampler(*this)); }
+int HaltonSampler::DeviceSampler() const { return PBR_SAMPLER_HALTON; }
+Point2i HaltonSampler::SampleRaster() const {
+    return Point2i(sampleBounds.pMax.x - sampleBounds.pMin.x, sampleBounds.pMax.y - sampleBounds.pMin.y);
+}
+namespace {
+void check(pbr_hip_ctx* ctx, int rc, const char* what);
+pbr_hip_ctx* helper_ctx();
+int64_t round_up_pow2(int64_t v) {
+    int64_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+}  // namespace
+SobolSampler::SobolSampler(int64_t samplesPerPixel, const Bounds2i& sampleBounds)
+    : GlobalSampler(round_up_pow2(samplesPerPixel)), sampleBounds(sampleBounds) {
+    if (samplesPerPixel <= 0) throw std::invalid_argument("SobolSampler: samplesPerPixel must be positive");
+}
+std::unique_ptr<Sampler> SobolSampler::Clone(int) { return std::unique_ptr<Sampler>(new SobolSampler(*this)); }
+int SobolSampler::DeviceSampler() const { return PBR_SAMPLER_SOBOL; }
+Point2i SobolSampler::SampleRaster() const {
+    return Point2i(sampleBounds.pMax.x - sampleBounds.pMin.x, sampleBounds.pMax.y - sampleBounds.pMin.y);
+}
+
+// ---- Sampler (Sampler/Sampler.cpp:7-67)
+void Sampler::StartPixel(const Point2i& p) {
+    currentPixel = p;
+    currentPixelSampleIndex = 0;
+    array1DOffset = array2DOffset = 0;
+}
+CameraSample Sampler::GetCameraSample(const Point2i& pRaster) {
+    CameraSample cs;
+    const Point2f u = Get2D();
+    cs.pFilm = Point2f((float)pRaster.x + u.x, (float)pRaster.y + u.y);
+    cs.time = Get1D();
+    cs.pLens = Get2D();
+    return cs;
+}
+bool Sampler::StartNextSample() {
+    array1DOffset = array2DOffset = 0;
+    return ++currentPixelSampleIndex < samplesPerPixel;
+}
+bool Sampler::SetSampleNumber(int64_t sampleNum) {
+    array1DOffset = array2DOffset = 0;
+    currentPixelSampleIndex = sampleNum;
+    return currentPixelSampleIndex < samplesPerPixel;
+}
+void Sampler::Request1DArray(int n) {
+    samples1DArraySizes.push_back(n);
+    sampleArray1D.push_back(std::vector<float>((size_t)n * samplesPerPixel));
+}
+void Sampler::Request2DArray(int n) {
+    samples2DArraySizes.push_back(n);
+    sampleArray2D.push_back(std::vector<Point2f>((size_t)n * samplesPerPixel));
+}
+const float* Sampler::Get1DArray(int n) {
+    if (array1DOffset == sampleArray1D.size()) return nullptr;
+    return &sampleArray1D[array1DOffset++][currentPixelSampleIndex * n];
+}
+const Point2f* Sampler::Get2DArray(int n) {
+    if (array2DOffset == sampleArray2D.size()) return nullptr;
+    return &sampleArray2D[array2DOffset++][currentPixelSampleIndex * n];
+}
+
+// ---- GlobalSampler (Sampler/Sampler.cpp:97-143); SampleDimension on the device
+void GlobalSampler::SampleValues(const std::vector<int64_t>& sampleNums, const std::vector<int>& dims, float* out) const {
+    if (sampleNums.size() != dims.size()) throw std::invalid_argument("SampleValues: sizes differ");
+    if (sampleNums.empty()) return;
+    const Point2i R = SampleRaster();
+    std::vector<int32_t> q(4 * dims.size());
+    for (size_t i = 0; i < dims.size(); ++i) {
+        if (dims[i] < 0 || dims[i] >= MaxDimensions()) throw std::out_of_range("sampler dimension beyond the sampler's tables");
+        if (sampleNums[i] < 0 || sampleNums[i] > 0x7fffffff) throw std::out_of_range("sample number beyond 31 bits");
+        q[4 * i] = currentPixel.x; q[4 * i + 1] = currentPixel.y;
+        q[4 * i + 2] = (int32_t)sampleNums[i]; q[4 * i + 3] = dims[i];
+    }
+    pbr_hip_ctx* h = helper_ctx();
+    check(h, pbr_hip_sampler_values(h, DeviceSampler(), R.x, R.y, (int)samplesPerPixel, (int)dims.size(), q.data(), out),
+          "pbr_hip_sampler_values");
+}
+float GlobalSampler::SampleValue(int64_t sampleNum, int dim) const {
+    float v = 0;
+    SampleValues({sampleNum}, {dim}, &v);
+    return v;
+}
+float GlobalSampler::value(int dim) {
+    if (cacheBase < 0 || dim < cacheBase || dim >= cacheBase + kValueBlock) {
+        const int n = std::max(1, std::min(kValueBlock, MaxDimensions() - dim));
+        std::vector<int64_t> nums(n, currentPixelSampleIndex);
+        std::vector<int> dims(n);
+        for (int k = 0; k < n; ++k) dims[k] = dim + k;
+        SampleValues(nums, dims, cache);
+        cacheBase = dim;
+    }
+    return cache[dim - cacheBase];
+}
+void GlobalSampler::StartPixel(const Point2i& p) {
+    Sampler::StartPixel(p);
+    dimension = 0;
+    cacheBase = -1;
+    arrayEndDim = arrayStartDim + (int)sampleArray1D.size() + 2 * (int)sampleArray2D.size();
+    // the arrays of every sample of the pixel, in one device query
+    std::vector<int64_t> nums;
+    std::vector<int> dims;
+    for (size_t i = 0; i < samples1DArraySizes.size(); ++i)
+        for (int64_t j = 0; j < samples1DArraySizes[i] * samplesPerPixel; ++j) { nums.push_back(j); dims.push_back(arrayStartDim + (int)i); }
+    int dim = arrayStartDim + (int)samples1DArraySizes.size();
+    for (size_t i = 0; i < samples2DArraySizes.size(); ++i, dim += 2)
+        for (int64_t j = 0; j < samples2DArraySizes[i] * samplesPerPixel; ++j)
+            for (int k = 0; k < 2; ++k) { nums.push_back(j); dims.push_back(dim + k); }
+    std::vector<float> v(nums.size());
+    SampleValues(nums, dims, v.data());
+    size_t k = 0;
+    for (size_t i = 0; i < samples1DArraySizes.size(); ++i)
+        for (auto& x : sampleArray1D[i]) x = v[k++];
+    for (size_t i = 0; i < samples2DArraySizes.size(); ++i)
+        for (auto& pt : sampleArray2D[i]) { pt.x = v[k++]; pt.y = v[k++]; }
+}
+bool GlobalSampler::StartNextSample() {
+    dimension = 0;
+    cacheBase = -1;
+    return Sampler::StartNextSample();
+}
+bool GlobalSampler::SetSampleNumber(int64_t sampleNum) {
+    dimension = 0;
+    cacheBase = -1;
+    return Sampler::SetSampleNumber(sampleNum);
+}
+float GlobalSampler::Get1D() {
+    if (dimension >= arrayStartDim && dimension < arrayEndDim) dimension = arrayEndDim;
+    return value(dimension++);
+}
+Point2f GlobalSampler::Get2D() {
+    if (dimension + 1 >= arrayStartDim && dimension < arrayEndDim) dimension = arrayEndDim;
+    const float x = value(dimension), y = value(dimension + 1);
+    dimension += 2;
+    return Point2f(x, y);
+}
 
 // ============================================================================ flattening
 struct FlatScene {
@@ -869,6 +1007,14 @@ void camera_desc(const PerspectiveCamera& cam, pbr_camera_desc* c) {
     c->focal_distance = cam.focalDistance;
     c->medium = -1;
 }
+// The samplers the device runs: HaltonSampler (any raster: its values depend on the pixel only) and
+// SobolSampler, whose resolution must be the camera's raster (the device derives it from there).
+void check_sampler(const Sampler& s, const PerspectiveCamera& cam, const char* who) {
+    if (!dynamic_cast<const HaltonSampler*>(&s) && !dynamic_cast<const SobolSampler*>(&s))
+        throw std::invalid_argument(std::string(who) + ": only HaltonSampler and SobolSampler are on the GPU path");
+    if (s.DeviceSampler() == PBR_SAMPLER_SOBOL && (s.SampleRaster().x != cam.RasterWidth || s.SampleRaster().y != cam.RasterHeight))
+        throw std::invalid_argument(std::string(who) + ": SobolSampler bounds must be the camera raster");
+}
 // Device 0 context for the stateless helpers (camera rays, sampler values).  Kept for the life of the
 // process: destroying it from a static destructor could run after the HIP runtime has shut down.
 pbr_hip_ctx* helper_ctx() {
@@ -883,8 +1029,7 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     auto t0 = std::chrono::steady_clock::now();
     auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
     if (!cam) throw std::invalid_argument("Render: only PerspectiveCamera is on the GPU path");
-    auto* halton = dynamic_cast<const HaltonSampler*>(sampler.get());
-    if (!halton) throw std::invalid_argument("Render: only HaltonSampler is on the GPU path");
+    check_sampler(*sampler, *cam, "Render");
     const int W = pixelBounds.pMax.x, H = pixelBounds.pMax.y;   // the reference reads pMax only
     if (W <= 0 || H <= 0 || W > cam->RasterWidth || H > cam->RasterHeight)
         throw std::invalid_argument("Render: pixelBounds outside the camera raster");
@@ -902,8 +1047,8 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     rd.max_depth = MaxDepth();
     rd.rr_threshold = RRThreshold();
     rd.light_strategy = LightStrategy();
-    rd.sampler = PBR_SAMPLER_HALTON;
-    rd.spp = (int)halton->samplesPerPixel;
+    rd.sampler = sampler->DeviceSampler();
+    rd.spp = (int)sampler->samplesPerPixel;
     camera_desc(*cam, &rd.camera);
     rd.camera.medium = MediumIndex(*flat, cam->medium);
     std::vector<pbr_tile> tl;
@@ -1102,23 +1247,6 @@ float PerspectiveCamera::GenerateRay(const CameraSample& sample, Ray* ray) const
     return 1;
 }
 
-CameraSample HaltonSampler::GetCameraSample(const Point2i& pRaster) {   // Sampler.cpp:10-21
-    const int W = sampleBounds.pMax.x - sampleBounds.pMin.x, H = sampleBounds.pMax.y - sampleBounds.pMin.y;
-    int32_t q[20];
-    for (int k = 0; k < 5; ++k) {
-        q[4 * k] = pRaster.x; q[4 * k + 1] = pRaster.y; q[4 * k + 2] = (int32_t)currentPixelSampleIndex; q[4 * k + 3] = k;
-    }
-    float v[5];
-    pbr_hip_ctx* h = helper_ctx();
-    check(h, pbr_hip_sampler_values(h, PBR_SAMPLER_HALTON, W, H, (int)samplesPerPixel, 5, q, v), "pbr_hip_sampler_values");
-    CameraSample cs;
-    cs.pFilm = Point2f((float)pRaster.x + v[0], (float)pRaster.y + v[1]);
-    cs.time = v[2];
-    cs.pLens = Point2f(v[3], v[4]);
-    dimension = 5;
-    return cs;
-}
-
 void SamplerIntegrator::ensure_scene(const Scene& scene) const {
     auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
     const Medium* cm = cam ? cam->medium : nullptr;
@@ -1136,10 +1264,13 @@ void SamplerIntegrator::Preprocess(const Scene& scene, Sampler&) { ensure_scene(
 std::vector<Spectrum> SamplerIntegrator::Li(const std::vector<Ray>& rays, const std::vector<Point2i>& pixels,
                                             const std::vector<int64_t>& samples, int dimension, const Scene& scene,
                                             int depth) const {
+    return LiWith(*sampler, rays, pixels, samples, dimension, scene, depth);
+}
+std::vector<Spectrum> SamplerIntegrator::LiWith(const Sampler& smp, const std::vector<Ray>& rays,
+                                                const std::vector<Point2i>& pixels, const std::vector<int64_t>& samples,
+                                                int dimension, const Scene& scene, int depth) const {
     if (pixels.size() != rays.size() || samples.size() != rays.size())
         throw std::invalid_argument("Li: rays, pixels and samples differ in length");
-    auto* halton = dynamic_cast<const HaltonSampler*>(sampler.get());
-    if (!halton) throw std::invalid_argument("Li: only HaltonSampler is on the GPU path");
     ensure_scene(scene);
     pbr_render_desc rd;
     std::memset(&rd, 0, sizeof(rd));
@@ -1147,10 +1278,10 @@ std::vector<Spectrum> SamplerIntegrator::Li(const std::vector<Ray>& rays, const 
     rd.max_depth = MaxDepth();
     rd.rr_threshold = RRThreshold();
     rd.light_strategy = LightStrategy();
-    rd.sampler = PBR_SAMPLER_HALTON;
-    rd.spp = (int)halton->samplesPerPixel;
-    rd.camera.width = halton->sampleBounds.pMax.x - halton->sampleBounds.pMin.x;   // the sampler's raster
-    rd.camera.height = halton->sampleBounds.pMax.y - halton->sampleBounds.pMin.y;
+    rd.sampler = smp.DeviceSampler();
+    rd.spp = (int)smp.samplesPerPixel;
+    rd.camera.width = smp.SampleRaster().x;   // the sampler's raster
+    rd.camera.height = smp.SampleRaster().y;
     rd.camera.fov = 90.f;
     rd.camera.camera_to_world.m[0] = rd.camera.camera_to_world.m[5] = rd.camera.camera_to_world.m[10] =
         rd.camera.camera_to_world.m[15] = 1.f;
@@ -1171,8 +1302,8 @@ std::vector<Spectrum> SamplerIntegrator::Li(const std::vector<Ray>& rays, const 
 }
 
 Spectrum SamplerIntegrator::Li(const RayDifferential& ray, const Scene& scene, Sampler& s, int depth) const {
-    return Li(std::vector<Ray>{ray}, std::vector<Point2i>{s.currentPixel}, std::vector<int64_t>{s.currentPixelSampleIndex},
-              s.dimension, scene, depth)[0];
+    return LiWith(s, std::vector<Ray>{ray}, std::vector<Point2i>{s.CurrentPixel()},
+                  std::vector<int64_t>{s.CurrentSampleNumber()}, s.CurrentDimension(), scene, depth)[0];
 }
 
 // ============================================================================ multi-GPU
@@ -1249,8 +1380,7 @@ void SamplerIntegrator::RenderMulti(const Scene& scene, double& timeConsume) {
     auto t0 = std::chrono::steady_clock::now();
     auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
     if (!cam) throw std::invalid_argument("Render: only PerspectiveCamera is on the GPU path");
-    auto* halton = dynamic_cast<const HaltonSampler*>(sampler.get());
-    if (!halton) throw std::invalid_argument("Render: only HaltonSampler is on the GPU path");
+    check_sampler(*sampler, *cam, "Render");
     if (!tiles.empty()) throw std::invalid_argument("Render: SetTiles and SetDevices are exclusive");
     const int W = pixelBounds.pMax.x, H = pixelBounds.pMax.y;
     if (W <= 0 || H <= 0 || W > cam->RasterWidth || H > cam->RasterHeight)
@@ -1306,8 +1436,8 @@ void SamplerIntegrator::RenderMulti(const Scene& scene, double& timeConsume) {
     rd.max_depth = MaxDepth();
     rd.rr_threshold = RRThreshold();
     rd.light_strategy = LightStrategy();
-    rd.sampler = PBR_SAMPLER_HALTON;
-    rd.spp = (int)halton->samplesPerPixel;
+    rd.sampler = sampler->DeviceSampler();
+    rd.spp = (int)sampler->samplesPerPixel;
     camera_desc(*cam, &rd.camera);
     rd.camera.medium = MediumIndex(*flat, cam->medium);
     rd.outputs_on_device = 1;

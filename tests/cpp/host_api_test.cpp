@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <unistd.h>
 #include <memory>
 #include <string>
 #include <vector>
@@ -154,14 +155,15 @@ void build_textured(Built& b, int W, int H) {
 }
 
 // The same camera/render settings as SamplerIntegrator::Render builds, for the oracle.
-pbr_render_desc oracle_desc(const Built& b, const FlatScene& flat, int integrator, int spp, int depth, float rr) {
+pbr_render_desc oracle_desc(const Built& b, const FlatScene& flat, int integrator, int spp, int depth, float rr,
+                            int sampler = PBR_SAMPLER_HALTON) {
     auto* cam = dynamic_cast<const PerspectiveCamera*>(b.cam.get());
     pbr_render_desc rd;
     std::memset(&rd, 0, sizeof(rd));
     rd.integrator = integrator;
     rd.max_depth = depth;
     rd.rr_threshold = rr;
-    rd.sampler = PBR_SAMPLER_HALTON;
+    rd.sampler = sampler;
     rd.spp = spp;
     rd.camera.width = cam->RasterWidth;
     rd.camera.height = cam->RasterHeight;
@@ -174,11 +176,11 @@ pbr_render_desc oracle_desc(const Built& b, const FlatScene& flat, int integrato
 
 // Renders `integrator` through the host API and compares its FrameBuffer with the oracle.
 void compare(const char* name, Built& b, std::shared_ptr<SamplerIntegrator> integ, FrameBuffer& fb, int itype, int spp,
-             int depth, float rr) {
+             int depth, float rr, int sampler = PBR_SAMPLER_HALTON) {
     double t = 0;
     integ->Render(*b.scene, t);
     auto flat = FlattenScene(*b.scene, nullptr);
-    pbr_render_desc rd = oracle_desc(b, *flat, itype, spp, depth, rr);
+    pbr_render_desc rd = oracle_desc(b, *flat, itype, spp, depth, rr, sampler);
     const int W = fb.width, H = fb.height;
     std::vector<float> rgb((size_t)W * H * 3);
     std::vector<uint8_t> rgba((size_t)W * H * 4);
@@ -374,17 +376,137 @@ void scene_queries() {
     expect(threw, "GeometricPrimitive outside a Scene throws");
 }
 
+// The sampler surface of Sampler.h: Get1D / Get2D / GetCameraSample / the 1D-2D arrays of a
+// GlobalSampler (Sampler.cpp:97-143) equal the oracle's SampleDimension for Halton and pbrt-v3's
+// SobolSampler, and Clone copies the sampler.
+void sampler_surface() {
+    const int W = 37, H = 21;
+    for (int kind = 0; kind < 2; ++kind) {
+        std::unique_ptr<GlobalSampler> s;
+        if (kind == 0) s.reset(new HaltonSampler(16, Bounds2i(Point2i(0, 0), Point2i(W, H))));
+        else s.reset(new SobolSampler(12, Bounds2i(Point2i(0, 0), Point2i(W, H))));   // → 16 spp
+        expect(s->samplesPerPixel == 16, kind ? "SobolSampler rounds spp up to a power of two" : "Halton spp");
+        s->Request1DArray(2);
+        s->Request2DArray(1);
+        int bad = 0, n = 0;
+        for (int px : {0, 5, 36})
+            for (int py : {0, 7, 20}) {
+                const Point2i pixel(px, py);
+                auto c = s->Clone(py * W + px);
+                c->StartPixel(pixel);
+                int64_t sample = 0;
+                do {
+                    // expected dims: 0..4 (camera), the 1D array at 5, the 2D array at 6-7 (arrayEndDim = 8),
+                    // then Get1D → 8, Get2D → 9, 10
+                    CameraSample cs = c->GetCameraSample(pixel);
+                    const float* a1 = c->Get1DArray(2);
+                    const Point2f* a2 = c->Get2DArray(1);
+                    const float u = c->Get1D();
+                    const Point2f v = c->Get2D();
+                    std::vector<int32_t> q;
+                    const int dims[] = {0, 1, 2, 3, 4, 8, 9, 10};
+                    for (int d : dims) q.insert(q.end(), {px, py, (int32_t)sample, d});
+                    // the arrays: the 1D array at dim 5 (its k-th value of sample s is sample number 2·s + k),
+                    // the 2D array at dims 6, 7
+                    for (int k = 0; k < 2; ++k) q.insert(q.end(), {px, py, (int32_t)(2 * sample + k), 5});
+                    q.insert(q.end(), {px, py, (int32_t)sample, 6});
+                    q.insert(q.end(), {px, py, (int32_t)sample, 7});
+                    const int nq = (int)q.size() / 4;
+                    std::vector<float> ref(nq);
+                    std::vector<int64_t> idx(nq);
+                    if (kind == 0) expect(oracle_halton(W, H, 16, nq, q.data(), ref.data()) == 0, "oracle_halton");
+                    else expect(oracle_sobol(W, H, nq, q.data(), nullptr, 0, ref.data(), idx.data()) == 0, "oracle_sobol");
+                    const float got[] = {cs.pFilm.x - (float)px, cs.pFilm.y - (float)py, cs.time, cs.pLens.x, cs.pLens.y, u, v.x, v.y,
+                                         a1[0], a1[1], a2[0].x, a2[0].y};
+                    for (int k = 0; k < nq; ++k) {
+                        const float g = got[k];
+                        float want = ref[k];
+                        if (k < 2) want = ((float)(k == 0 ? px : py) + ref[k]) - (float)(k == 0 ? px : py);
+                        if (std::memcmp(&g, &want, 4) != 0) ++bad;
+                        ++n;
+                    }
+                    ++sample;
+                } while (c->StartNextSample());
+                expect(sample == 16, "StartNextSample runs samplesPerPixel samples");
+            }
+        char msg[160];
+        std::snprintf(msg, sizeof msg, "%s: GetCameraSample / Get1D / Get2D / Get1DArray / Get2DArray = the oracle's "
+                      "SampleDimension (%d values, %d differ)", kind ? "SobolSampler" : "HaltonSampler", n, bad);
+        expect(bad == 0, msg);
+    }
+}
+
+// An ingested mesh through the C++ surface on the device: tests/golden/mesh_small.3d
+// read by plyInfo and built as main.cpp:332-348 builds the dragon (TriangleMesh with an
+// object-to-world translation, one Triangle per face, GeometricPrimitive with a glass material),
+// rendered by PathIntegrator::Render = the oracle on the flattened scene.
+void ply3d_render() {
+    char exe[4096];
+    const ssize_t len = readlink("/proc/self/exe", exe, sizeof exe - 1);
+    if (len <= 0) { expect(false, "locate the test binary"); return; }
+    exe[len] = 0;
+    std::string dir(exe);
+    dir = dir.substr(0, dir.rfind('/'));
+    plyInfo plyi(dir + "/../golden/mesh_small.3d");
+    expect(plyi.nVertices == 64 && plyi.nTriangles == 110, "plyInfo reads mesh_small.3d (64 vertices, 110 faces)");
+    Built b;
+    const int W = 40, H = 30, spp = 8;
+    build_area(b, W, H, false);   // floor + area light + camera; its tetrahedron is replaced below
+    std::vector<std::shared_ptr<Primitive>> prims;
+    auto* agg = dynamic_cast<const BVHAccel*>(b.scene->GetAggregate().get());
+    for (const auto& p : agg->Primitives()) {   // keep the floor and the light (not the glass tetrahedron)
+        auto gp = std::dynamic_pointer_cast<GeometricPrimitive>(p);
+        if (!gp || !dynamic_cast<const GlassMaterial*>(gp->material.get())) prims.push_back(p);
+    }
+    const Transform* o2w = keep(b, Translate(Vector3f(0.0f, -0.35f, 0.0f)));
+    const Transform* w2o = keep(b, Inverse(*o2w));
+    auto mesh = std::make_shared<TriangleMesh>(*o2w, plyi.nTriangles, plyi.vertexIndices.data(), plyi.nVertices,
+                                               plyi.vertexArray.data(), nullptr, nullptr, nullptr, nullptr);
+    auto glass = std::make_shared<GlassMaterial>(rgbTex(1, 1, 1), rgbTex(1, 1, 1), fTex(0.1f), fTex(0.1f), fTex(1.5f), nullptr, false);
+    for (int i = 0; i < plyi.nTriangles; ++i)
+        prims.push_back(std::make_shared<GeometricPrimitive>(std::make_shared<Triangle>(o2w, w2o, false, mesh, i), glass, nullptr,
+                                                             MediumInterface()));
+    b.scene = std::make_unique<Scene>(std::make_shared<BVHAccel>(prims, 1), b.scene->lights);
+    FrameBuffer fb;
+    fb.InitBuffer(W, H, 4);
+    auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+    auto p = std::make_shared<PathIntegrator>(8, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &fb);
+    compare("Path, plyInfo mesh_small.3d (glass)", b, p, fb, PBR_INTEGRATOR_PATH, spp, 8, 0.8f);
+}
+
+// pbrt-v3's SobolSampler through PathIntegrator::Render (C3's sampler, area light) = the oracle.
+void sobol_render() {
+    Built b;
+    const int W = 48, H = 40, spp = 16;
+    build_area(b, W, H, false);
+    FrameBuffer fb;
+    fb.InitBuffer(W, H, 4);
+    auto sampler = std::make_shared<SobolSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+    auto p = std::make_shared<PathIntegrator>(8, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &fb);
+    compare("Path + area light, SobolSampler", b, p, fb, PBR_INTEGRATOR_PATH, spp, 8, 0.8f, PBR_SAMPLER_SOBOL);
+    bool threw = false;
+    try {   // Sobol's resolution comes from the camera raster: other bounds are refused
+        auto other = std::make_shared<SobolSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W + 1, H)));
+        PathIntegrator q(8, b.cam, other, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &fb);
+        double t = 0;
+        q.Render(*b.scene, t);
+    } catch (const std::invalid_argument&) { threw = true; }
+    expect(threw, "SobolSampler bounds other than the camera raster are refused");
+}
+
 // The reference's per-sample loop (Integrator.cpp:286-313) written against the host API —
 // StartPixel, GetCameraSample, GenerateRayDifferential, Li, colObj += L, StartNextSample,
 // colObj / spp — gives bit for bit the frame Render gives.
 void decomposed_render_loop() {
-    for (int itype = 0; itype < 2; ++itype) {
+    for (int itype = 0; itype < 3; ++itype) {
         Built b;
         const int W = 20, H = 14, spp = 4;
         if (itype == 0) build_c1(b, W, H); else build_area(b, W, H, false);
         FrameBuffer fb;
         fb.InitBuffer(W, H, 4);
-        auto sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        std::shared_ptr<Sampler> sampler;
+        if (itype == 2) sampler = std::make_shared<SobolSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
+        else sampler = std::make_shared<HaltonSampler>(spp, Bounds2i(Point2i(0, 0), Point2i(W, H)));
         std::shared_ptr<SamplerIntegrator> integ;
         if (itype == 0) integ = std::make_shared<WhittedIntegrator>(5, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), &fb);
         else integ = std::make_shared<PathIntegrator>(6, b.cam, sampler, Bounds2i(Point2i(0, 0), Point2i(W, H)), 0.8f, "uniform", &fb);
@@ -395,24 +517,26 @@ void decomposed_render_loop() {
         for (int y = 0; y < H; y += 3)
             for (int x = 0; x < W; x += 2) {
                 const Point2i pixel(x, y);
-                sampler->StartPixel(pixel);
+                std::unique_ptr<Sampler> pixelSampler = sampler->Clone(W * y + x);
+                pixelSampler->StartPixel(pixel);
                 float col[3] = {0.f, 0.f, 0.f};
                 do {
-                    CameraSample cs = sampler->GetCameraSample(pixel);
+                    CameraSample cs = pixelSampler->GetCameraSample(pixel);
                     RayDifferential r;
                     b.cam->GenerateRayDifferential(cs, &r);
-                    r.ScaleDifferentials(1 / std::sqrt((float)sampler->samplesPerPixel));
-                    Spectrum L = integ->Li(r, *b.scene, *sampler, 0);
+                    r.ScaleDifferentials(1 / std::sqrt((float)pixelSampler->samplesPerPixel));
+                    Spectrum L = integ->Li(r, *b.scene, *pixelSampler, 0);
                     for (int c = 0; c < 3; ++c) col[c] = col[c] + L[c];
-                } while (sampler->StartNextSample());
+                } while (pixelSampler->StartNextSample());
                 for (int c = 0; c < 3; ++c) col[c] = col[c] / (float)spp;
                 const float* f = &fb.getFCbuffer()[((size_t)x + (size_t)(H - 1 - y) * W) * 4];
                 if (std::memcmp(col, f, sizeof col) != 0) ++bad;
                 ++checked;
             }
         char msg[200];
-        std::snprintf(msg, sizeof msg, "%s: the reference's per-sample loop through GetCameraSample / GenerateRay / Li "
-                      "= Render, bit for bit (%d pixels)", itype == 0 ? "Whitted C1" : "Path area light", checked);
+        std::snprintf(msg, sizeof msg, "%s: the reference's per-sample loop through Clone / StartPixel / GetCameraSample / "
+                      "GenerateRay / Li = Render, bit for bit (%d pixels)",
+                      itype == 0 ? "Whitted C1" : (itype == 1 ? "Path area light" : "Path area light, SobolSampler"), checked);
         expect(bad == 0, msg);
     }
 }
@@ -503,6 +627,9 @@ int run_gpu() {
     }
     scene_queries();
     decomposed_render_loop();
+    sampler_surface();
+    sobol_render();
+    ply3d_render();
     multi_gpu_render();
     return failures ? 1 : 0;
 }

@@ -32,6 +32,7 @@ sys.path[:0] = [os.path.dirname(os.path.dirname(HERE)), os.path.dirname(HERE)]
 import numpy as np  # noqa: E402
 
 import ref_lib as R  # noqa: E402
+from pysicalbasedraytracer_amd import scenes  # noqa: E402
 import ref_scenes as RS  # noqa: E402
 
 OUT = os.path.join(HERE, "ref_fixtures.json")
@@ -46,6 +47,10 @@ def main():
     out = {"generator": "tests/golden/make_ref_fixtures.py", "library": "oracle/_ref/libpbr_ref.so "
            "(reference sources unmodified, oracle/ref/Makefile)", "renders": {}, "frames": {}, "bvh": {}}
     for name, (s, rd) in RS.render_cases().items():
+        if "mesh_3d" in s.info:   # an ingested mesh: the reference's own reader gives the arrays the scene holds
+            v, i = R.ply_info(s.info["mesh_3d"])
+            V, F = scenes.load_3d(s.info["mesh_3d"])
+            assert np.array_equal(v.view(np.uint32), V.view(np.uint32)) and np.array_equal(i, F), name
         rgb, rgba, sec = R.render(s, rd)
         out["renders"][name] = {"digest": RS.scene_digest(s, rd), "n": int(rgb.shape[0]),
                                 "rgb": b64(rgb.astype("<f4")), "rgba": b64(rgba)}

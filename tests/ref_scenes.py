@@ -175,6 +175,21 @@ def render_cases():
     s.point_light((0.3, 1.2, 1.5), (8.0, 8.0, 8.0))
     out["whitted_facing_mirrors_d12"] = (s, scenes.render_desc(scenes.camera(32, 20, **CAM_C), capi.INTEGRATOR_WHITTED, 4, 12))
 
+    # an ingested mesh: tests/golden/mesh_small.3d through scenes.load_3d — the
+    # generator checks that the reference's own reader (plyInfo, Shape/plyRead.h:22-47) returns the
+    # same arrays — placed as main.cpp:332-348 does (TriangleMesh with an object-to-world translation)
+    import os
+    path3d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mesh_small.3d")
+    V, F = scenes.load_3d(path3d)
+    s = scenes.Scene()
+    s.mesh(V, F, s.glass(), xform=scenes.translate(0.0, -0.35, 0.0))
+    Pf, If = scenes.quad(-1.12, 6.0)
+    s.mesh(Pf, If, s.matte((0.7, 0.7, 0.7)))
+    Pl, Il = scenes.quad(2.45, 1.4, flip=True)
+    s.area_light_mesh(Pl, Il, (5.0, 5.0, 5.0), s.matte((0.5, 0.5, 0.5)), n_samples=2)
+    s.info["mesh_3d"] = path3d
+    out["path_mesh_small_3d"] = (s, scenes.render_desc(scenes.camera(40, 24, **CAM_C), capi.INTEGRATOR_PATH, 16, 8, 0.8))
+
     # thin-lens cameras (Perspective.cpp:28-32,49-62): PerspectiveCamera with an aperture, pLens from
     # the sampler's dimensions 3-4 through ConcentricSampleDisk, focused behind / in front of the dragon
     for integ, name, spp, (lr, fd) in ((capi.INTEGRATOR_WHITTED, "whitted", 8, (0.08, 2.7)),
