@@ -147,6 +147,10 @@ def cpu_baseline(config, budget_s):
     what = ("the reference's own code (oracle/_ref/libpbr_ref.so: its unmodified sources, SamplerIntegrator::"
             "Render's per-pixel body over the sampled rows)" if kind == "reference" else
             "the oracle/ CPU restatement")
+    from pysicalbasedraytracer_amd import scenes
+    if kind == "reference" and scenes.CONFIGS[config]()[1].sampler != 0:
+        what += (", run with the reference's HaltonSampler in place of the Sobol sampler the GPU uses (the "
+                 "reference ships the Sobol tables but no SobolSampler, F3); same scene, raster, spp and depth")
     limit = ""
     if topo["physical_cores_socket0"] and topo["threads"] < topo["physical_cores_socket0"]:
         limit = (f"; the job may use {topo['threads']} of socket 0's {topo['physical_cores_socket0']} physical cores "

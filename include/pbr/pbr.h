@@ -482,7 +482,8 @@ class Aggregate : public Primitive {   // Core/Primitive.h:47-55
 class BVHAccel : public Aggregate {   // Accelerator/BVHAccel.h:16-21; built on the device at upload
   public:
     // SAH is the reference's builder; HLBVH falls through to SAH there (BVHAccel.cpp:131-160, no
-    // HLBVH code path) and here.  Middle and EqualCounts are not on the GPU path (refused).
+    // HLBVH code path) and here.  SAH/HLBVH build on the device; Middle and EqualCounts run the host
+    // builder (std::partition / std::nth_element as BVHAccel.cpp:136-158 calls them) at upload.
     enum class SplitMethod { SAH, HLBVH, Middle, EqualCounts };
     BVHAccel(std::vector<std::shared_ptr<Primitive>> p, int maxPrimsInNode = 1, SplitMethod splitMethod = SplitMethod::SAH);
     const std::vector<std::shared_ptr<Primitive>>& Primitives() const { return primitives; }

@@ -2015,6 +2015,11 @@ int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height,
         s.hiShift = 32 - 2 * s.sobolLog2Res;
         s.spp = 0;   // the mask (spp - 1) of sobol_dimension becomes all ones
     }
+    // queries index the prime / permutation (Halton: 1000 dimensions) and matrix (Sobol) tables
+    const int maxDims = sampler == PBR_SAMPLER_SOBOL ? s.nSobolDims : 1000;
+    for (int i = 0; i < n; ++i)
+        if (q[4 * i] < 0 || q[4 * i + 1] < 0 || q[4 * i + 2] < 0 || q[4 * i + 3] < 0 || q[4 * i + 3] >= maxDims)
+            return set_err(ctx, PBR_E_INVALID, "sampler query: negative pixel / sample or dimension beyond the tables");
     HaltonParams hp = hparams(s);
     HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 16));
     HIP_TRY(ctx->dScratchOut.ensure((size_t)n * 4));
