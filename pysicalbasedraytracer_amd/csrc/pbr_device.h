@@ -254,6 +254,22 @@ __device__ __forceinline__ bool node_slab(f3 lo, f3 hi, const Ray& r, f3 inv, bo
 constexpr int kShortStack = PBR_SHORT_STACK_DEPTH;
 __shared__ int s_trav_ref[kShortStack * 256];
 __shared__ float s_trav_t[kShortStack * 256];
+// A deeper LDS short stack for the kernels with LDS to spare: the closest-hit lane-refill kernels
+// (5 workgroups per CU) and the camera kernels (no segment scan).  C3 / C5 frame ms with the refill
+// kernels at 6 entries 276.6 / 1416, 10: 271.6 / 1386, 14 (4 workgroups per CU fit): 285.5 / 1403.
+#ifndef PBR_REFILL_SHORT
+#define PBR_REFILL_SHORT 10
+#endif
+constexpr int kRefillShort = PBR_REFILL_SHORT;
+__shared__ int s_trav_ref_r[kRefillShort * 256];
+__shared__ float s_trav_t_r[kRefillShort * 256];
+// the LDS short stack of depth SHORT ([entry][lane]) for this thread
+template <int SHORT>
+__device__ __forceinline__ void trav_lds(int** ref, float** t) {
+    static_assert(SHORT == kShortStack || SHORT == kRefillShort, "short stack depth");
+    if constexpr (SHORT == kShortStack) { *ref = s_trav_ref + threadIdx.x; *t = s_trav_t + threadIdx.x; }
+    else { *ref = s_trav_ref_r + threadIdx.x; *t = s_trav_t_r + threadIdx.x; }
+}
 
 // The binary traversal below over the quad layout of build_quad_nodes: one node fetch covers two
 // binary levels, halving the chain of dependent node loads per ray.  Visit order stays BVHAccel's:
@@ -361,7 +377,7 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
     float stackT[PRIV];
     int* lref = nullptr;
     float* lt = nullptr;
-    if constexpr (SHORT > 0) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
+    if constexpr (SHORT > 0) trav_lds<SHORT>(&lref, &lt);
     int sp = 0;             // entries held (stack depth; with BT at most SHORT)
     int top = 0;            // BT: ring position of the next push
     bool dropped = false;   // BT: an entry was overwritten
@@ -484,7 +500,7 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
 // there a far child whose slab fails is still pushed (with a NaN key, so its pop test fails).
 template <bool ANY, bool STATS, int SHORT = 0>
 __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
-    static_assert(SHORT == 0 || SHORT == kShortStack, "short stack is kShortStack deep");
+    static_assert(SHORT == 0 || SHORT == kShortStack || SHORT == kRefillShort, "short stack depth");
     if (STATS) c->rays++;
     if (S.nNodes == 0) return false;
     f3 inv = ANY ? mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z) : mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
@@ -499,7 +515,7 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
     float stackT[64 - SHORT];
     int* lref = nullptr;
     float* lt = nullptr;
-    if constexpr (SHORT > 0) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
+    if constexpr (SHORT > 0) trav_lds<SHORT>(&lref, &lt);
     int cur = S.rootRef, sp = 0;
     bool found = false;
     while (true) {

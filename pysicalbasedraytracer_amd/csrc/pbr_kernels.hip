@@ -1212,7 +1212,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         int cur = 0;
         W.cur = queue(l, 0);
         PROF_LAUNCH(KP_WF_CAMERA, st,
-            if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
+            if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kCameraShort>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
             else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, st, W));
         prof_host(ctx, KP_WF_CAMERA, 0, (unsigned long long)W.nSamples);
         const hipStream_t sst = shadowOverlap ? ctx->shadowStream[l] : st;
@@ -1370,7 +1370,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
         W.cur = queue(l, 0);
-        PROF_LAUNCH(KP_WFP_CAMERA, st, hipLaunchKernelGGL(k_wfp_camera_extend<kShortStack>, dim3((W.nSamples + 255) / 256), blk, 0, st, X));
+        PROF_LAUNCH(KP_WFP_CAMERA, st, hipLaunchKernelGGL(k_wfp_camera_extend<kCameraShort>, dim3((W.nSamples + 255) / 256), blk, 0, st, X));
         prof_host(ctx, KP_WFP_CAMERA, 0, (unsigned long long)W.nSamples);
         for (int level = 0;; ++level) {   // ends below: at maxLevels, or when no continuation is queued
             W.cur = queue(l, cur);

@@ -172,15 +172,14 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 #define PBR_REFILL_OCC_TR 6
 #endif
 constexpr int kRefill = PBR_REFILL;
-// LDS entries of the closest-hit refill kernels' short stack (their 5 workgroups per CU leave LDS
-// room for more than the 6 of the other traversal kernels).  C3 / C5 frame ms: 6 entries 276.6 /
-// 1416, 10: 271.6 / 1386, 14 (4 workgroups per CU fit): 285.5 / 1403.
-#ifndef PBR_REFILL_SHORT
-#define PBR_REFILL_SHORT 10
+// LDS short-stack entries of the camera kernels.  They have no segment scan, so 7 workgroups per CU
+// would fit 10 entries (20 KB): C2's camera kernel then took 8.95 → 8.02 ms/frame, but the other
+// lane's extend, sharing the CUs, 5.28 → 6.75 and the frame 17.7 → 18.0 ms — kept at 6.
+#ifndef PBR_CAMERA_SHORT
+#define PBR_CAMERA_SHORT PBR_SHORT_STACK_DEPTH
 #endif
-constexpr int kRefillShort = PBR_REFILL_SHORT;
-__shared__ int s_trav_ref_r[kRefillShort * 256];
-__shared__ float s_trav_t_r[kRefillShort * 256];
+constexpr int kCameraShort = PBR_CAMERA_SHORT;
+
 // load(i, &key) → the i-th ray of the queue (key: what store needs, e.g. its queue position);
 // store(key, hit, ray, h) → the ray's result (closest hit: ray.tMax and h; any hit: hit only).
 template <bool ANY, int SHORT, class Load, class Store>
@@ -193,8 +192,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
     const unsigned long long below = (1ull << lane) - 1ull;
     int* lref;
     float* lt;
-    if constexpr (SHORT == kShortStack) { lref = s_trav_ref + threadIdx.x; lt = s_trav_t + threadIdx.x; }
-    else { static_assert(SHORT == kRefillShort, "short stack depth"); lref = s_trav_ref_r + threadIdx.x; lt = s_trav_t_r + threadIdx.x; }
+    trav_lds<SHORT>(&lref, &lt);
     constexpr int PRIV = 64 - SHORT;
     int stackRef[PRIV];
     float stackT[PRIV];
@@ -505,7 +503,12 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                     }
                     float flagsA = 0.f;
                     bool final_ = true;
-                    if (depth + 1 < P.maxDepth) {   // SpecularReflect (Integrator.cpp:179-222)
+                    // SpecularReflect (Integrator.cpp:179-222).  A BSDF without a specular reflection lobe
+                    // returns black from Sample_f whatever the sample (Reflection.cpp:113-114), and the
+                    // path ends here, so the two sampler dimensions are not drawn (C2's matte dragon)
+                    if (depth + 1 < P.maxDepth && num_components(bsdf, BSDF_REFLECTION | BSDF_SPECULAR) == 0) {
+                        flagsA = 1.f;   // L += Spectrum(0) from a failed SpecularReflect
+                    } else if (depth + 1 < P.maxDepth) {
                         f3 wi = mk(0, 0, 0);
                         float pdf = 0;
                         int stype = 0;
@@ -711,7 +714,11 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
             const size_t ri = (size_t)depth * W.cap + id;
             float flagsA = 0.f;
             bool final_ = true;
-            if (depth + 1 < P.maxDepth) {   // SpecularReflect (Integrator.cpp:179-222)
+            // SpecularReflect (Integrator.cpp:179-222); no specular reflection lobe: black, the path
+            // ends, no sampler dimensions drawn (as k_wf_shade)
+            if (depth + 1 < P.maxDepth && num_components(bsdf, BSDF_REFLECTION | BSDF_SPECULAR) == 0) {
+                flagsA = 1.f;   // L += Spectrum(0) from a failed SpecularReflect
+            } else if (depth + 1 < P.maxDepth) {
                 f3 wi = mk(0, 0, 0);
                 float pdf = 0;
                 int stype = 0;
