@@ -782,7 +782,14 @@ struct WfBufs {
 };
 // Chunks alternate between two lanes (own buffers, own stream) so one chunk's launch tails overlap
 // the other's work — what keeps a small per-GPU shard of a multi-GPU frame efficient.
-constexpr int kWfLanes = 2;
+// Lanes a frame may use (PBR_LANES), and the default.  Measured (frame ms, bit-identical):
+// C2 2 lanes 17.73-17.80, 3: 17.49, 4: 17.97 (4 lanes of 2^24-sample chunks 19.10); C3 268.7 /
+// 267.3 / 274.9; C5 1396 / 1379 / 1414.
+constexpr int kWfLanes = 4;
+#ifndef PBR_LANES_DEFAULT
+#define PBR_LANES_DEFAULT 3
+#endif
+constexpr int kWfDefaultLanes = PBR_LANES_DEFAULT;
 
 struct pbr_hip_ctx {
     int device = 0;
@@ -808,8 +815,8 @@ struct pbr_hip_ctx {
     bool inFlight = false;
     // wavefront buffers of the two chunk lanes, and the lane-1 stream with its fork/join events
     WfBufs wb[kWfLanes];
-    hipStream_t side = nullptr;
-    hipEvent_t evFork = nullptr, evJoin = nullptr;
+    hipStream_t side[kWfLanes] = {};     // lanes 1.. (lane 0 runs on the caller's stream)
+    hipEvent_t evFork = nullptr, evJoin[kWfLanes] = {};
     // Whitted: per lane, a stream for the shadow rays and per-level events (shade done, shadow done)
     hipStream_t shadowStream[kWfLanes] = {};
     hipEvent_t evShade[kWfLanes][kWfMaxDepth + 2] = {}, evShadow[kWfLanes][kWfMaxDepth + 2] = {};
@@ -867,7 +874,8 @@ int drain(pbr_hip_ctx* ctx) {
 void quiesce(pbr_hip_ctx* ctx, hipStream_t s) {
     if (s) (void)hipStreamSynchronize(s);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    for (int l = 0; l < kWfLanes; ++l)
+        if (ctx->side[l]) (void)hipStreamSynchronize(ctx->side[l]);
     for (int l = 0; l < kWfLanes; ++l)
         if (ctx->shadowStream[l]) (void)hipStreamSynchronize(ctx->shadowStream[l]);
     ctx->inFlight = false;
@@ -1028,7 +1036,7 @@ WfChunks wf_chunks(const KParams& P, int maxLog2 = 25) {
     WfChunks c;
     int chunkLog2 = maxLog2;
     if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
-    c.lanes = kWfLanes;
+    c.lanes = kWfDefaultLanes;
     if (const char* e = getenv("PBR_LANES")) c.lanes = std::min(kWfLanes, std::max(1, atoi(e)));
     c.chunkPix = std::max(1LL, (1LL << chunkLog2) / P.spp);
     if (c.chunkPix >= P.nPixels) {   // one chunk: splitting a small frame only adds launch tails
@@ -1044,19 +1052,22 @@ WfChunks wf_chunks(const KParams& P, int maxLog2 = 25) {
 // Fork lane 1 off `s` at the start of a frame, join it back at the end.
 int wf_fork(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
     if (lanes < 2) return PBR_OK;
-    if (!ctx->side) {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->evJoin, hipEventDisableTiming));
-    }
+    if (!ctx->evFork) HIP_TRY(hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
+    for (int l = 1; l < lanes; ++l)
+        if (!ctx->side[l]) {
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->side[l], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->evJoin[l], hipEventDisableTiming));
+        }
     HIP_TRY(hipEventRecord(ctx->evFork, s));
-    HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->evFork, 0));
+    for (int l = 1; l < lanes; ++l) HIP_TRY(hipStreamWaitEvent(ctx->side[l], ctx->evFork, 0));
     return PBR_OK;
 }
 int wf_join(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
     if (lanes < 2) return PBR_OK;
-    HIP_TRY(hipEventRecord(ctx->evJoin, ctx->side));
-    HIP_TRY(hipStreamWaitEvent(s, ctx->evJoin, 0));
+    for (int l = 1; l < lanes; ++l) {
+        HIP_TRY(hipEventRecord(ctx->evJoin[l], ctx->side[l]));
+        HIP_TRY(hipStreamWaitEvent(s, ctx->evJoin[l], 0));
+    }
     return PBR_OK;
 }
 dim3 resident_grid(pbr_hip_ctx* ctx, const void* fn) {
@@ -1204,7 +1215,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     int chunk = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
         const int l = chunk % ch.lanes;
-        const hipStream_t st = l ? ctx->side : s;
+        const hipStream_t st = l ? ctx->side[l] : s;
         WfParams& W = WL[l];
         W.chunkPix0 = p0;
         W.chunkPix = (int)std::min<long long>(ch.chunkPix, P.nPixels - p0);
@@ -1361,7 +1372,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     int chunk = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
         const int l = chunk % ch.lanes;
-        const hipStream_t st = l ? ctx->side : s;
+        const hipStream_t st = l ? ctx->side[l] : s;
         WfvParams& V = VL[l];
         WfpParams& X = V.X;
         WfParams& W = X.W;
@@ -1654,7 +1665,8 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)drain(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    for (int l = 0; l < kWfLanes; ++l)
+        if (ctx->side[l]) (void)hipStreamSynchronize(ctx->side[l]);
     for (int l = 0; l < kWfLanes; ++l) {
         if (ctx->shadowStream[l]) (void)hipStreamSynchronize(ctx->shadowStream[l]);
         for (int k = 0; k < kWfMaxDepth + 2; ++k) {
@@ -1664,8 +1676,10 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
         if (ctx->shadowStream[l]) (void)hipStreamDestroy(ctx->shadowStream[l]);
     }
     if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
-    if (ctx->evJoin) (void)hipEventDestroy(ctx->evJoin);
-    if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    for (int l = 0; l < kWfLanes; ++l) {
+        if (ctx->evJoin[l]) (void)hipEventDestroy(ctx->evJoin[l]);
+        if (ctx->side[l]) (void)hipStreamDestroy(ctx->side[l]);
+    }
     for (auto& e : ctx->profEv) {
         if (e.a) (void)hipEventDestroy(e.a);
         if (e.b) (void)hipEventDestroy(e.b);

@@ -116,7 +116,10 @@ __device__ __forceinline__ int shade_sort(int q, bool active, int key) {
 
 // One bounce of PathIntegrator::Li for every queued ray.
 // Waves per SIMD: 3 for either lobe set (all lobes, C4: 2 → 9.58 s, 3 → 8.86 s, 4 → 9.32 s)
-template <int LOBES, bool MATS_LDS, int OCC = 3>
+#ifndef PBR_WFP_OCC
+#define PBR_WFP_OCC 3
+#endif
+template <int LOBES, bool MATS_LDS, int OCC = PBR_WFP_OCC>
 __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0) {
     WfParams& W = X.W;
     const KParams& P = W.P;
