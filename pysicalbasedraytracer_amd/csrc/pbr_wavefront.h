@@ -390,6 +390,9 @@ __global__ __launch_bounds__(256, REFILL ? PBR_REFILL_OCC : PBR_TRAV_OCC) void k
 // One level of WhittedIntegrator::Li for every queued ray (single-light scenes).  LOBES: the lobe
 // kinds present in the scene (kSimpleLobes drops the microfacet code and its registers).
 constexpr int kSimpleLobes = (1 << L_LAMBERT) | (1 << L_OREN) | (1 << L_SPEC_R) | (1 << L_SPEC_T) | (1 << L_FRESNEL_SPEC);
+// Lambert and rough (microfacet) reflection / transmission only — matte, plastic, metal and rough
+// glass: the Path/VolPath shading kernels for C4 and C5 without the specular and Oren-Nayar code
+constexpr int kMicroLobes = (1 << L_LAMBERT) | (1 << L_MF_R) | (1 << L_MF_T);
 // MATS_LDS: the material templates fit kLdsMats and are read from an LDS copy (the BSDF code walks
 // them with dependent loads).
 constexpr int kLdsMats = 32;
