@@ -155,156 +155,192 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
             active = q >= 0;
             if (!active) q = 0;
         }
+        // Two phases around the light-estimate pushes: the estimate's record, shadow and probe rays
+        // are written as soon as they exist, so their registers are free during the path's BSDF
+        // sample; only the record's target (the continuation's position) is written at the end.
         bool pushShadow = false, pushProbe = false, pushDirect = false, pushNext = false;
+        bool cont2 = false;   // phase 2 runs: the path samples its BSDF
         int id = 0, dim = 0, bounces = 0;
         bool specularBounce = false;
-        Ray shadow, probe, cont;
-        rgb L, beta, A, fB, betaD;
-        float etaScale = 1.f, pmfD = 0.f, weightB = 1.f, scatPdfD = 0.f;
+        Ray cont, ray;
+        rgb L, beta;
+        float etaScale = 1.f;
         uint32_t sIndex = 0;
-        int dflagsD = 0, lightD = 0;
-        if (active) {
-            float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
-            id = level0 ? q : W.cur.id[q];
-            const int dd = __float_as_int(d.w);
-            dim = dd & 0xffff;
-            bounces = (dd >> 16) & 0x7f;
-            specularBounce = (dd >> 23) & 1;
-            Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
-            const int slot = __float_as_int(hr.x);
-            const bool found = slot >= 0;
-            if (level0) {
-                L = sp(0.f); beta = sp(1.f); etaScale = 1.f;
-                sIndex = W.sampleIndex[q];
-            } else {
-                const float4 a = W.cur.s0[q], b = W.cur.s1[q];
-                L = sp3(a.x, a.y, a.z); beta = sp3(a.w, b.x, b.y);
-                etaScale = b.z;
-                sIndex = __float_as_uint(b.w);
-            }
-            Isect isect;
-            if (found) {
-                int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
-                if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
-                else triangle_si(S, slot, ray, hr.y, hr.z, hr.w, flags, &isect);
-                isect.slot = slot;
-                isect.medIn = isect.medOut = -1;
-            }
-            if (bounces == 0 || specularBounce) {
-                if (found) L = L + beta * si_Le(S, isect, -ray.d);
-                else for (int k = 0; k < S.nInfinite; ++k) L = L + beta * light_Le(S, S.lights[S.infinite[k]], ray);
-            }
-            bool alive = found && bounces < P.maxDepth;
-            BSDF bsdf;
-            MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
-            if (alive && !make_bsdf<(LOBES & kTexturedLobes) != 0>(S, mats, isect, true, &bsdf, &texLocal)) {
-                cont = spawn_ray(isect, ray.d);   // isect.SpawnRay(ray.d); bounces-- then ++: same bounce
-                pushNext = true;
-                alive = false;
-            } else if (alive) {
-                SState st;
-                st.index = sIndex;
-                st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
-                st.dim = dim;
-                st.px = st.py = 0;
-                const f3 wo = isect.wo;
-                if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0 && S.nLights > 0) {
-                    // UniformSampleOneLight: light choice, then EstimateDirect's two strategies
-                    float pmf;
-                    const int li = sample_light(S, get1d<true>(P.smp, st), &pmf);
-                    if (pmf != 0) {
-                        float uL0, uL1, uS0, uS1;
-                        get2d<true>(P.smp, st, &uL0, &uL1);
-                        get2d<true>(P.smp, st, &uS0, &uS1);
-                        const DLight& light = S.lights[li];
-                        const bool delta = light.type == LT_POINT;
-                        const int flagsNS = BSDF_ALL & ~BSDF_SPECULAR;
-                        int dflags = 0;
-                        f3 wi = mk(0, 0, 0);
-                        float lightPdf = 0, scatteringPdf = 0;
-                        VisPt vis;
-                        rgb Li = sample_li(S, light, isect, uL0, uL1, &wi, &lightPdf, &vis);
-                        A = sp(0.f);
-                        if (lightPdf > 0 && !black(Li)) {
-                            rgb f = bsdf_f<LOBES>(bsdf, wo, wi, flagsNS) * absdot(wi, isect.sn);
-                            scatteringPdf = bsdf_pdf<LOBES>(bsdf, wo, wi, flagsNS);
-                            if (!black(f)) {
-                                if (delta) A = f * Li / lightPdf;
-                                else {
-                                    float fp = 1 * lightPdf, gp = 1 * scatteringPdf;
-                                    float weight = (fp * fp) / (fp * fp + gp * gp);
-                                    A = f * Li * weight / lightPdf;
-                                }
-                                shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
-                                pushShadow = true;
-                                dflags |= kWfpAPending;
-                            }
-                        }
-                        fB = sp(0.f);
-                        weightB = 1.f;
-                        if (!delta) {
-                            int stype = 0;
-                            fB = bsdf_sample<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
-                            fB = fB * absdot(wi, isect.sn);
-                            const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
-                            if (!black(fB) && scatteringPdf > 0) {
-                                bool probeIt = true;
-                                if (!sampledSpecular) {
-                                    float lp = pdf_li(S, light, isect, wi);
-                                    if (lp == 0) probeIt = false;
+        Isect isect;
+        BSDF bsdf;
+        MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+        SState st;
+        st.index = 0; st.sid = 0; st.dim = 0; st.px = st.py = 0;
+        int di = -1;
+        {
+            Ray shadow, probe;
+            rgb A, fB;
+            float pmfD = 0.f, weightB = 1.f, scatPdfD = 0.f;
+            int dflagsD = 0, lightD = 0;
+            if (active) {
+                float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
+                id = level0 ? q : W.cur.id[q];
+                const int dd = __float_as_int(d.w);
+                dim = dd & 0xffff;
+                bounces = (dd >> 16) & 0x7f;
+                specularBounce = (dd >> 23) & 1;
+                ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
+                const int slot = __float_as_int(hr.x);
+                const bool found = slot >= 0;
+                if (level0) {
+                    L = sp(0.f); beta = sp(1.f); etaScale = 1.f;
+                    sIndex = W.sampleIndex[q];
+                } else {
+                    const float4 a = W.cur.s0[q], b = W.cur.s1[q];
+                    L = sp3(a.x, a.y, a.z); beta = sp3(a.w, b.x, b.y);
+                    etaScale = b.z;
+                    sIndex = __float_as_uint(b.w);
+                }
+                if (found) {
+                    int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
+                    if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
+                    else triangle_si(S, slot, ray, hr.y, hr.z, hr.w, flags, &isect);
+                    isect.slot = slot;
+                    isect.medIn = isect.medOut = -1;
+                }
+                if (bounces == 0 || specularBounce) {
+                    if (found) L = L + beta * si_Le(S, isect, -ray.d);
+                    else for (int k = 0; k < S.nInfinite; ++k) L = L + beta * light_Le(S, S.lights[S.infinite[k]], ray);
+                }
+                bool alive = found && bounces < P.maxDepth;
+                if (alive && !make_bsdf<(LOBES & kTexturedLobes) != 0>(S, mats, isect, true, &bsdf, &texLocal)) {
+                    cont = spawn_ray(isect, ray.d);   // isect.SpawnRay(ray.d); bounces-- then ++: same bounce
+                    pushNext = true;
+                    alive = false;
+                } else if (alive) {
+                    cont2 = true;
+                    st.index = sIndex;
+                    st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
+                    st.dim = dim;
+                    const f3 wo = isect.wo;
+                    if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0 && S.nLights > 0) {
+                        // UniformSampleOneLight: light choice, then EstimateDirect's two strategies
+                        float pmf;
+                        const int li = sample_light(S, get1d<true>(P.smp, st), &pmf);
+                        if (pmf != 0) {
+                            float uL0, uL1, uS0, uS1;
+                            get2d<true>(P.smp, st, &uL0, &uL1);
+                            get2d<true>(P.smp, st, &uS0, &uS1);
+                            const DLight& light = S.lights[li];
+                            const bool delta = light.type == LT_POINT;
+                            const int flagsNS = BSDF_ALL & ~BSDF_SPECULAR;
+                            int dflags = 0;
+                            f3 wi = mk(0, 0, 0);
+                            float lightPdf = 0, scatteringPdf = 0;
+                            VisPt vis;
+                            rgb Li = sample_li(S, light, isect, uL0, uL1, &wi, &lightPdf, &vis);
+                            A = sp(0.f);
+                            if (lightPdf > 0 && !black(Li)) {
+                                rgb f = bsdf_f<LOBES>(bsdf, wo, wi, flagsNS) * absdot(wi, isect.sn);
+                                scatteringPdf = bsdf_pdf<LOBES>(bsdf, wo, wi, flagsNS);
+                                if (!black(f)) {
+                                    if (delta) A = f * Li / lightPdf;
                                     else {
-                                        float fp = 1 * scatteringPdf, gp = 1 * lp;
-                                        weightB = (fp * fp) / (fp * fp + gp * gp);
+                                        float fp = 1 * lightPdf, gp = 1 * scatteringPdf;
+                                        float weight = (fp * fp) / (fp * fp + gp * gp);
+                                        A = f * Li * weight / lightPdf;
+                                    }
+                                    shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
+                                    pushShadow = true;
+                                    dflags |= kWfpAPending;
+                                }
+                            }
+                            fB = sp(0.f);
+                            weightB = 1.f;
+                            if (!delta) {
+                                int stype = 0;
+                                fB = bsdf_sample<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
+                                fB = fB * absdot(wi, isect.sn);
+                                const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
+                                if (!black(fB) && scatteringPdf > 0) {
+                                    bool probeIt = true;
+                                    if (!sampledSpecular) {
+                                        float lp = pdf_li(S, light, isect, wi);
+                                        if (lp == 0) probeIt = false;
+                                        else {
+                                            float fp = 1 * scatteringPdf, gp = 1 * lp;
+                                            weightB = (fp * fp) / (fp * fp + gp * gp);
+                                        }
+                                    }
+                                    if (probeIt) {
+                                        probe = spawn_ray(isect, wi);
+                                        pushProbe = true;
+                                        dflags |= kWfpBPending;
                                     }
                                 }
-                                if (probeIt) {
-                                    probe = spawn_ray(isect, wi);
-                                    pushProbe = true;
-                                    dflags |= kWfpBPending;
-                                }
+                            }
+                            if (dflags) {
+                                pmfD = pmf;
+                                scatPdfD = scatteringPdf;
+                                dflagsD = dflags;
+                                lightD = li;
+                                pushDirect = true;
                             }
                         }
-                        if (dflags) {   // the record is written at its queue position below
-                            pmfD = pmf;
-                            scatPdfD = scatteringPdf;
-                            dflagsD = dflags;
-                            lightD = li;
-                            pushDirect = true;
-                        }
                     }
                 }
-                betaD = beta;   // beta at the estimate (the direct record's)
-                // BSDF sample for the path (PathIntegrator.cpp:80-105): wo is -ray.d here, not the
-                // normalised isect.wo the light estimate uses
-                const f3 woPath = -ray.d;
-                f3 wi = mk(0, 0, 0);
-                float pdf = 0;
-                int flags = 0;
-                float u0, u1;
-                get2d<true>(P.smp, st, &u0, &u1);
-                rgb f = bsdf_sample<LOBES>(bsdf, woPath, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
-                if (!(black(f) || pdf == 0.f)) {
-                    beta = beta * (f * absdot(wi, isect.sn) / pdf);
-                    specularBounce = (flags & BSDF_SPECULAR) != 0;
-                    if ((flags & BSDF_SPECULAR) && (flags & BSDF_TRANSMISSION)) {
-                        float eta = bsdf.mt->eta;
-                        etaScale *= (dot(woPath, isect.n) > 0) ? (eta * eta) : 1 / (eta * eta);
-                    }
-                    cont = spawn_ray(isect, wi);
-                    bool stop = false;
-                    rgb rrBeta = beta * etaScale;
-                    if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
-                        float qq = mx((float).05, 1 - maxval(rrBeta));
-                        if (get1d<true>(P.smp, st) < qq) stop = true;
-                        else beta = beta / (1 - qq);
-                    }
-                    if (!stop) {
-                        pushNext = true;
-                        bounces += 1;
-                    }
-                }
-                dim = st.dim;
             }
+            // the estimate's record (beta at the estimate: the path's beta before its BSDF sample),
+            // its shadow and probe rays
+            di = base + wave_push(&s_push[2], pushDirect);
+            if (pushDirect) {
+                X.dA[di] = make_float4(A.r, A.g, A.b, pmfD);
+                X.dB[di] = make_float4(fB.r, fB.g, fB.b, weightB);
+                X.dBeta[di] = make_float4(beta.r, beta.g, beta.b, scatPdfD);
+                X.dFlags[di] = dflagsD;
+                X.dLight[di] = lightD;
+            }
+            const int si = base + wave_push(&s_push[0], pushShadow);
+            if (pushShadow) {
+                W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
+                W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, 0.f);
+                W.sid[si] = di;
+            }
+            const int pi = base + wave_push(&s_push[1], pushProbe);
+            if (pushProbe) {
+                X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
+                X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
+                X.pid[pi] = di;
+            }
+        }
+        if (cont2) {
+            // BSDF sample for the path (PathIntegrator.cpp:80-105): wo is -ray.d here, not the
+            // normalised isect.wo the light estimate uses
+            const f3 woPath = -ray.d;
+            f3 wi = mk(0, 0, 0);
+            float pdf = 0;
+            int flags = 0;
+            float u0, u1;
+            get2d<true>(P.smp, st, &u0, &u1);
+            rgb f = bsdf_sample<LOBES>(bsdf, woPath, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
+            if (!(black(f) || pdf == 0.f)) {
+                beta = beta * (f * absdot(wi, isect.sn) / pdf);
+                specularBounce = (flags & BSDF_SPECULAR) != 0;
+                if ((flags & BSDF_SPECULAR) && (flags & BSDF_TRANSMISSION)) {
+                    float eta = bsdf.mt->eta;
+                    etaScale *= (dot(woPath, isect.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                }
+                cont = spawn_ray(isect, wi);
+                bool stop = false;
+                rgb rrBeta = beta * etaScale;
+                if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
+                    float qq = mx((float).05, 1 - maxval(rrBeta));
+                    if (get1d<true>(P.smp, st) < qq) stop = true;
+                    else beta = beta / (1 - qq);
+                }
+                if (!stop) {
+                    pushNext = true;
+                    bounces += 1;
+                }
+            }
+            dim = st.dim;
+        }
+        if (active) {
             if (X.lastLevel) pushNext = false;   // never taken: no bounce is left at the last level
             if (!pushNext) X.stL[id] = make_float4(L.r, L.g, L.b, 0.f);   // the path ends here
         }
@@ -316,27 +352,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
             W.next.s0[ni] = make_float4(L.r, L.g, L.b, beta.r);
             W.next.s1[ni] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
         }
-        const int di = base + wave_push(&s_push[2], pushDirect);
-        if (pushDirect) {
-            X.dA[di] = make_float4(A.r, A.g, A.b, pmfD);
-            X.dB[di] = make_float4(fB.r, fB.g, fB.b, weightB);
-            X.dBeta[di] = make_float4(betaD.r, betaD.g, betaD.b, scatPdfD);
-            X.dFlags[di] = dflagsD;
-            X.dLight[di] = lightD;
-            X.dTgt[di] = pushNext ? ni : ~id;
-        }
-        const int si = base + wave_push(&s_push[0], pushShadow);
-        if (pushShadow) {
-            W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
-            W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, 0.f);
-            W.sid[si] = di;
-        }
-        const int pi = base + wave_push(&s_push[1], pushProbe);
-        if (pushProbe) {
-            X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
-            X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
-            X.pid[pi] = di;
-        }
+        if (pushDirect) X.dTgt[di] = pushNext ? ni : ~id;
     }
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -78,14 +78,28 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             active = q >= 0;
             if (!active) q = 0;
         }
+        // Two phases around the light-estimate pushes (as k_wfp_shade): the record, the transmittance
+        // walk and the probe ray are written before the path's phase-function / BSDF sample.
         bool pushTr = false, pushProbe = false, pushDirect = false, pushNext = false;
         int id = 0, dim = 0, bounces = 0;
         bool specularBounce = false;
-        Ray shadow, probe, cont;
-        VisPt vis;
-        rgb L, beta, fA, fB, Li, betaD;
-        float etaScale = 1.f, pmfD = 0.f, weightA = 0.f, weightB = 1.f, lightPdf = 0.f, scatPdfD = 0.f;
+        Ray cont, ray;
+        rgb L, beta;
+        float etaScale = 1.f;
         uint32_t sIndex = 0;
+        SState st;
+        st.index = 0; st.sid = 0; st.dim = 0; st.px = st.py = 0;
+        Isect isect, mi;
+        BSDF bsdf;
+        MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+        bool estimate = false, mediumEvent = false;
+        float g = 0;
+        int di = -1;
+        {
+        Ray shadow, probe;
+        VisPt vis;
+        rgb fA, fB, Li;
+        float pmfD = 0.f, weightA = 0.f, weightB = 1.f, lightPdf = 0.f, scatPdfD = 0.f;
         int dflagsD = 0, lightD = 0;
         if (active) {
             float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
@@ -95,7 +109,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             bounces = (dd >> 16) & 0x7f;
             specularBounce = (dd >> 23) & 1;
             const int medium = ((dd >> 24) & 0xff) - 1;
-            Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, medium);
+            ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, medium);
             const int slot = __float_as_int(hr.x);
             const bool found = slot >= 0;
             if (level0) {
@@ -107,12 +121,9 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 etaScale = b.z;
                 sIndex = __float_as_uint(b.w);
             }
-            SState st;
             st.index = sIndex;
             st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
             st.dim = dim;
-            st.px = st.py = 0;
-            Isect isect;
             if (found) {
                 int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
                 if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
@@ -121,9 +132,6 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 set_interface(S, &isect, ray.medium);
             }
             // HomogeneousMedium::Sample (HomogeneousMedium.cpp:15-45)
-            bool mediumEvent = false;
-            Isect mi;
-            float g = 0;
             if (ray.medium >= 0) {
                 const float* md = S.media + 10 * ray.medium;
                 int channel = (int)(get1d<true>(P.smp, st) * 3);
@@ -146,11 +154,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 if (pdf == 0) pdf = 1;
                 beta = beta * (sampled ? (Tr * sp3(md[3], md[4], md[5]) / pdf) : (Tr / pdf));
             }
-            bool alive = !black(beta), doRR = false;
-            BSDF bsdf;
-            MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
+            bool alive = !black(beta);
             const Isect* ip = mediumEvent ? &mi : &isect;
-            bool estimate = false;
             if (alive && mediumEvent) {
                 if (bounces >= P.maxDepth) alive = false;
                 else estimate = true;
@@ -236,13 +241,44 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                     if (dflags & (kWfpAPending | kWfpBPending)) {   // written at its queue position below
                         pmfD = pmf;
                         scatPdfD = scatteringPdf;
-                        betaD = beta;
                         dflagsD = dflags;
                         lightD = li;
                         pushDirect = true;
                     }
                 }
             }
+        }
+            // the estimate's record (beta at the estimate), its transmittance walk and probe ray
+            di = base + wave_push(&s_push[2], pushDirect);
+            if (pushDirect) {
+                X.dA[di] = make_float4(fA.r, fA.g, fA.b, pmfD);
+                V.dLiA[di] = make_float4(Li.r, Li.g, Li.b, lightPdf);
+                V.dWA[di] = weightA;
+                X.dB[di] = make_float4(fB.r, fB.g, fB.b, weightB);
+                X.dBeta[di] = make_float4(beta.r, beta.g, beta.b, scatPdfD);
+                X.dFlags[di] = dflagsD;
+                X.dLight[di] = lightD;
+            }
+            const int ti = base + wave_push(&s_push[0], pushTr);
+            if (pushTr) {
+                V.to[ti] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
+                V.td[ti] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(shadow.medium));
+                if (!V.anyHitTr) {   // the walk's target; one any-hit query needs none of it
+                    V.tp[ti] = make_float4(vis.p.x, vis.p.y, vis.p.z, 0.f);
+                    V.te[ti] = make_float4(vis.pError.x, vis.pError.y, vis.pError.z, 0.f);
+                    V.tn[ti] = make_float4(vis.n.x, vis.n.y, vis.n.z, 0.f);
+                }
+                V.tid[ti] = di;
+            }
+            const int pi = base + wave_push(&s_push[1], pushProbe);
+            if (pushProbe) {
+                X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
+                X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
+                X.pid[pi] = di;
+            }
+        }
+        if (active) {
+            bool doRR = false;
             if (estimate) {
                 if (mediumEvent) {   // HenyeyGreenstein::Sample_p, then the ray leaves the interaction
                     f3 wo = -ray.d, wi;
@@ -297,32 +333,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             W.next.s0[ni] = make_float4(L.r, L.g, L.b, beta.r);
             W.next.s1[ni] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
         }
-        const int di = base + wave_push(&s_push[2], pushDirect);
-        if (pushDirect) {
-            X.dA[di] = make_float4(fA.r, fA.g, fA.b, pmfD);
-            V.dLiA[di] = make_float4(Li.r, Li.g, Li.b, lightPdf);
-            V.dWA[di] = weightA;
-            X.dB[di] = make_float4(fB.r, fB.g, fB.b, weightB);
-            X.dBeta[di] = make_float4(betaD.r, betaD.g, betaD.b, scatPdfD);
-            X.dFlags[di] = dflagsD;
-            X.dLight[di] = lightD;
-            X.dTgt[di] = pushNext ? ni : ~id;
-        }
-        const int ti = base + wave_push(&s_push[0], pushTr);
-        if (pushTr) {
-            V.to[ti] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
-            V.td[ti] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(shadow.medium));
-            V.tp[ti] = make_float4(vis.p.x, vis.p.y, vis.p.z, 0.f);
-            V.te[ti] = make_float4(vis.pError.x, vis.pError.y, vis.pError.z, 0.f);
-            V.tn[ti] = make_float4(vis.n.x, vis.n.y, vis.n.z, 0.f);
-            V.tid[ti] = di;
-        }
-        const int pi = base + wave_push(&s_push[1], pushProbe);
-        if (pushProbe) {
-            X.po[pi] = make_float4(probe.o.x, probe.o.y, probe.o.z, probe.tMax);
-            X.pd[pi] = make_float4(probe.d.x, probe.d.y, probe.d.z, 0.f);
-            X.pid[pi] = di;
-        }
+        if (pushDirect) X.dTgt[di] = pushNext ? ni : ~id;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
