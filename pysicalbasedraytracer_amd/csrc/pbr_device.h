@@ -945,34 +945,36 @@ PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float
 }
 // ImageTexture::Evaluate (ImageTexture.h:52-60) with zero differentials: MIPMap::triangle(0, st)
 // (MIPMap.h:240-252) on the level-0 texels, Texel's wrap modes (:166-190).
-__device__ __forceinline__ float4 tex_texel(const DeviceScene& S, const TexDev& t, int s, int u) {
+__device__ __forceinline__ float4 tex_texel(const float4* texels, const TexDev& t, int s, int u) {
     if (t.wrap == 0) { s = s % t.w; if (s < 0) s += t.w; u = u % t.h; if (u < 0) u += t.h; }
     else if (t.wrap == 2) { s = clampi(s, 0, t.w - 1); u = clampi(u, 0, t.h - 1); }
     else if (s < 0 || s >= t.w || u < 0 || u >= t.h) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return S.texels[t.offset + (size_t)u * t.w + s];
+    return texels[t.offset + (size_t)u * t.w + s];
 }
-__device__ __forceinline__ float4 tex_lookup(const DeviceScene& S, const TexDev& t, float su, float sv) {
+__device__ __forceinline__ float4 tex_lookup(const float4* texels, const TexDev& t, float su, float sv) {
     const float s = su * t.w - 0.5f, u = sv * t.h - 0.5f;
     const int s0 = (int)floorf(s), u0 = (int)floorf(u);
     const float ds = s - s0, du = u - u0;
     const float w00 = (1 - ds) * (1 - du), w01 = (1 - ds) * du, w10 = ds * (1 - du), w11 = ds * du;
-    const float4 a = tex_texel(S, t, s0, u0), b = tex_texel(S, t, s0, u0 + 1), c = tex_texel(S, t, s0 + 1, u0),
-                 d = tex_texel(S, t, s0 + 1, u0 + 1);
+    const float4 a = tex_texel(texels, t, s0, u0), b = tex_texel(texels, t, s0, u0 + 1), c = tex_texel(texels, t, s0 + 1, u0),
+                 d = tex_texel(texels, t, s0 + 1, u0 + 1);
     return make_float4(w00 * a.x + w01 * b.x + w10 * c.x + w11 * d.x, w00 * a.y + w01 * b.y + w10 * c.y + w11 * d.y,
                        w00 * a.z + w01 * b.z + w10 * c.z + w11 * d.z, 0.f);
 }
 // A textured material's lobes at one hit: its textures evaluated through their UVMapping2D
 // (Texture.cpp:8-14), then the material's ComputeScatteringFunctions (pbr_material.h).  Out of line:
-// the untextured scenes' shading kernels pay no registers for it.
-__device__ __noinline__ void textured_template(const DeviceScene& S, int mat, float u, float v, bool multiLobe,
-                                               MatTemplate* out) {
-    const TexMat& tm = S.texMats[mat];
+// the untextured scenes' shading kernels pay no registers for it.  It takes the three arrays by value:
+// a reference to the kernel's DeviceScene parameter would make the compiler copy the whole parameter
+// block into per-lane scratch and read every parameter from there.
+__device__ __noinline__ void textured_template(const TexMat* texMats, const TexDev* textures, const float4* texels, int mat,
+                                               float u, float v, bool multiLobe, MatTemplate* out) {
+    const TexMat& tm = texMats[mat];
     MatParams p = tm.p;
     for (int k = 0; k < 6; ++k) {
         const int ti = tm.tex[k];
         if (ti < 0) continue;
-        const TexDev& t = S.textures[ti];
-        const float4 val = tex_lookup(S, t, t.su * u + t.du, t.sv * v + t.dv);
+        const TexDev& t = textures[ti];
+        const float4 val = tex_lookup(texels, t, t.su * u + t.du, t.sv * v + t.dv);
         float* dst = k == 0 ? p.Kd : (k == 1 ? p.Ks : (k == 2 ? p.Kr : p.Kt));
         if (k == 4) p.sigma = val.x;
         else if (k == 5) p.roughness = val.x;
@@ -994,7 +996,7 @@ __device__ __forceinline__ bool make_bsdf(const DeviceScene& S, const MatTemplat
     if (!mt->valid) return false;
     if constexpr (TEX) {
         if (mt->textured) {
-            textured_template(S, mat, si.u, si.v, multiLobe, texLocal);
+            textured_template(S.texMats, S.textures, S.texels, mat, si.u, si.v, multiLobe, texLocal);
             mt = texLocal;
         }
     }

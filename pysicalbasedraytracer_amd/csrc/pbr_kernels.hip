@@ -59,8 +59,10 @@ __shared__ uint4 s_halton_tab[kLdsDims];           // prime, floor(2^32/prime), 
 __device__ __forceinline__ int sobol_lds_dims(const DeviceSampler& s) {
     return min(min(s.ldsDims, kLdsSobolDims), s.nSobolDims);
 }
-// Whole workgroup; call before the first LDS sample and follow with __syncthreads().
-__device__ void stage_halton_lds(const DeviceSampler& s) {
+// Whole workgroup; call before the first LDS sample and follow with __syncthreads().  Inlined: an
+// out-of-line call taking the sampler by reference makes the compiler copy the whole by-value kernel
+// parameter block into per-lane scratch and read every parameter back from there.
+__device__ __forceinline__ void stage_halton_lds(const DeviceSampler& s) {
     if (s.type == PBR_SAMPLER_SOBOL) {
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_halton_perm);
         const int n = sobol_lds_dims(s) * kSobolNib;
