@@ -100,6 +100,25 @@ __device__ __forceinline__ int wf_block() {
     }
 }
 
+// The same remap for the resident-size lane-refill traversal grids (5-7 workgroups per CU, so
+// G = 1280-1792): runs of PBR_XCD_TRAV_RUN workgroups per XCD (-1: one contiguous band per XCD,
+// 0: dispatch order).
+#ifndef PBR_XCD_TRAV_RUN
+#define PBR_XCD_TRAV_RUN 0
+#endif
+__device__ __forceinline__ int trav_block() {
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    constexpr int K = PBR_XCD_TRAV_RUN;
+    if constexpr (K == 0) return b;
+    else {
+        if (G % kXcds != 0) return b;
+        const int per = G / kXcds, run = K < 0 ? per : K;
+        if (per % run != 0) return b;
+        const int x = b % kXcds, k = b / kXcds;
+        return ((k / run) * kXcds + x) * run + k % run;
+    }
+}
+
 // LDS counter; the wave's lanes must be converged
 __device__ __forceinline__ int wave_push(int* counter, bool pred) {
     unsigned long long m = __ballot(pred);
@@ -187,7 +206,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
                                 int diagKind = 0) {
     const int lane = (int)__lane_id();
     const int stride = (int)(gridDim.x * blockDim.x);
-    const int wbase = wf_block() * (int)blockDim.x + ((int)threadIdx.x & ~63);
+    const int wbase = trav_block() * (int)blockDim.x + ((int)threadIdx.x & ~63);
     auto rayOf = [&](int j) { return (j >> 6) * stride + wbase + (j & 63); };   // increasing in j
     const unsigned long long below = (1ull << lane) - 1ull;
     int* lref;
