@@ -417,7 +417,12 @@ constexpr int kMicroLobes = (1 << L_LAMBERT) | (1 << L_MF_R) | (1 << L_MF_T);
 constexpr int kLdsMats = 32;
 __shared__ MatTemplate s_mats[kLdsMats];
 
-template <int LOBES, bool MATS_LDS, int OCC = (LOBES & ~kSimpleLobes) ? 2 : 4>
+// Waves per SIMD of the Whitted shade kernel for the simple lobe set (C2).  Measured (C2 ms):
+// round 1 4: 19.97, 3: 20.16, 5: 20.11; round 3 4: 17.91-18.02, 3: 18.64, 5: 18.55.
+#ifndef PBR_WF_SHADE_OCC
+#define PBR_WF_SHADE_OCC 4
+#endif
+template <int LOBES, bool MATS_LDS, int OCC = (LOBES & ~kSimpleLobes) ? 2 : PBR_WF_SHADE_OCC>
 __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     const KParams& P = W.P;
     const DeviceScene& S = P.S;
