@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
         uint32_t sIndex = 0;
         SState st;
         st.index = 0; st.sid = 0; st.dim = 0; st.px = st.py = 0;
-        Isect isect, mi;
+        Isect isect;   // the surface hit, or the medium interaction once one is sampled
         BSDF bsdf;
         MatTemplate texLocal;   // a textured material's per-hit lobes (make_bsdf)
         bool estimate = false, mediumEvent = false;
@@ -140,9 +140,11 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 float t = mn(dist / len(ray.d), ray.tMax);
                 bool sampled = t < ray.tMax;
                 if (sampled) {
-                    mi.p = ray.o + ray.d * t; mi.wo = -ray.d; mi.n = mk(0, 0, 0); mi.pError = mk(0, 0, 0);
-                    mi.sn = mk(0, 0, 0); mi.dpdu = mk(0, 0, 0);
-                    mi.medIn = mi.medOut = ray.medium; mi.slot = -1;
+                    // MediumInteraction: it replaces the surface record, which a medium event never
+                    // reads again (one record, no pointer select between two: that kept both in scratch)
+                    isect.p = ray.o + ray.d * t; isect.wo = -ray.d; isect.n = mk(0, 0, 0); isect.pError = mk(0, 0, 0);
+                    isect.sn = mk(0, 0, 0); isect.dpdu = mk(0, 0, 0);
+                    isect.medIn = isect.medOut = ray.medium; isect.slot = -1;
                     g = md[9];
                     mediumEvent = true;
                 }
@@ -155,7 +157,6 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 beta = beta * (sampled ? (Tr * sp3(md[3], md[4], md[5]) / pdf) : (Tr / pdf));
             }
             bool alive = !black(beta);
-            const Isect* ip = mediumEvent ? &mi : &isect;
             if (alive && mediumEvent) {
                 if (bounces >= P.maxDepth) alive = false;
                 else estimate = true;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             }
             if (estimate && S.nLights > 0) {
                 // UniformSampleOneLight(handleMedia = true) / EstimateDirect
-                const Isect& ref = *ip;
+                const Isect& ref = isect;
                 float pmf;
                 const int li = sample_light(S, get1d<true>(P.smp, st), &pmf);
                 if (pmf != 0) {
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                     float u0, u1;
                     get2d<true>(P.smp, st, &u0, &u1);
                     hg_sample(g, wo, &wi, u0, u1);
-                    cont = spawn_ray(mi, wi);
+                    cont = spawn_ray(isect, wi);
                     specularBounce = false;
                     doRR = true;
                 } else {
