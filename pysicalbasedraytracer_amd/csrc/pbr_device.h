@@ -486,6 +486,165 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
     return found;
 }
 
+// Wave-packet traversal of the quad layout for coherent waves (a camera wave holds one pixel's
+// sub-pixel rays; a flat mirror keeps them together).  The wave walks ONE node at a time with a
+// wave-uniform stack in LDS; each lane tests the node's four slots against its own ray, and the
+// wave enters the first slot (in visit order) that any lane passes, pushing the later ones that
+// some lane passes.  Per lane this is traverse_quad exactly:
+//   * the visit order of a quad node's slots depends only on the ray's direction signs on the
+//     node's split axes; the caller takes this path only when every live lane has the same three
+//     signs (closest hit — any hit keeps build order, which depends on nothing), so the order is
+//     wave-uniform;
+//   * a lane is `active` at the wave's current node iff its own traversal would enter it: it passed
+//     that slot's test (entered now, or on a pop) — inactive lanes test nothing there;
+//   * a stack entry is (parent node, slot column) plus the ballot of the lanes that pushed it; on a
+//     pop each of those lanes re-derives the slot's slab (the same float operations on the same
+//     box, so the same tEnter) and tests it against its current tMax — what traverse_quad's pop
+//     test computes from the stored tEnter.
+// So every lane runs its own primitive tests in BVHAccel's order with its own tMax (F8 ties
+// unchanged), while node and triangle fetches are scalar (one per wave), the stack costs no
+// per-lane memory and control flow is wave-uniform.  The stack is 64 entries per wave, like the
+// per-lane one.
+constexpr int kPacketStack = 64;
+__shared__ int s_pk_ref[4][kPacketStack];                  // parent quad node << 2 | slot column
+__shared__ unsigned long long s_pk_mask[4][kPacketStack];  // lanes that pushed the entry
+#ifndef PBR_PACKET
+#define PBR_PACKET 1
+#endif
+constexpr bool kPacket = PBR_PACKET != 0;
+#ifndef PBR_PACKET_EXTEND
+#define PBR_PACKET_EXTEND 1
+#endif
+template <bool ANY>
+__device__ bool traverse_packet(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, bool n0, bool n1, bool n2, bool alive,
+                                int u0, int u1, int u2) {
+    const int wv = (int)(threadIdx.x >> 6);
+    int* sref = s_pk_ref[wv];
+    unsigned long long* smask = s_pk_mask[wv];
+    const unsigned long long lanebit = 1ull << __lane_id();
+    int sp = 0;
+    bool found = false;
+    int cur = S.quadRootRef;
+    bool active = alive;
+    // closest hit: the live lanes' common signs, wave-uniform, so the near/far plane selects of the
+    // slab tests are scalar (any hit: each lane's own signs)
+    if constexpr (!ANY) { n0 = u0 != 0; n1 = u1 != 0; n2 = u2 != 0; }
+    while (true) {
+        if (cur < 0) {   // leaf: the active lanes test its primitives in slot order
+            if (active) {
+                int slot = cur & 0x7fffffff;
+                while (true) {
+                    const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)slot);
+                    const float4 v0 = as_f4(tv[0]), v1 = as_f4(tv[1]), v2 = as_f4(tv[2]);
+                    const int flags = __float_as_int(v0.w);
+                    float t, b0 = 0, b1 = 0, b2 = 0;
+                    const bool hit = (flags & PRIM_SPHERE)
+                                         ? sphere_test(S.spheres[__float_as_int(v0.x)], r, &t)
+                                         : tri_test(mk(v0.x, v0.y, v0.z), mk(v1.x, v1.y, v1.z), mk(v2.x, v2.y, v2.z), r, &t, &b0, &b1, &b2);
+                    if (hit) {
+                        found = true;
+                        if (ANY) { alive = false; active = false; break; }
+                        r.tMax = t;   // GeometricPrimitive::Intersect (Primitive.cpp:26)
+                        h->slot = slot; h->b0 = b0; h->b1 = b1; h->b2 = b2;
+                    }
+                    if (flags & PRIM_LEAF_END) break;
+                    ++slot;
+                }
+            }
+            if (ANY && __builtin_amdgcn_ballot_w64(alive) == 0ull) break;
+        } else {
+            const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)cur);
+            const float4 LX = as_f4(w[0]), LY = as_f4(w[1]), LZ = as_f4(w[2]), HX = as_f4(w[3]), HY = as_f4(w[4]),
+                         HZ = as_f4(w[5]), R = as_f4(w[6]);
+            const int meta = __float_as_int(w[7].x);
+            float t[4] = {0.f, 0.f, 0.f, 0.f};
+            bool p[4];
+            p[0] = active && node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t[0]) && ((meta >> 8) & 1) && t[0] < r.tMax;
+            p[1] = active && node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t[1]) && ((meta >> 9) & 1) && t[1] < r.tMax;
+            p[2] = active && node_slab(mk(LX.z, LY.z, LZ.z), mk(HX.z, HY.z, HZ.z), r, inv, n0, n1, n2, &t[2]) && ((meta >> 10) & 1) && t[2] < r.tMax;
+            p[3] = active && node_slab(mk(LX.w, LY.w, LZ.w), mk(HX.w, HY.w, HZ.w), r, inv, n0, n1, n2, &t[3]) && ((meta >> 11) & 1) && t[3] < r.tMax;
+            const unsigned long long bm[4] = {__builtin_amdgcn_ballot_w64(p[0]), __builtin_amdgcn_ballot_w64(p[1]),
+                                              __builtin_amdgcn_ballot_w64(p[2]), __builtin_amdgcn_ballot_w64(p[3])};
+            // visit position → slot column (quad_slots' swaps; any hit: build order)
+            int col[4] = {0, 1, 2, 3};
+            if constexpr (!ANY) {
+                // the live lanes' common direction signs (u0, u1, u2) on the three split axes
+                const int aN = meta & 3, aA = (meta >> 2) & 3, aB = (meta >> 4) & 3;
+                const int sN = aN == 0 ? u0 : (aN == 1 ? u1 : u2);
+                const int sA = aA == 0 ? u0 : (aA == 1 ? u1 : u2);
+                const int sB = aB == 0 ? u0 : (aB == 1 ? u1 : u2);
+                for (int pos = 0; pos < 4; ++pos) {
+                    const int hi = (pos >> 1) ^ sN;
+                    col[pos] = hi * 2 + ((pos & 1) ^ (hi == 0 ? sA : sB));
+                }
+            }
+            int first = -1;
+            for (int pos = 0; pos < 4; ++pos)
+                if (first < 0 && bm[col[pos]] != 0ull) first = pos;
+            if (first >= 0 && sp <= kPacketStack - 3) {
+                for (int pos = 3; pos > first; --pos)
+                    if (bm[col[pos]] != 0ull) {
+                        sref[sp] = (cur << 2) | col[pos];   // every lane stores the same values
+                        smask[sp] = bm[col[pos]];
+                        ++sp;
+                    }
+                const int c = col[first];
+                active = c == 0 ? p[0] : (c == 1 ? p[1] : (c == 2 ? p[2] : p[3]));
+                cur = __float_as_int(c == 0 ? R.x : (c == 1 ? R.y : (c == 2 ? R.z : R.w)));
+                cur = __builtin_amdgcn_readfirstlane(cur);
+                continue;
+            }
+        }
+        // pop until some lane that pushed an entry passes its re-derived test against its tMax
+        bool more = false;
+        while (sp > 0) {
+            --sp;
+            const int e = __builtin_amdgcn_readfirstlane(sref[sp]);
+            const unsigned long long m = smask[sp];   // a uniform LDS address: the same value in every lane
+            const int parent = e >> 2, c = e & 3;
+            const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)parent);
+            const float4 LX = as_f4(w[0]), LY = as_f4(w[1]), LZ = as_f4(w[2]), HX = as_f4(w[3]), HY = as_f4(w[4]),
+                         HZ = as_f4(w[5]), R = as_f4(w[6]);
+            auto pick = [c](float4 v) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
+            float tt = 0.f;
+            bool a = (m & lanebit) != 0ull && (!ANY || alive);
+            a = a && node_slab(mk(pick(LX), pick(LY), pick(LZ)), mk(pick(HX), pick(HY), pick(HZ)), r, inv, n0, n1, n2, &tt) && tt < r.tMax;
+            if (__builtin_amdgcn_ballot_w64(a) != 0ull) {
+                active = a;
+                cur = __builtin_amdgcn_readfirstlane(__float_as_int(pick(R)));
+                more = true;
+                break;
+            }
+        }
+        if (!more) break;
+    }
+    return found;
+}
+
+// traverse() for a whole wave as packet walks.  Closest hit: one walk per direction-sign class
+// (octant) present among the live lanes — a camera wave inside one pixel nearly always holds one;
+// each lane takes part in its own class's walk only, so its result is its own traversal's.  Any
+// hit: one walk (build order).  Every lane of the wave that is still running must call it (`live`
+// = the lane has a ray).  No per-lane stack: the kernels that use it need no scratch for one.
+template <bool ANY>
+__device__ bool traverse_wave(const DeviceScene& S, Ray& r, HitRec* h, bool live) {
+    f3 inv = ANY ? mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z) : mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
+    bool n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
+    const bool ok = live && S.nNodes > 0 && node_hit(S.nodes[0], S.nodes[1], r, inv, n0, n1, n2);   // the root first
+    unsigned long long left = __builtin_amdgcn_ballot_w64(ok);
+    if constexpr (ANY) return left ? traverse_packet<true>(S, r, h, inv, n0, n1, n2, ok, 0, 0, 0) : false;
+    const int cls = (int)n0 | ((int)n1 << 1) | ((int)n2 << 2);
+    bool found = false;
+    while (left) {
+        const int c = __builtin_amdgcn_readlane(cls, __ffsll((long long)left) - 1);
+        const bool mine = ok && cls == c;
+        left &= ~__builtin_amdgcn_ballot_w64(mine);
+        const bool f = traverse_packet<false>(S, r, h, inv, n0, n1, n2, mine, c & 1, (c >> 1) & 1, (c >> 2) & 1);
+        if (mine) found = f;
+    }
+    return found;
+}
+
 // BVHAccel::Intersect / IntersectP (BVHAccel.cpp:285-366) over the wide layout of
 // build_wide_nodes.  The reference pops a node and tests its box against the current ray.tMax;
 // since only the last comparison of that test reads ray.tMax (Geometry.h:1438-1468), the slab part

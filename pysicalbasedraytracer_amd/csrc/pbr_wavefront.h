@@ -355,7 +355,13 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_camera_extend(WfParams
     Ray r = camera_sample_ray(P, st, x, y);
     HitRec h;
     Counters c;
-    bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
+    bool hit;
+    if constexpr (kPacket && kQuadTraversal) {   // a wave holds one pixel's samples: coherent
+        h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
+        hit = traverse_wave<false>(P.S, r, &h, true);
+    } else {
+        hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
+    }
     trav_diag(W.prof, KP_WF_CAMERA, h);
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(st.dim, 0)));
@@ -395,7 +401,13 @@ __global__ __launch_bounds__(256, REFILL ? PBR_REFILL_OCC : PBR_TRAV_OCC) void k
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
         Counters c;
-        bool hit = traverse<false, false, SHORT>(W.P.S, r, &h, &c);
+        bool hit;
+        if constexpr (kPacket && PBR_PACKET_EXTEND && kQuadTraversal) {   // Whitted's mirror continuations stay coherent
+            h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
+            hit = traverse_wave<false>(W.P.S, r, &h, true);
+        } else {
+            hit = traverse<false, false, SHORT>(W.P.S, r, &h, &c);
+        }
         trav_diag(W.prof, KP_WF_EXTEND, h);
         // the whole 16-B origin record is rewritten with the hit distance: full-line stores.  Measured
         // (bit-identical; C3 / C5 / C2 frame ms): o.w alone 325 / 1642 / 17.66, the whole record

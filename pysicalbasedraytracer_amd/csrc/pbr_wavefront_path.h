@@ -66,7 +66,13 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
     Ray r = camera_sample_ray(P, st, x, y);
     HitRec h;
     Counters c;
-    bool hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
+    bool hit;
+    if constexpr (kPacket && kQuadTraversal) {   // a wave holds (part of) one pixel's samples
+        h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
+        hit = traverse_wave<false>(P.S, r, &h, true);
+    } else {
+        hit = traverse<false, false, SHORT>(P.S, r, &h, &c);
+    }
     trav_diag(W.prof, KP_WFP_CAMERA, h);
     W.cur.o[q] = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
     W.cur.d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_path(st.dim, 0, false)));
