@@ -827,6 +827,7 @@ struct pbr_hip_ctx {
     // per-kernel profile (pbr_hip_set_profiling): a HIP event pair around every launch, on the
     // launch's stream, and the work counters of each kernel family (device rows + host-known counts)
     bool profOn = false, profCount = false;
+    bool wfFused = false;                // the last Whitted frame traced in its shade kernels (profile bytes)
     struct ProfEv { int kind; hipEvent_t a, b; };
     std::vector<ProfEv> profEv;
     size_t profUsed = 0;
@@ -1024,6 +1025,12 @@ int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
 }
 
 
+// PBR_LOBE_SETS=0: no Lambert + mirror specialisation of the shading kernels (A/B switch)
+bool lobe_set_switch() {
+    const char* e = getenv("PBR_LOBE_SETS");
+    return !(e && e[0] == '0');
+}
+
 // Chunking of the wavefront schedules: at most 2^chunkLog2 samples per chunk; chunks alternate
 // over the lanes.  Measured on C2: two lanes 23.4 ms vs 24.9 for one; forcing a one-chunk
 // (1/8-frame shard) frame into two concurrent half chunks was slower (4.00 vs 3.86 ms).
@@ -1151,12 +1158,21 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const size_t sqcap = qcap * (size_t)lightsPerShade;   // shadow-queue entries
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
+    const bool mm = (lobes & ~kMatteMirrorLobes) == 0 && lobe_set_switch();   // Lambert + mirror only (C2)
     const bool textured = (lobes & kTexturedLobes) != 0;
     // tuning switches (results are bit-identical either way): LDS short stack, shade occupancy
     const char* eStack = getenv("PBR_SHORT_STACK");
     const bool shortStack = !(eStack && eStack[0] == '0');
     const char* eMats = getenv("PBR_MATS_LDS");
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
+    // the level-0 shade traces its own camera rays (PBR_FUSED_CAMERA=0: the camera kernel + queue)
+    const char* eFuse = getenv("PBR_FUSED_CAMERA");
+    // Frames of one chunk (a quarter- or eighth-frame rank shard) keep the separate kernels: there the
+    // camera kernel's 8 waves per SIMD and the extend launch's overlap with the shadow rays win
+    // (C2 shard 0/8 2.71 → 2.97 ms fused; PBR_FUSED_CAMERA=2 fuses them too).
+    const bool fuseCamera = kPacket && kQuadTraversal && !(eFuse && eFuse[0] == '0') && (mm || simple) && matsLds &&
+                            !textured && !ml && (ch.chunkPix < P.nPixels || (eFuse && eFuse[0] == '2'));
+    ctx->wfFused = fuseCamera;
     // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
     const int maxLevels = levels;   // no material-less primitives here (those scenes run the megakernel)
     // Shadow rays of level L run on a second stream, overlapping extend(L+1) and shade(L+1) (they
@@ -1238,9 +1254,11 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         W.nSamples = W.chunkPix * spp;
         int cur = 0;
         W.cur = queue(l, 0);
-        PROF_LAUNCH(KP_WF_CAMERA, st,
-            if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kCameraShort>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
-            else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, st, W));
+        if (!fuseCamera) {
+            PROF_LAUNCH(KP_WF_CAMERA, st,
+                if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kCameraShort>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
+                else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, st, W));
+        }
         prof_host(ctx, KP_WF_CAMERA, 0, (unsigned long long)W.nSamples);
         const hipStream_t sst = shadowOverlap ? ctx->shadowStream[l] : st;
         WfBufs& B = ctx->wb[l];
@@ -1265,7 +1283,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 else if (simple) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
                 else if (matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, true>), gstride, blk, 0, st, W, l0);
                 else hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, false>), gstride, blk, 0, st, W, l0);
-            } else if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
+            } else if (fuseCamera && l0 && mm) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
+            else if (fuseCamera && l0) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
+            else if (mm && matsLds) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true>), gstride, blk, 0, st, W, l0);
+            else if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
             else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, st, W, l0);
             else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, st, W, l0));
@@ -1311,9 +1332,12 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
     const bool micro = (lobes & ~kMicroLobes) == 0;   // Lambert + microfacet reflection/transmission (C4, C5)
+    const bool mm = (lobes & ~kMatteMirrorLobes) == 0 && lobe_set_switch();   // Lambert + mirror only (C3)
     const bool textured = (lobes & kTexturedLobes) != 0;
     const char* eMats = getenv("PBR_MATS_LDS");
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
+    // (the level-0 shade tracing its own camera rays, as Whitted's does, measured slower here: C3
+    // 254 → 268-271 ms, C4 6575 → 6702 ms at 3 shading waves per SIMD; profiles/r3_fused_ab.log)
     WfvParams VL[kWfLanes];
     int* cntL[kWfLanes];
     for (int l = 0; l < ch.lanes; ++l) {
@@ -1417,6 +1441,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
             } else {
                 PROF_LAUNCH(KP_WFP_SHADE, st,
                     if (textured) hipLaunchKernelGGL((k_wfp_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, X, l0);
+                    else if (mm && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true>), gshade, blk, 0, st, X, l0);
                     else if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
                     else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0);
                     else if (micro && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMicroLobes, true>), gshade, blk, 0, st, X, l0);
@@ -1981,7 +2006,10 @@ int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int*
         const unsigned long long* f = c[k];
         switch (k) {
         case KP_WF_CAMERA: return 52 * f[0];                                   // o, d, hit, index
-        case KP_WF_SHADE: return 72 * f[0] + 4 * f[5] + 52 * f[1] + 52 * f[4]; // ray + index + recA + depth; shadow; next + recF/P
+        case KP_WF_SHADE:   // ray + hit + index + recA + depth; shadow; next + recF/P
+            // (fused: level 0 reads no ray, hit or index; it writes the index, 4 B)
+            if (ctx->wfFused) return 72 * f[0] - 48 * c[KP_WF_CAMERA][0] + 4 * f[5] + 52 * f[1] + 52 * f[4];
+            return 72 * f[0] + 4 * f[5] + 52 * f[1] + 52 * f[4];
         case KP_WF_SHADOW: return 52 * f[0] + 32 * f[1];                       // o, d, contribution, id; recA RMW
         case KP_WF_EXTEND: return 64 * f[0];                                   // o, d read; o, hit written
         case KP_WF_FINISH: return 16 * f[0] + 4 * f[1] + 16 * c[KP_WF_SHADE][0] + 20 * c[KP_WF_SHADE][4];

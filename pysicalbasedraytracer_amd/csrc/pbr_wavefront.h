@@ -424,6 +424,9 @@ constexpr int kSimpleLobes = (1 << L_LAMBERT) | (1 << L_OREN) | (1 << L_SPEC_R) 
 // Lambert and rough (microfacet) reflection / transmission only — matte, plastic, metal and rough
 // glass: the Path/VolPath shading kernels for C4 and C5 without the specular and Oren-Nayar code
 constexpr int kMicroLobes = (1 << L_LAMBERT) | (1 << L_MF_R) | (1 << L_MF_T);
+// Lambert and perfect mirror reflection only — matte (σ = 0) and mirror materials: C2's dragon and
+// floor, C3's scene
+constexpr int kMatteMirrorLobes = (1 << L_LAMBERT) | (1 << L_SPEC_R);
 // MATS_LDS: the material templates fit kLdsMats and are read from an LDS copy (the BSDF code walks
 // them with dependent loads).
 constexpr int kLdsMats = 32;
@@ -434,7 +437,56 @@ __shared__ MatTemplate s_mats[kLdsMats];
 #ifndef PBR_WF_SHADE_OCC
 #define PBR_WF_SHADE_OCC 4
 #endif
-template <int LOBES, bool MATS_LDS, int OCC = (LOBES & ~kSimpleLobes) ? 2 : PBR_WF_SHADE_OCC>
+#ifndef PBR_WF_SHADE_OCC_MM
+#define PBR_WF_SHADE_OCC_MM PBR_WF_SHADE_OCC
+#endif
+#ifndef PBR_WF_FUSED_OCC
+#define PBR_WF_FUSED_OCC PBR_WF_SHADE_OCC
+#endif
+// k_wf_camera_extend's work for queue position q inside the level-0 shade (CAMERA): the camera
+// sample's ray and its closest hit, as the queue entry the shade would have read.  Every lane of
+// the wave calls it (the packet walk is wave-wide); `active` lanes hold a sample.
+__device__ __forceinline__ void camera_trace(const WfParams& W, bool active, int q, float4* o, float4* d, float4* hr,
+                                             uint32_t* index) {
+    const KParams& P = W.P;
+    Ray r;
+    r.o = mk(0, 0, 0); r.d = mk(0, 0, 1); r.tMax = 0; r.medium = -1;
+    int dim = 0;
+    if (active) {
+        const int lp = q / P.spp, s = q - lp * P.spp;
+        int x, y;
+        pixel_xy(P, W.chunkPix0 + lp, &x, &y);
+        SState st;
+        st.index = sample_index(P.smp, x, y, s).lo;
+        st.sid = s;
+        st.dim = 0;
+        st.px = x;
+        st.py = y;
+        r = camera_sample_ray(P, st, x, y);
+        dim = st.dim;
+        *index = st.index;
+        W.sampleIndex[q] = st.index;   // later levels read it by sample id
+        if (W.initRecords) {
+            W.depthOf[q] = 0;
+            W.recA[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    HitRec h;
+    h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
+    const bool hit = traverse_wave<false>(P.S, r, &h, active);
+    *o = make_float4(r.o.x, r.o.y, r.o.z, r.tMax);
+    *d = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(pack_dd(dim, 0)));
+    *hr = make_float4(__int_as_float(hit ? h.slot : -1), h.b0, h.b1, h.b2);
+}
+
+// CAMERA (level 0 only): the shade generates and traces its camera rays itself — the camera
+// kernel's 52-B queue entry is neither written nor read back, and the chunk has one launch fewer.
+// The walk is the camera kernel's wave packet.  Measured (bit-identical, C2 frame ms): 17.33-17.39
+// → 17.18 (profiles/r3_fused_ab.log).  Tracing the continuations inside the later shades as well
+// (no extend launch) was slower: 17.46.
+template <int LOBES, bool MATS_LDS,
+          int OCC = (LOBES & ~kSimpleLobes) ? 2 : (LOBES == kMatteMirrorLobes ? PBR_WF_SHADE_OCC_MM : PBR_WF_SHADE_OCC),
+          bool CAMERA = false>
 __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     const KParams& P = W.P;
     const DeviceScene& S = P.S;
@@ -463,8 +515,11 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
         int id = 0, depth = 0, dim = 0, emitDepth = 0;
         Ray ray, shadow, cont;
         rgb contrib = sp(0.f);
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f), d = o, hr = o;
+        uint32_t camIndex = 0;
+        if constexpr (CAMERA) camera_trace(W, active, q, &o, &d, &hr, &camIndex);   // level 0 only
+        else if (active) { o = W.cur.o[q]; d = W.cur.d[q]; hr = W.cur.hit[q]; }
         if (active) {
-            float4 o = W.cur.o[q], d = W.cur.d[q], hr = W.cur.hit[q];
             id = level0 ? q : W.cur.id[q];
             int dd = __float_as_int(d.w);
             dim = dd & 0xffff;
@@ -495,7 +550,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                     rgb L = sp(0.f);
                     L = L + si_Le(S, isect, wo);
                     SState st;
-                    st.index = W.sampleIndex[id];
+                    st.index = CAMERA ? camIndex : W.sampleIndex[id];
                     st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
                     st.dim = dim;
                     st.px = st.py = 0;   // dims >= 2 only past the camera

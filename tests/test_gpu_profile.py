@@ -19,8 +19,11 @@ def _c2_small():
 
 
 @pytest.mark.gpu
-def test_whitted_profile_counts_are_consistent(hip, monkeypatch):
-    monkeypatch.setenv("PBR_CHUNK_LOG2", "16")   # several chunks over both lanes
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_whitted_profile_counts_are_consistent(hip, monkeypatch, fused):
+    monkeypatch.setenv("PBR_CHUNK_LOG2", "16")   # several chunks over the lanes
+    # fused: the level-0 shade traces its own camera rays (multi-chunk frames, the default)
+    monkeypatch.setenv("PBR_FUSED_CAMERA", fused)
     s, rd = _c2_small()
     hip.upload(s)
     ref, ref8, _ = hip.render(rd)
@@ -30,11 +33,14 @@ def test_whitted_profile_counts_are_consistent(hip, monkeypatch):
     hip.set_profiling(0)
     assert np.array_equal(g, ref) and np.array_equal(g8, ref8)   # profiling changes nothing
     n = 192 * 108 * 16
-    cam, shade, shadow, extend, fin = (prof[k] for k in ("k_wf_camera_extend", "k_wf_shade", "k_wf_shadow",
-                                                         "k_wf_extend", "k_wf_finish"))
-    assert cam["units"] == n and fin["units"] == 192 * 108 and fin["counts"][1] == n
-    assert cam["launches"] == fin["launches"] > 1
-    assert shade["launches"] == cam["launches"] * rd.max_depth == shadow["launches"]
+    shade, shadow, extend, fin = (prof[k] for k in ("k_wf_shade", "k_wf_shadow", "k_wf_extend", "k_wf_finish"))
+    assert fin["units"] == 192 * 108 and fin["counts"][1] == n and fin["launches"] > 1
+    if fused == "0":
+        cam = prof["k_wf_camera_extend"]
+        assert cam["units"] == n and cam["launches"] == fin["launches"]
+    else:
+        assert "k_wf_camera_extend" not in prof
+    assert shade["launches"] == fin["launches"] * rd.max_depth == shadow["launches"]
     # shade's level-0 input is every sample; deeper levels read what the previous level pushed
     assert shade["units"] == n + extend["units"]
     assert shadow["units"] == shade["counts"][1] and 0 < shadow["counts"][1] <= shadow["units"]
