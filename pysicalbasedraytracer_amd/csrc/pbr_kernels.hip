@@ -1167,11 +1167,12 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
     // the level-0 shade traces its own camera rays (PBR_FUSED_CAMERA=0: the camera kernel + queue)
     const char* eFuse = getenv("PBR_FUSED_CAMERA");
-    // Frames of one chunk (a quarter- or eighth-frame rank shard) keep the separate kernels: there the
-    // camera kernel's 8 waves per SIMD and the extend launch's overlap with the shadow rays win
-    // (C2 shard 0/8 2.71 → 2.97 ms fused; PBR_FUSED_CAMERA=2 fuses them too).
+    // Frames with fewer chunks than lanes (rank shards of a multi-GPU C2 job) keep the separate
+    // kernels: there the camera kernel's 8 waves per SIMD win (C2 shard 0/8, one chunk: 2.58 → 3.10
+    // ms fused; shard 0/2, two chunks: 9.58-9.63 → 10.12-10.22).  PBR_FUSED_CAMERA=2 fuses them too.
+    const long long nChunks = (P.nPixels + ch.chunkPix - 1) / ch.chunkPix;
     const bool fuseCamera = kPacket && kQuadTraversal && !(eFuse && eFuse[0] == '0') && (mm || simple) && matsLds &&
-                            !textured && !ml && (ch.chunkPix < P.nPixels || (eFuse && eFuse[0] == '2'));
+                            !textured && !ml && (nChunks >= std::max(2, ch.lanes) || (eFuse && eFuse[0] == '2'));
     ctx->wfFused = fuseCamera;
     // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
     const int maxLevels = levels;   // no material-less primitives here (those scenes run the megakernel)

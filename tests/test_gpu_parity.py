@@ -260,6 +260,23 @@ def test_wavefront_equals_megakernel(hip, monkeypatch):
     assert np.array_equal(wf8, mk8)
 
 
+def test_fused_level0_shade_equals_camera_kernel(hip, monkeypatch):
+    """The level-0 shade that traces its own camera rays (multi-chunk frames) = the camera kernel
+    + level-0 queue = the megakernel, bit for bit.  64 spp: a camera wave is one pixel's samples;
+    the centre column's pixels hold rays of two direction-sign octants (two packet walks)."""
+    s, rd = scenes.config_c2(160, 90, 64, mesh=small_dragon(64))
+    hip.upload(s)
+    monkeypatch.setenv("PBR_CHUNK_LOG2", "17")   # 8 chunks over the lanes: the fused schedule
+    monkeypatch.setenv("PBR_FUSED_CAMERA", "1")
+    fu, fu8, _ = hip.render(rd)
+    monkeypatch.setenv("PBR_FUSED_CAMERA", "0")
+    ck, ck8, _ = hip.render(rd)
+    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    mk, mk8, _ = hip.render(rd)
+    assert np.array_equal(fu.view(np.uint32), ck.view(np.uint32)) and np.array_equal(fu8, ck8)
+    assert np.array_equal(fu.view(np.uint32), mk.view(np.uint32)) and np.array_equal(fu8, mk8)
+
+
 SOBOL = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "sobol_kats.json")))
 
 
