@@ -10,12 +10,19 @@ runs on a communication stream while frame k+1 renders into the other of two out
 Measurement windows (all after the warm-up frames):
   1. the timed region: K frames back to back, barrier + synchronize on both sides → `value`;
   2. K more frames with a HIP event pair around every kernel launch, on the stream it runs on
-     (pbr_hip_set_profiling(1)) → per-kernel-family launch durations;
+     (pbr_hip_set_profiling(1)) → per-kernel-family launch durations under the default schedule,
+     where up to three chunk lanes run kernels concurrently (`roofline.kernels_overlapped`);
   3. one frame with work counters (pbr_hip_set_profiling(2)) → units and algorithmic HBM bytes per
-     family (the compulsory queue / record / output bytes of the wavefront design).
-The roofline names the family with the largest summed duration: achieved = its algorithmic bytes
-per launch ÷ its mean launch duration; traffic = rocprofv3 PMC bytes per launch of the same family
+     family (the compulsory queue / record / output bytes of the wavefront design, DESIGN.md §7);
+  4. windows 2-3 again on the SERIAL schedule (pbr_hip_set_schedule serial: every launch on one
+     stream, one after another) → each family's own launch durations (`roofline.kernels`).
+`roofline.frame` is the whole frame of window 1: every family's algorithmic (and PMC) bytes per
+frame over the frame time.  The roofline's top-level fields name the family with the largest
+standalone time per frame: achieved = its algorithmic bytes per launch ÷ its own mean launch
+duration (window 4); traffic = rocprofv3 PMC bytes per launch of the same family
 (profiles/<config>_traffic.json, used only when measured on the very build that is loaded).
+`--serial` runs every window on the serial schedule (the command whose rocprofv3 kernel stats back
+the standalone durations, profiles/r4_*_kernel_stats.csv).
 
 The CPU baseline (rank 0, N=1) runs FIRST, in a child process started before this process touches
 the GPU: the reference itself (oracle/_ref/libpbr_ref.so, its unmodified sources built by
@@ -195,6 +202,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU render for the baseline")
     ap.add_argument("--no-model", action="store_true", help="skip the SURVEY-model counting pass")
+    ap.add_argument("--serial", action="store_true", help="every window on the serial (one-stream) schedule")
     ap.add_argument("--cpu-baseline-worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--threads", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--budget", type=float, default=10.0, help=argparse.SUPPRESS)
@@ -228,6 +236,8 @@ def main():
     npx = sum((t[2] - t[0]) * (t[3] - t[1]) for t in tiles)
 
     r = HipRenderer(local)
+    if args.serial:
+        r.set_schedule(serial=True)
     build_info = r.lib.pbr_hip_build_info().decode()
     t0 = time.time()
     r.upload(scene)
@@ -297,6 +307,21 @@ def main():
     window(1)
     counts = r.get_profile()
     r.set_profiling(0)
+    # 4. the same on the serial schedule: each kernel family's own launch durations
+    if args.serial:
+        timing_s, counts_s, elapsed_s = timing, counts, elapsed_ev
+    else:
+        r.set_schedule(serial=True)
+        render()
+        r.sync()
+        r.set_profiling(1)
+        elapsed_s = window(args.steps)
+        timing_s = r.get_profile()
+        r.set_profiling(2)
+        window(1)
+        counts_s = r.get_profile()
+        r.set_profiling(0)
+        r.set_schedule()
     # SURVEY §8(d) model counts: the instrumented megakernel pass (binary traversal; same tests)
     model = None
     if not args.no_model:
@@ -319,55 +344,66 @@ def main():
 
     if rank == 0:
         pmc, pmc_src = pmc_traffic(args.config, build_info) if world == 1 else (None, "1 GPU only")
-        kernels = {}
-        for fam, tv in timing.items():
-            cv = counts.get(fam, {})
-            lpf = tv["launches"] / args.steps                     # launches per frame
-            avg_ms = tv["ms"] / max(1, tv["launches"])
-            cl = cv.get("launches", 0) or 1
-            alg_launch = cv.get("bytes", 0) / cl                  # algorithmic bytes per launch
-            k = {"launches_per_frame": round(lpf, 2), "ms_per_frame": round(tv["ms"] / args.steps, 3),
-                 "avg_launch_us": round(avg_ms * 1e3, 1), "units_per_frame": cv.get("units"),
-                 "alg_bytes_per_launch": round(alg_launch), "counts_per_frame": cv.get("counts"),
-                 "achieved_gbs": round(alg_launch / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None}
-            k["frac"] = round(k["achieved_gbs"] / HBM_PEAK_GBS, 4) if k["achieved_gbs"] is not None else None
-            if pmc is not None:
-                fb = family_traffic(pmc, fam)
-                if fb is not None and lpf > 0:
-                    k["traffic_per_launch"] = round(fb / lpf)
-                    k["traffic_gbs"] = round(fb / lpf / (avg_ms * 1e-3) / 1e9, 1)
-                    k["traffic_frac"] = round(k["traffic_gbs"] / HBM_PEAK_GBS, 4)
-            kernels[fam] = k
+
+        def families(timing, counts):
+            kernels = {}
+            for fam, tv in timing.items():
+                cv = counts.get(fam, {})
+                lpf = tv["launches"] / args.steps                     # launches per frame
+                avg_ms = tv["ms"] / max(1, tv["launches"])
+                cl = cv.get("launches", 0) or 1
+                alg_launch = cv.get("bytes", 0) / cl                  # algorithmic bytes per launch
+                k = {"launches_per_frame": round(lpf, 2), "ms_per_frame": round(tv["ms"] / args.steps, 3),
+                     "avg_launch_us": round(avg_ms * 1e3, 1), "units_per_frame": cv.get("units"),
+                     "alg_bytes_per_launch": round(alg_launch), "counts_per_frame": cv.get("counts"),
+                     "achieved_gbs": round(alg_launch / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None}
+                k["frac"] = round(k["achieved_gbs"] / HBM_PEAK_GBS, 4) if k["achieved_gbs"] is not None else None
+                if pmc is not None:
+                    fb = family_traffic(pmc, fam)
+                    if fb is not None and lpf > 0:
+                        k["traffic_per_launch"] = round(fb / lpf)
+                        k["traffic_gbs"] = round(fb / lpf / (avg_ms * 1e-3) / 1e9, 1)
+                        k["traffic_frac"] = round(k["traffic_gbs"] / HBM_PEAK_GBS, 4)
+                kernels[fam] = k
+            return kernels
+
+        kernels = families(timing_s, counts_s)          # standalone (serial schedule)
+        overlapped = families(timing, counts)           # default schedule, lanes concurrent
         dom = max(kernels, key=lambda f: kernels[f]["ms_per_frame"]) if kernels else None
         dk = kernels.get(dom, {})
+        # The whole frame of the timed schedule: every family's algorithmic (and PMC) bytes per frame
+        # over the frame's wall time.
+        fr_ms = elapsed / args.steps * 1e3
+        alg_frame = sum(k["alg_bytes_per_launch"] * k["launches_per_frame"] for k in overlapped.values())
+        frame = {"alg_bytes": round(alg_frame), "achieved_gbs": round(alg_frame / (fr_ms * 1e-3) / 1e9, 1),
+                 "frac": round(alg_frame / (fr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "frame_ms": round(fr_ms, 3)}
+        if pmc is not None:
+            pmc_frame = sum(k.get("traffic_per_launch", 0) * k["launches_per_frame"] for k in overlapped.values())
+            frame.update({"traffic": round(pmc_frame), "traffic_gbs": round(pmc_frame / (fr_ms * 1e-3) / 1e9, 1),
+                          "traffic_frac": round(pmc_frame / (fr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "traffic_over_alg": round(pmc_frame / alg_frame, 3) if alg_frame else None})
         roofline = {"bound": "hbm", "kernel": dom, "achieved": dk.get("achieved_gbs"), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": dk.get("frac"), "traffic": dk.get("traffic_per_launch"),
+                    "frame": frame,
                     "traffic_gbs": dk.get("traffic_gbs"), "traffic_frac": dk.get("traffic_frac"),
                     "copy_peak_gbs": HBM_COPY_GBS,
                     "frac_of_copy_peak": round(dk["achieved_gbs"] / HBM_COPY_GBS, 4) if dk.get("achieved_gbs") else None,
                     "alg_bytes_per_launch": dk.get("alg_bytes_per_launch"), "avg_launch_us": dk.get("avg_launch_us"),
-                    "launches_per_frame": dk.get("launches_per_frame"),
-                    "definition": "achieved = the family's algorithmic HBM bytes per launch (compulsory queue/record/"
-                                  "output bytes per counted unit, DESIGN.md 7, counted on the device) / its mean launch "
-                                  "duration (HIP events on its own stream); traffic = rocprofv3 PMC bytes per launch "
-                                  "(FETCH_SIZE x2 + WRITE_SIZE)",
-                    "traffic_source": pmc_src, "window_ms_per_step": round(elapsed_ev / args.steps * 1e3, 3),
-                    "kernels": kernels, "survey_model": model, "build": build_info}
-        # The chunk lanes run kernels concurrently, so a launch's HIP-event duration includes
-        # the time it shares the GPU with the other lanes' kernels, and the per-kernel figures above
-        # understate each kernel's own rate.  The whole frame's rate: every family's algorithmic (and PMC)
-        # bytes per frame over the frame's wall time.
-        fr_ms = elapsed_ev / args.steps * 1e3
-        alg_frame = sum(k["alg_bytes_per_launch"] * k["launches_per_frame"] for k in kernels.values())
-        roofline["frame"] = {"alg_bytes": round(alg_frame), "achieved_gbs": round(alg_frame / (fr_ms * 1e-3) / 1e9, 1),
-                             "frac": round(alg_frame / (fr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                             "kernel_ms_per_frame": round(sum(k["ms_per_frame"] for k in kernels.values()), 3),
-                             "concurrency": round(sum(k["ms_per_frame"] for k in kernels.values()) / fr_ms, 2)}
-        if pmc is not None:
-            pmc_frame = sum(k.get("traffic_per_launch", 0) * k["launches_per_frame"] for k in kernels.values())
-            roofline["frame"].update({"traffic": round(pmc_frame),
-                                      "traffic_gbs": round(pmc_frame / (fr_ms * 1e-3) / 1e9, 1),
-                                      "traffic_frac": round(pmc_frame / (fr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+                    "launches_per_frame": dk.get("launches_per_frame"), "ms_per_frame": dk.get("ms_per_frame"),
+                    "definition": "frame = the timed schedule's whole frame: algorithmic HBM bytes per frame (compulsory "
+                                  "queue/record/output bytes per counted unit, DESIGN.md 7, counted on the device) / frame "
+                                  "time, PMC bytes likewise.  Top level = the kernel family with the most standalone time "
+                                  "per frame: its algorithmic bytes per launch / its own mean launch duration (HIP events, "
+                                  "serial schedule: one stream, no concurrent kernels); traffic = rocprofv3 PMC bytes per "
+                                  "launch (FETCH_SIZE x2 + WRITE_SIZE)",
+                    "traffic_source": pmc_src,
+                    "serial_frame_ms": round(elapsed_s / args.steps * 1e3, 3),
+                    "kernels": kernels,
+                    "kernels_overlapped": {"window_ms_per_step": round(elapsed_ev / args.steps * 1e3, 3),
+                                           "concurrency": round(sum(k["ms_per_frame"] for k in overlapped.values()) /
+                                                                (elapsed_ev / args.steps * 1e3), 2),
+                                           "families": overlapped},
+                    "survey_model": model, "build": build_info}
         out = {
             "metric": "Msamples/sec (whole node) + wall-clock to 1080p/64spp frame; %HBM roofline",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -379,6 +415,7 @@ def main():
                        "scene": scene.info.get("dragon", ""), "triangles": scene.info.get("triangles"),
                        "parallelism": (f"tiles32x32 round-robin over {world} GPUs, RCCL gather of RGBA8 spans"
                                        if world > 1 else "1 GPU, whole frame (no exchange)"),
+                       "schedule": "serial (one stream)" if args.serial else "default (3 chunk lanes)",
                        "frame_ms": round(ms_per_step, 3), "scene_upload_s": round(upload_s, 3)},
             "roofline": roofline,
         }

@@ -32,7 +32,9 @@
  * Whitted Li or Path/VolPath path, 256 interfaces on one transmittance walk — and a frame in which
  * a walk reaches a bound fails with PBR_E_UNSUPPORTED (synchronous renders: that call;
  * asynchronous ones: the next pbr_hip_render or pbr_hip_sync on the context) instead of returning
- * a truncated image.
+ * a truncated image.  BVH traversal keeps the reference's 64-entry stack (BVHAccel.cpp:293): an
+ * upload whose tree could overflow it (or the 1.5-entries-per-level need of the two-level node walk)
+ * fails with PBR_E_UNSUPPORTED.
  */
 #ifndef PBR_HIP_H
 #define PBR_HIP_H
@@ -44,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PBR_HIP_ABI_VERSION 3
+#define PBR_HIP_ABI_VERSION 4
 
 /* ---- status codes ---- */
 enum {
@@ -271,6 +273,33 @@ const char* pbr_hip_last_error(const pbr_hip_ctx* ctx);
 /* Waits for the context's asynchronous frames; returns PBR_E_UNSUPPORTED if one of them stopped at
  * a safety bound (see above). */
 int pbr_hip_sync(pbr_hip_ctx* ctx);
+
+/* ---- schedule (no reference counterpart) ----
+ * How a frame is cut into launches on the device.  Every setting renders the same bits (the GPU
+ * tests compare them with each other and with the reference); the defaults — a zeroed struct or
+ * NULL — are the measured schedule of DESIGN.md §4.  The library reads no environment variables:
+ * this call is the only run-time switch.  The setting holds for the context's later renders. */
+enum pbr_kernels_mode {
+    PBR_KERNELS_AUTO = 0,       /* the wavefront schedule wherever the integrator and scene allow it */
+    PBR_KERNELS_MEGAKERNEL = 1  /* one kernel per frame, whole Li per lane */
+};
+enum pbr_fuse_mode {
+    PBR_FUSE_AUTO = 0,          /* Whitted's level-0 shade traces its own camera rays in frames of at
+                                 * least max(2, lanes) chunks (a separate camera kernel otherwise) */
+    PBR_FUSE_OFF = 1,
+    PBR_FUSE_ON = 2
+};
+typedef struct pbr_schedule {
+    int kernels;                /* pbr_kernels_mode */
+    int chunk_log2;             /* at most 2^chunk_log2 samples per chunk (10..28; 0 = the default: 25 for
+                                 * Whitted, less with several lights, 26 for Path / VolPath); capped at
+                                 * the default, which bounds the queue memory per lane */
+    int lanes;                  /* chunk lanes, each its own stream and queues (1..4); 0 = 3 */
+    int fuse_camera;            /* pbr_fuse_mode */
+    int serial;                 /* 1: every launch of a frame on the caller's stream, one after another
+                                 * (one lane, no shadow stream) — measures each kernel on its own */
+} pbr_schedule;
+int pbr_hip_set_schedule(pbr_hip_ctx* ctx, const pbr_schedule* sched);
 
 /* ---- per-kernel profile (measurement; no reference counterpart) ----
  * While profiling is on, every kernel launch of a render is bracketed by a HIP event pair on the

@@ -49,6 +49,7 @@ class HipRenderer:
 
     def upload(self, scene: "scenes.Scene"):
         self._desc = scene.desc()
+        self._desc.abi_version = self.lib.pbr_hip_abi_version()   # (an older A/B build: same descriptors)
         self._scene = scene
         self._check(self.lib.pbr_hip_upload_scene(self.ctx, C.byref(self._desc)), "upload_scene")
 
@@ -85,6 +86,13 @@ class HipRenderer:
         self._check(self.lib.pbr_hip_render(self.ctx, C.byref(rdesc), rgb_ptr or None, rgba_ptr or None,
                                             C.byref(st) if st is not None else None), "render")
         return st
+
+    def set_schedule(self, kernels=capi.KERNELS_AUTO, chunk_log2=0, lanes=0, fuse_camera=capi.FUSE_AUTO, serial=False):
+        """How later frames are cut into launches (pbr_hip_set_schedule); no arguments = the measured
+        default; serial=True runs every launch on the caller's stream in turn (measurement).  Results
+        are the same bits under every schedule."""
+        s = capi.Schedule(kernels, chunk_log2, lanes, fuse_camera, int(serial))
+        self._check(self.lib.pbr_hip_set_schedule(self.ctx, C.byref(s)), "set_schedule")
 
     def set_profiling(self, on: bool = True):
         """Start (on) or stop a per-kernel measurement window (pbr_hip_set_profiling)."""

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 PBR_OK = 0
 PBR_E_INVALID = -1
@@ -210,6 +210,15 @@ class KernelProfile(C.Structure):
     ]
 
 
+KERNELS_AUTO, KERNELS_MEGAKERNEL = 0, 1
+FUSE_AUTO, FUSE_OFF, FUSE_ON = 0, 1, 2
+
+
+class Schedule(C.Structure):
+    _fields_ = [("kernels", C.c_int), ("chunk_log2", C.c_int), ("lanes", C.c_int), ("fuse_camera", C.c_int),
+                ("serial", C.c_int)]
+
+
 # Every symbol include/pbr_hip.h declares, with its ctypes signature.
 EXPORTS = {
     "pbr_hip_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -233,6 +242,7 @@ EXPORTS = {
     "pbr_hip_bounds": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float)]),
     "pbr_hip_li": (C.c_int, [C.c_void_p, C.POINTER(RenderDesc), C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int32),
                              C.c_int, C.POINTER(C.c_float)]),
+    "pbr_hip_set_schedule": (C.c_int, [C.c_void_p, C.POINTER(Schedule)]),
     "pbr_hip_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "pbr_hip_get_profile": (C.c_int, [C.c_void_p, C.POINTER(KernelProfile), C.c_int, C.POINTER(C.c_int)]),
     "pbr_hip_set_bvh_build": (C.c_int, [C.c_void_p, C.c_int]),
@@ -249,7 +259,8 @@ _lib = None
 
 
 OPTIONAL_FOR_AB = ("pbr_hip_sync", "pbr_hip_set_profiling", "pbr_hip_get_profile", "pbr_hip_query", "pbr_hip_bounds",
-                   "pbr_hip_li", "pbr_hip_set_bvh_build", "pbr_hip_bvh_build_info", "pbr_hip_build_bvh")
+                   "pbr_hip_li", "pbr_hip_set_bvh_build", "pbr_hip_bvh_build_info", "pbr_hip_build_bvh",
+                   "pbr_hip_set_schedule")
 
 
 def load_library(path: str | None = None) -> C.CDLL:
@@ -274,7 +285,10 @@ def load_library(path: str | None = None) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.pbr_hip_abi_version() != ABI_VERSION:
+    v = lib.pbr_hip_abi_version()
+    # an experimental build passed by path (A/B timing) may be one ABI version older: v3 → v4 only
+    # added pbr_hip_set_schedule, the descriptors are unchanged
+    if v != ABI_VERSION and not (path is not None and v == ABI_VERSION - 1):
         raise RuntimeError("libpbr_hip.so ABI version mismatch")
     if path is None:
         _lib = lib

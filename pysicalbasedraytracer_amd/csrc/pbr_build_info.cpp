@@ -5,4 +5,9 @@
 #ifndef PBR_SRC_HASH
 #define PBR_SRC_HASH "unknown"
 #endif
-extern "C" const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 wavefront+megakernel src " PBR_SRC_HASH; }
+#if defined(PBR_DEV_KNOBS) && PBR_DEV_KNOBS
+#define PBR_BUILD_KIND " dev-knobs"   // an A/B build whose tuning switches may differ from the defaults
+#else
+#define PBR_BUILD_KIND ""
+#endif
+extern "C" const char* pbr_hip_build_info(void) { return "pbr_hip gfx950 wavefront+megakernel src " PBR_SRC_HASH PBR_BUILD_KIND; }

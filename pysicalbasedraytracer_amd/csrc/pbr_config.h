@@ -1,0 +1,21 @@
+// pbr_config.h — the build's tuning switches.
+//
+// Every kernel parameter below has ONE measured default (DESIGN.md §4/§7 give the A/B numbers).
+// Release builds take the defaults only: overriding a switch from the command line is an error
+// unless the build opts into development knobs with -DPBR_DEV_KNOBS=1 (what the A/B scripts in
+// tools/ do), so the shipped libpbr_hip.so has a single schedule and reads no environment.  The
+// run-time choices that remain — chunk size, lanes, megakernel vs wavefront, level-0 fusion — are
+// explicit arguments of pbr_hip_set_schedule (include/pbr_hip.h), each covered by the GPU tests.
+#pragma once
+
+#if !defined(PBR_DEV_KNOBS) || !PBR_DEV_KNOBS
+#if defined(PBR_TRAV_DIAG) || defined(PBR_HELPER) || defined(PBR_SHORT_STACK_DEPTH) || defined(PBR_TRAV_OCC) ||   \
+    defined(PBR_REFILL_SHORT) || defined(PBR_SCALAR_LOADS) || defined(PBR_QUAD_TRAVERSAL) || defined(PBR_PACKET) || \
+    defined(PBR_PACKET_EXTEND) || defined(PBR_XCD_RUN) || defined(PBR_XCD_TRAV_RUN) || defined(PBR_REFILL) ||       \
+    defined(PBR_REFILL_OCC) || defined(PBR_REFILL_OCC_ANY) || defined(PBR_REFILL_OCC_TR) ||                          \
+    defined(PBR_CAMERA_SHORT) || defined(PBR_WF_SHADE_OCC) || defined(PBR_WF_SHADE_OCC_MM) ||                        \
+    defined(PBR_WF_FUSED_OCC) || defined(PBR_WFP_OCC) || defined(PBR_WFV_OCC) || defined(PBR_LANES_DEFAULT) ||       \
+    defined(PBR_INLINE_TRANS)
+#error "tuning switches are development builds only: add -DPBR_DEV_KNOBS=1"
+#endif
+#endif

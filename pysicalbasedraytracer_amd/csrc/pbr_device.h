@@ -298,32 +298,10 @@ __device__ __forceinline__ float4 as_f4(ScalarF4 v) { return make_float4(v.x, v.
 #define PBR_QUAD_TRAVERSAL 1
 #endif
 constexpr bool kQuadTraversal = PBR_QUAD_TRAVERSAL != 0;
-// Short stack without scratch (PBR_STACK_BACKTRACK, default): the LDS entries form a ring; a push
-// into a full ring overwrites the oldest entry and marks the traversal "dropped".  When the ring
-// runs empty after a drop, the next node is found by walking parent links instead (quad nodes keep
-// `parent << 2 | slot` in word 29, leaves in S.leafParent): from the last reference entered, up to
-// its parent, re-deriving that node's slab tests and visit order (the same float operations, so the
-// same tEnter values) and taking the first slot after the one we came from that passes against the
-// current tMax — which is exactly what popping the dropped entry would have given (the ring held,
-// for every node on the current path, the passing slots after the path; a dropped one is re-tested
-// against a tMax that can only have shrunk, like the pop test).  Leaves are therefore tested in the
-// reference's order, bit for bit, with no scratch stack (the deeper entries of the 64-entry stack
-// used to spill to scratch: ≈ 19 B of HBM writes per camera ray on C2).  Closest hit keeps the
-// smallest tEnter of the overwritten entries: once it is >= tMax every one of them would fail its
-// pop test, and the walk is skipped.  Bit-identical frames with 1-, 2- and 6-entry rings, but
-// slower than spilling to scratch, which the caches absorb: C2 18.5 → 19.6 ms, C3 331 → 382 ms,
-// C5 1752 → 1951 ms (profiles/r2_stackless_ab.log) — a parent walk re-fetches and re-tests a
-// node where a pop reads 8 B — so it is off by default.
-#ifndef PBR_STACK_BACKTRACK
-#define PBR_STACK_BACKTRACK 0
-#endif
-constexpr bool kBacktrack = PBR_STACK_BACKTRACK != 0;
-
 struct QuadSlots {   // one quad node's four slots in visit order
     float t[4];
     int ref[4];
     bool k[4];       // slab passes (box valid)
-    bool sA, sB, sN; // the swaps that produced the order (for the parent-link slot → position map)
 };
 template <bool ANY>
 __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const Ray& r, f3 inv, bool n0, bool n1, bool n2,
@@ -351,7 +329,6 @@ __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const 
     int r0 = __float_as_int(R.x), r1 = __float_as_int(R.y), r2 = __float_as_int(R.z), r3 = __float_as_int(R.w);
     auto swp = [](bool c, auto& a, auto& b) { auto x = c ? b : a; b = c ? a : b; a = x; };
     auto neg = [&](int axis) { return axis == 0 ? n0 : (axis == 1 ? n1 : n2); };
-    q->sA = q->sB = q->sN = false;
     // Any-hit (IntersectP) keeps the slots in build order instead.  Its answer does not
     // depend on the visit order: ray.tMax never shrinks, so every box test and the set of
     // reachable leaves are order-free, and the result is whether any primitive there is
@@ -362,7 +339,6 @@ __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const 
         swp(sB, k2, k3); swp(sB, t2, t3); swp(sB, r2, r3);
         swp(sN, k0, k2); swp(sN, t0, t2); swp(sN, r0, r2);
         swp(sN, k1, k3); swp(sN, t1, t3); swp(sN, r1, r3);
-        q->sA = sA; q->sB = sB; q->sN = sN;
     }
     q->t[0] = t0; q->t[1] = t1; q->t[2] = t2; q->t[3] = t3;
     q->ref[0] = r0; q->ref[1] = r1; q->ref[2] = r2; q->ref[3] = r3;
@@ -371,38 +347,21 @@ __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const 
 
 template <bool ANY, int SHORT>
 __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, bool n0, bool n1, bool n2) {
-    constexpr bool BT = kBacktrack && SHORT > 0;
-    constexpr int PRIV = BT ? 1 : 64 - SHORT;
+    constexpr int PRIV = kTraversalStack - SHORT;
     int stackRef[PRIV];
     float stackT[PRIV];
     int* lref = nullptr;
     float* lt = nullptr;
     if constexpr (SHORT > 0) trav_lds<SHORT>(&lref, &lt);
-    int sp = 0;             // entries held (stack depth; with BT at most SHORT)
-    int top = 0;            // BT: ring position of the next push
-    bool dropped = false;   // BT: an entry was overwritten
-    float dropT = __builtin_inff();   // BT, closest hit: smallest entry distance of an overwritten entry
+    int sp = 0;
     // any-hit: ray.tMax never shrinks, so a pushed slot (tEnter < tMax) always passes its re-test
     // on the way out and only the reference is kept
     auto push = [&](int ref, float t) {
-        if constexpr (BT) {
-            if (sp == SHORT) {   // overwriting the oldest entry
-                dropped = true;
-                if (!ANY) dropT = fminf(dropT, lt[top * 256]);
-            }
-            lref[top * 256] = ref;
-            if (!ANY) lt[top * 256] = t;
-            top = top + 1 == SHORT ? 0 : top + 1;
-            if (sp < SHORT) ++sp;
-        } else {
-            if (SHORT && sp < SHORT) { lref[sp * 256] = ref; if (!ANY) lt[sp * 256] = t; }
-            else { stackRef[sp - SHORT] = ref; if (!ANY) stackT[sp - SHORT] = t; }
-            ++sp;
-        }
+        if (SHORT && sp < SHORT) { lref[sp * 256] = ref; if (!ANY) lt[sp * 256] = t; }
+        else { stackRef[sp - SHORT] = ref; if (!ANY) stackT[sp - SHORT] = t; }
+        ++sp;
     };
     int cur = S.quadRootRef;
-    int last = cur;   // BT: the reference entered last (the subtree in progress)
-    int from = -1;    // BT: re-entering node `cur` from its slot `from` (parent-link walk), else -1
     bool found = false;
     while (true) {
 #if PBR_TRAV_DIAG
@@ -437,51 +396,31 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
         } else {
             QuadSlots q;
             quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
-            // slots at or before the visit position of `from` are done (only on a parent-link walk)
-            int done = -1;
-            if (BT && from >= 0) {
-                const int rh = from >> 1, rl = from & 1;   // inverse of quad_slots' swaps
-                done = ((rh ^ (int)q.sN) << 1) | (rl ^ (int)(rh ? q.sB : q.sA));
-            }
             const float tM = r.tMax;
-            const bool p0 = done < 0 && q.k[0] && q.t[0] < tM, p1 = done < 1 && q.k[1] && q.t[1] < tM,
-                       p2 = done < 2 && q.k[2] && q.t[2] < tM, p3 = done < 3 && q.k[3] && q.t[3] < tM;
-            from = -1;
+            const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
+                       p3 = q.k[3] && q.t[3] < tM;
             if (p0 | p1 | p2 | p3) {
-                if (!BT && sp > 64 - 3) break;   // never reached: SAH trees here stay < 30 binary levels
+                // unreachable: the upload refuses trees whose quad walk can need more (kQuadStackLimit)
+                if (sp > kQuadStackLimit) { atomicOr(S.guard, kGuardStack); break; }
                 const int first = p0 ? 0 : (p1 ? 1 : (p2 ? 2 : 3));
                 if (p3 && first < 3) push(q.ref[3], q.t[3]);
                 if (p2 && first < 2) push(q.ref[2], q.t[2]);
                 if (p1 && first < 1) push(q.ref[1], q.t[1]);
                 cur = first == 0 ? q.ref[0] : (first == 1 ? q.ref[1] : (first == 2 ? q.ref[2] : q.ref[3]));
-                last = cur;
                 continue;
             }
         }
         bool more = false;   // pop until an entry passes its box test against the current tMax
         while (sp > 0) {
             --sp;
-            int e = sp;
-            if constexpr (BT) { top = top == 0 ? SHORT - 1 : top - 1; e = top; }
             int rr;
             float tt;
-            if (ANY) { cur = (SHORT && e < SHORT) ? lref[e * 256] : stackRef[e - SHORT]; more = true; break; }
-            if (SHORT && e < SHORT) { rr = lref[e * 256]; tt = lt[e * 256]; }
-            else { rr = stackRef[e - SHORT]; tt = stackT[e - SHORT]; }
+            if (ANY) { cur = (SHORT && sp < SHORT) ? lref[sp * 256] : stackRef[sp - SHORT]; more = true; break; }
+            if (SHORT && sp < SHORT) { rr = lref[sp * 256]; tt = lt[sp * 256]; }
+            else { rr = stackRef[sp - SHORT]; tt = stackT[sp - SHORT]; }
             if (tt < r.tMax) { cur = rr; more = true; break; }
         }
-        // ring empty after a drop: re-enter the parent of `last` after the slot it came from — unless
-        // every overwritten entry would fail its pop test now (closest hit: tEnter >= tMax)
-        if (BT && !more && dropped && (ANY || dropT < r.tMax)) {
-            const int link = last < 0 ? S.leafParent[last & 0x7fffffff] : __float_as_int(S.quad[8 * (size_t)last + 7].y);
-            if (link >= 0) {
-                cur = link >> 2;
-                from = link & 3;
-                more = true;
-            }
-        }
         if (!more) break;
-        last = cur;
     }
     return found;
 }
@@ -505,7 +444,7 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
 // unchanged), while node and triangle fetches are scalar (one per wave), the stack costs no
 // per-lane memory and control flow is wave-uniform.  The stack is 64 entries per wave, like the
 // per-lane one.
-constexpr int kPacketStack = 64;
+constexpr int kPacketStack = kTraversalStack;
 __shared__ int s_pk_ref[4][kPacketStack];                  // parent quad node << 2 | slot column
 __shared__ unsigned long long s_pk_mask[4][kPacketStack];  // lanes that pushed the entry
 #ifndef PBR_PACKET
@@ -581,7 +520,12 @@ __device__ bool traverse_packet(const DeviceScene& S, Ray& r, HitRec* h, f3 inv,
             int first = -1;
             for (int pos = 0; pos < 4; ++pos)
                 if (first < 0 && bm[col[pos]] != 0ull) first = pos;
-            if (first >= 0 && sp <= kPacketStack - 3) {
+            // unreachable: the upload refuses trees whose quad walk can need more (kQuadStackLimit)
+            if (first >= 0 && sp > kQuadStackLimit) {
+                atomicOr(S.guard, kGuardStack);
+                break;
+            }
+            if (first >= 0) {
                 for (int pos = 3; pos > first; --pos)
                     if (bm[col[pos]] != 0ull) {
                         sref[sp] = (cur << 2) | col[pos];   // every lane stores the same values
@@ -669,9 +613,15 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
         if (STATS) c->nodes++;
         if (!node_hit(a, b, r, inv, n0, n1, n2)) return false;
     }
-    if constexpr (!STATS && kQuadTraversal) return traverse_quad<ANY, SHORT>(S, r, h, inv, n0, n1, n2);
-    int stackRef[64 - SHORT];
-    float stackT[64 - SHORT];
+    // The quad walk, except in a tree whose quad walk could need more stack than it has
+    // (S.binaryWalk, see pbr_hip_upload_scene): those run the megakernel (SHORT == 0) over the
+    // binary layout, whose one-entry-per-level stack holds BVHAccel's 64 levels.  Same primitive
+    // tests in the same order either way.
+    if constexpr (!STATS && kQuadTraversal) {
+        if (SHORT > 0 || !S.binaryWalk) return traverse_quad<ANY, SHORT>(S, r, h, inv, n0, n1, n2);
+    }
+    int stackRef[kTraversalStack - SHORT];
+    float stackT[kTraversalStack - SHORT];
     int* lref = nullptr;
     float* lt = nullptr;
     if constexpr (SHORT > 0) trav_lds<SHORT>(&lref, &lt);
@@ -716,7 +666,8 @@ __device__ bool traverse(const DeviceScene& S, Ray& r, HitRec* h, Counters* c) {
             if (okN && tN < r.tMax) {
                 if (STATS && !okF) tF = __int_as_float(0x7fc00000);
                 if (okF || STATS) {
-                    if (sp >= 64) break;   // BVHAccel's 64-entry stack; the SAH builds here stay < 30 deep
+                    // unreachable: the upload refuses trees deeper than BVHAccel's 64-entry stack
+                    if (sp >= kTraversalStack) { atomicOr(S.guard, kGuardStack); break; }
                     if (SHORT && sp < SHORT) { lref[sp * 256] = farRef; lt[sp * 256] = tF; }
                     else { stackRef[sp - SHORT] = farRef; stackT[sp - SHORT] = tF; }
                     ++sp;
@@ -1267,24 +1218,32 @@ __device__ __forceinline__ void tri_verts(const DeviceScene& S, int slot, f3* p0
 }
 // InfiniteAreaLight::Sample_Li (InfiniteAreaLight.cpp:78-100) with Distribution2D::SampleContinuous
 // (Sampling.h:146-156)
-__device__ __noinline__ rgb inf_sample_li(const InfDev* Ep, float worldRadius, f3 refP, float u0, float u1, f3* wi,
-                                          float* pdf, VisPt* v) {
+// Out of line, returning by value: pointer out-parameters of a call make the caller keep its
+// (wi, pdf, vis) variables in private memory, so every shading kernel would store them to scratch
+// on every light sample, whichever light type it samples.
+struct InfLiSample { rgb L; f3 wi; float pdf; bool mapped; };   // mapped: mapPdf != 0 (wi set)
+__device__ __noinline__ InfLiSample inf_sample_li(const InfDev* Ep, float u0, float u1) {
     const InfDev& E = *Ep;
+    InfLiSample o;
+    o.L = sp(0.f);
+    o.wi = mk(0, 0, 0);
+    o.mapped = false;
     float pdf0, pdf1;
     int row, col;
     float d1 = sample_continuous(E.margFunc, E.margCdf, E.h, E.margInt, u1, &pdf1, &row);
     float d0 = sample_continuous(E.condFunc + (size_t)row * E.w, E.condCdf + (size_t)row * (E.w + 1), E.w,
                                  E.margFunc[row], u0, &pdf0, &col);
     float mapPdf = pdf0 * pdf1;
-    if (mapPdf == 0) { *pdf = 0; return sp(0.f); }
+    if (mapPdf == 0) { o.pdf = 0; return o; }
+    o.mapped = true;
     float theta = d1 * kPi, phi = d0 * 2 * kPi;
     float cosTheta = t_cos(theta), sinTheta = t_sin(theta);
     float sinPhi = t_sin(phi), cosPhi = t_cos(phi);
-    *wi = xf_vector(E.l2w, mk(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
-    *pdf = mapPdf / (2 * kPi * kPi * sinTheta);
-    if (sinTheta == 0) *pdf = 0;
-    v->p = refP + *wi * (2 * worldRadius); v->pError = mk(0, 0, 0); v->n = mk(0, 0, 0); v->medIn = -1; v->medOut = -1;
-    return inf_lookup(E, d0, d1);
+    o.wi = xf_vector(E.l2w, mk(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
+    o.pdf = mapPdf / (2 * kPi * kPi * sinTheta);
+    if (sinTheta == 0) o.pdf = 0;
+    o.L = inf_lookup(E, d0, d1);
+    return o;
 }
 PBR_HELPER rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref, float u0, float u1, f3* wi, float* pdf, VisPt* v) {
     if (l.type == LT_POINT) {   // PointLight.cpp:5-15
@@ -1320,7 +1279,14 @@ PBR_HELPER rgb sample_li(const DeviceScene& S, const DLight& l, const Isect& ref
         v->p = ip; v->pError = ipErr; v->n = in; v->medIn = -1; v->medOut = -1;
         return area_L(l, in, -*wi);
     }
-    if (l.type == LT_INF) return inf_sample_li(S.inf, l.worldRadius, ref.p, u0, u1, wi, pdf, v);
+    if (l.type == LT_INF) {   // InfiniteAreaLight::Sample_Li (InfiniteAreaLight.cpp:78-100)
+        const InfLiSample o = inf_sample_li(S.inf, u0, u1);
+        *pdf = o.pdf;
+        if (!o.mapped) return o.L;   // (wi and vis untouched, as the reference leaves them)
+        *wi = o.wi;
+        v->p = ref.p + o.wi * (2 * l.worldRadius); v->pError = mk(0, 0, 0); v->n = mk(0, 0, 0); v->medIn = -1; v->medOut = -1;
+        return o.L;
+    }
     // SkyBoxLight::Sample_Li (SkyBoxLight.cpp:43-56)
     *wi = uniform_sphere(u0, u1);
     *pdf = 1.f / (4 * kPi);

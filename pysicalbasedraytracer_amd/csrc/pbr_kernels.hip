@@ -784,7 +784,7 @@ struct WfBufs {
 };
 // Chunks alternate between two lanes (own buffers, own stream) so one chunk's launch tails overlap
 // the other's work — what keeps a small per-GPU shard of a multi-GPU frame efficient.
-// Lanes a frame may use (PBR_LANES), and the default.  Measured (frame ms, bit-identical):
+// Lanes a frame may use (pbr_schedule::lanes), and the default.  Measured (frame ms, bit-identical):
 // C2 2 lanes 17.73-17.80, 3: 17.49, 4: 17.97 (4 lanes of 2^24-sample chunks 19.10); C3 268.7 /
 // 267.3 / 274.9; C5 1396 / 1379 / 1414.
 constexpr int kWfLanes = 4;
@@ -802,7 +802,6 @@ struct pbr_hip_ctx {
     HostScene host;
     HaltonTables halton;
     DevBuf dInfTex, dInfCF, dInfCC, dInfMF, dInfMC, dInfRec;
-    DevBuf dLeafParent;
     DevBuf dTexels, dTextures, dTexMats;   // ImageTextures and the textured materials' parameters
     DevBuf dNodes, dWide, dQuad, dTri, dInfo, dUV, dSph, dMat, dLights, dEnv, dCdf, dFunc, dMedia;
     DevBuf dPrimes, dRecips, dPrimeSums, dPerms, dPrimIds;
@@ -824,6 +823,7 @@ struct pbr_hip_ctx {
     hipEvent_t evShade[kWfLanes][kWfMaxDepth + 2] = {}, evShadow[kWfLanes][kWfMaxDepth + 2] = {};
     int curStrategy = PBR_LIGHTS_UNIFORM;
     float funcInt = 0;
+    pbr_schedule sched = {};             // pbr_hip_set_schedule (zero = the measured defaults)
     // per-kernel profile (pbr_hip_set_profiling): a HIP event pair around every launch, on the
     // launch's stream, and the work counters of each kernel family (device rows + host-known counts)
     bool profOn = false, profCount = false;
@@ -898,6 +898,7 @@ int check_guard(pbr_hip_ctx* ctx) {
     std::string what;
     if (g & kGuardWhittedPassThrough) what += "a Whitted path crossed more than 1024 material-less surfaces; ";
     if (g & kGuardTransmittance) what += "a transmittance walk crossed more than 256 medium interfaces; ";
+    if (g & kGuardStack) what += "a BVH traversal stack was full; ";
     return set_err(ctx, PBR_E_UNSUPPORTED, what + "the frame is incomplete");
 }
 
@@ -910,7 +911,7 @@ DeviceScene device_scene(pbr_hip_ctx* ctx) {
     S.rootRef = h.rootRef;
     S.quad = (const float4*)ctx->dQuad.p;
     S.quadRootRef = h.quadRootRef;
-    S.leafParent = (const int*)ctx->dLeafParent.p;
+    S.binaryWalk = h.quadStackNeed > kQuadStackLimit ? 1 : 0;
     S.triVerts = (const float4*)ctx->dTri.p;
     S.guard = (int*)ctx->dGuard.p;
     S.primInfo = (const int4*)ctx->dInfo.p;
@@ -1025,12 +1026,6 @@ int upload_light_distribution(pbr_hip_ctx* ctx, int strategy) {
 }
 
 
-// PBR_LOBE_SETS=0: no Lambert + mirror specialisation of the shading kernels (A/B switch)
-bool lobe_set_switch() {
-    const char* e = getenv("PBR_LOBE_SETS");
-    return !(e && e[0] == '0');
-}
-
 // Chunking of the wavefront schedules: at most 2^chunkLog2 samples per chunk; chunks alternate
 // over the lanes.  Measured on C2: two lanes 23.4 ms vs 24.9 for one; forcing a one-chunk
 // (1/8-frame shard) frame into two concurrent half chunks was slower (4.00 vs 3.86 ms).
@@ -1041,12 +1036,10 @@ struct WfChunks {
     int segCap = 0;   // capacity of one queue segment
     size_t qcap = 0;  // queue entries
 };
-WfChunks wf_chunks(const KParams& P, int maxLog2 = 25) {
+WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25) {
     WfChunks c;
-    int chunkLog2 = maxLog2;
-    if (const char* e = getenv("PBR_CHUNK_LOG2")) chunkLog2 = std::min(28, std::max(16, atoi(e)));
-    c.lanes = kWfDefaultLanes;
-    if (const char* e = getenv("PBR_LANES")) c.lanes = std::min(kWfLanes, std::max(1, atoi(e)));
+    const int chunkLog2 = sch.chunk_log2 > 0 ? std::min(sch.chunk_log2, maxLog2) : maxLog2;   // the default bounds the memory
+    c.lanes = sch.serial ? 1 : (sch.lanes > 0 ? sch.lanes : kWfDefaultLanes);
     c.chunkPix = std::max(1LL, (1LL << chunkLog2) / P.spp);
     if (c.chunkPix >= P.nPixels) {   // one chunk: splitting a small frame only adds launch tails
         c.chunkPix = P.nPixels;
@@ -1057,12 +1050,9 @@ WfChunks wf_chunks(const KParams& P, int maxLog2 = 25) {
         // frame ms; default / rounded down / rounded up): C5 (32 chunks) 1215 / 1193 / 1200, C4
         // (254) 6628 / 6587 / 6572, C3 (16) 257.0 / 257.5 / 268.3, C2 (4) 17.5 / 18.6 / 18.3 —
         // with few chunks the power-of-two size wins, so only 24 or more are balanced.
-        // PBR_CHUNK_BALANCE: 0 off, 'u' round up, 'd' round down, whatever the count.
-        const char* e = getenv("PBR_CHUNK_BALANCE");
         long long n = (P.nPixels + c.chunkPix - 1) / c.chunkPix;
-        const char mode = e ? e[0] : (n >= 24 ? 'd' : '0');
-        if (mode == 'd' || mode == 'u') {
-            n = mode == 'd' ? std::max<long long>(c.lanes, n / c.lanes * c.lanes) : (n + c.lanes - 1) / c.lanes * c.lanes;
+        if (n >= 24) {
+            n = std::max<long long>(c.lanes, n / c.lanes * c.lanes);
             c.chunkPix = (P.nPixels + n - 1) / n;
         }
     }
@@ -1152,27 +1142,23 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     // they stay under 8 GB per lane (C2: 5 levels × 36 B × 2^25 = 6 GB)
     int maxLog2 = 25;
     while (maxLog2 > 20 && (double)levels * (36.0 + (ml ? 17.0 * nL : 0.0)) * (double)(1LL << maxLog2) > 8e9) --maxLog2;
-    const WfChunks ch = wf_chunks(P, maxLog2);
+    const WfChunks ch = wf_chunks(ctx->sched, P, maxLog2);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const int lightsPerShade = ml ? std::max(1, nL) : 1;
     const size_t sqcap = qcap * (size_t)lightsPerShade;   // shadow-queue entries
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
-    const bool mm = (lobes & ~kMatteMirrorLobes) == 0 && lobe_set_switch();   // Lambert + mirror only (C2)
+    const bool mm = (lobes & ~kMatteMirrorLobes) == 0;   // Lambert + mirror only (C2)
     const bool textured = (lobes & kTexturedLobes) != 0;
-    // tuning switches (results are bit-identical either way): LDS short stack, shade occupancy
-    const char* eStack = getenv("PBR_SHORT_STACK");
-    const bool shortStack = !(eStack && eStack[0] == '0');
-    const char* eMats = getenv("PBR_MATS_LDS");
-    const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
-    // the level-0 shade traces its own camera rays (PBR_FUSED_CAMERA=0: the camera kernel + queue)
-    const char* eFuse = getenv("PBR_FUSED_CAMERA");
-    // Frames with fewer chunks than lanes (rank shards of a multi-GPU C2 job) keep the separate
-    // kernels: there the camera kernel's 8 waves per SIMD win (C2 shard 0/8, one chunk: 2.58 → 3.10
-    // ms fused; shard 0/2, two chunks: 9.58-9.63 → 10.12-10.22).  PBR_FUSED_CAMERA=2 fuses them too.
+    const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats;   // templates staged in LDS
+    // The level-0 shade traces its own camera rays (no camera kernel and queue).  Frames with fewer
+    // chunks than lanes (rank shards of a multi-GPU C2 job) keep the separate kernels by default:
+    // there the camera kernel's 8 waves per SIMD win (C2 shard 0/8, one chunk: 2.58 → 3.10 ms fused;
+    // shard 0/2, two chunks: 9.58-9.63 → 10.12-10.22).
     const long long nChunks = (P.nPixels + ch.chunkPix - 1) / ch.chunkPix;
-    const bool fuseCamera = kPacket && kQuadTraversal && !(eFuse && eFuse[0] == '0') && (mm || simple) && matsLds &&
-                            !textured && !ml && (nChunks >= std::max(2, ch.lanes) || (eFuse && eFuse[0] == '2'));
+    const int fuse = ctx->sched.fuse_camera;
+    const bool fuseCamera = kPacket && kQuadTraversal && fuse != PBR_FUSE_OFF && (mm || simple) && matsLds && !textured &&
+                            !ml && (nChunks >= std::max(2, ch.lanes) || fuse == PBR_FUSE_ON);
     ctx->wfFused = fuseCamera;
     // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
     const int maxLevels = levels;   // no material-less primitives here (those scenes run the megakernel)
@@ -1180,8 +1166,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     // only read what shade(L) wrote); the shadow queue alternates between two buffers by level.
     // Default: when the frame is one chunk (no lane overlap).  Measured on C2: a 1/8 shard
     // 3.97 → 3.54 ms; the whole frame (two lanes) 23.43 → 23.76 ms, so off there.
-    const char* eOv = getenv("PBR_SHADOW_STREAM");
-    const bool shadowOverlap = (eOv ? eOv[0] == '1' : ch.lanes == 1) && maxLevels <= kWfMaxDepth + 2;
+    const bool shadowOverlap = ch.lanes == 1 && !ctx->sched.serial && maxLevels <= kWfMaxDepth + 2;
     WfParams WL[kWfLanes];
     int* cntL[kWfLanes];
     for (int l = 0; l < ch.lanes; ++l) {
@@ -1239,11 +1224,9 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const dim3 blk(256), gstride(kWfBlocks);
     // The queue consumers (extend, shadow) run exactly one resident wave of workgroups: a grid of
     // kWfBlocks would leave a partial second round (2048 = 1.33 × the 1536 resident at 6/CU).
-    const char* ePers = getenv("PBR_RESIDENT_GRID");
-    const bool pers = !(ePers && ePers[0] == '0');
-    const dim3 gShadow = pers ? resident_grid(ctx, shortStack ? (const void*)k_wf_shadow<kShortStack> : (const void*)k_wf_shadow<0>) : gstride;
-    const dim3 gShadowML = pers ? resident_grid(ctx, (const void*)k_wf_shadow_ml<kShortStack>) : gstride;
-    const dim3 gExtend = pers ? resident_grid(ctx, shortStack ? (const void*)k_wf_extend<kShortStack> : (const void*)k_wf_extend<0>) : gstride;
+    const dim3 gShadow = resident_grid(ctx, (const void*)k_wf_shadow<kShortStack>);
+    const dim3 gShadowML = resident_grid(ctx, (const void*)k_wf_shadow_ml<kShortStack>);
+    const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack>);
     if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
     int chunk = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
@@ -1257,8 +1240,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         W.cur = queue(l, 0);
         if (!fuseCamera) {
             PROF_LAUNCH(KP_WF_CAMERA, st,
-                if (shortStack) hipLaunchKernelGGL(k_wf_camera_extend<kCameraShort>, dim3((W.nSamples + 255) / 256), blk, 0, st, W);
-                else hipLaunchKernelGGL(k_wf_camera_extend<0>, dim3((W.nSamples + 255) / 256), blk, 0, st, W));
+                hipLaunchKernelGGL(k_wf_camera_extend<kCameraShort>, dim3((W.nSamples + 255) / 256), blk, 0, st, W));
         }
         prof_host(ctx, KP_WF_CAMERA, 0, (unsigned long long)W.nSamples);
         const hipStream_t sst = shadowOverlap ? ctx->shadowStream[l] : st;
@@ -1300,16 +1282,13 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             }
             PROF_LAUNCH(KP_WF_SHADOW, sst,
                 if (ml) hipLaunchKernelGGL(k_wf_shadow_ml<kShortStack>, gShadowML, blk, 0, sst, W);
-                else if (shortStack) hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, sst, W);
-                else hipLaunchKernelGGL(k_wf_shadow<0>, gShadow, blk, 0, sst, W));
+                else hipLaunchKernelGGL(k_wf_shadow<kShortStack>, gShadow, blk, 0, sst, W));
             if (int rc = prof_sums(ctx, sst, KP_WF_SHADOW, {W.shadowSeg})) return rc;
             if (shadowOverlap) HIP_TRY(hipEventRecord(ctx->evShadow[l][level], sst));
             if (level + 1 == maxLevels) break;
             cur ^= 1;
             W.cur = queue(l, cur);
-            PROF_LAUNCH(KP_WF_EXTEND, st,
-                if (shortStack) hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W);
-                else hipLaunchKernelGGL(k_wf_extend<0>, gExtend, blk, 0, st, W));
+            PROF_LAUNCH(KP_WF_EXTEND, st, hipLaunchKernelGGL(k_wf_extend<kShortStack>, gExtend, blk, 0, st, W));
             if (int rc = prof_sums(ctx, st, KP_WF_EXTEND, {W.cur.segCount})) return rc;
         }
         // the fold reads every level's records: after the last shadow launch (stream order on sst)
@@ -1328,15 +1307,14 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     const int spp = P.spp;
     // ≈ 290 B of queues + state per sample: 19.5 GB per 2^26 chunk and lane.  Measured (bit-identical):
     // C3 2^25 349.4 ms, 2^26 336.1, 2^27 340.4; C5 2^25 1979 ms, 2^26 1939, 2^27 1919
-    const WfChunks ch = wf_chunks(P, 26);
+    const WfChunks ch = wf_chunks(ctx->sched, P, 26);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
     const bool micro = (lobes & ~kMicroLobes) == 0;   // Lambert + microfacet reflection/transmission (C4, C5)
-    const bool mm = (lobes & ~kMatteMirrorLobes) == 0 && lobe_set_switch();   // Lambert + mirror only (C3)
+    const bool mm = (lobes & ~kMatteMirrorLobes) == 0;   // Lambert + mirror only (C3)
     const bool textured = (lobes & kTexturedLobes) != 0;
-    const char* eMats = getenv("PBR_MATS_LDS");
-    const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats && !(eMats && eMats[0] == '0');
+    const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats;   // templates staged in LDS
     // (the level-0 shade tracing its own camera rays, as Whitted's does, measured slower here: C3
     // 254 → 268-271 ms, C4 6575 → 6702 ms at 3 shading waves per SIMD; profiles/r3_fused_ab.log)
     WfvParams VL[kWfLanes];
@@ -1388,7 +1366,6 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         X.dFlags = (int*)B.rFlags.p; X.dLight = (int*)B.rLight.p; X.dTgt = (int*)B.rTgt.p;
         // Path: 5 camera dims + per bounce 1 + 2 + 2 (light) + 2 (BSDF) + 1 (RR)
         W.P.smp.ldsDims = std::min(kLdsDims, 5 + 8 * std::max(1, P.maxDepth) + 2);
-        if (const char* e = getenv("PBR_HALTON_LDS")) if (e[0] == '0') W.P.smp.ldsDims = 0;
     }
     auto queue = [&](int l, int k) {
         WfBufs& B = ctx->wb[l];
@@ -1772,12 +1749,20 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
         return set_err(ctx, PBR_E_HIP, e.what());
     }
     const HostScene& h = ctx->host;
+    // BVHAccel's 64-entry stack (BVHAccel.cpp:293) bounds the trees the reference can walk (deeper
+    // ones overflow it): those are refused rather than rendered with truncated traversals.  The
+    // quad walk needs up to 1.5 entries per binary level; a tree it could overflow (never an SAH
+    // tree of a real mesh) renders through the binary walk (device_scene: binaryWalk).
+    if (h.binaryStackNeed > kTraversalStack) {
+        ctx->haveScene = false;
+        return set_err(ctx, PBR_E_UNSUPPORTED, "BVH deeper than BVHAccel's 64-entry traversal stack (" +
+                                                   std::to_string(h.binaryStackNeed) + " interior levels)");
+    }
     HIP_TRY(hipMemsetAsync(ctx->dGuard.p, 0, sizeof(int), ctx->stream));
     *ctx->guardHost = 0;
     HIP_TRY(ctx->dNodes.upload(h.nodes, ctx->stream));
     HIP_TRY(ctx->dWide.upload(h.wide, ctx->stream));
     HIP_TRY(ctx->dQuad.upload(h.quad, ctx->stream));
-    HIP_TRY(ctx->dLeafParent.upload(h.leafParent, ctx->stream));
     HIP_TRY(ctx->dTri.upload(h.triVerts, ctx->stream));
     HIP_TRY(ctx->dInfo.upload(h.primInfo, ctx->stream));
     HIP_TRY(ctx->dUV.upload(h.triUV, ctx->stream));
@@ -1890,22 +1875,20 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     HIP_TRY(hipEventRecord(ctx->ev0, s));
     if (blocks > 0) {
         bool st = d->collect_stats != 0;
-        const char* wfEnv = getenv("PBR_WAVEFRONT");
+        // (a tree too deep for the quad walk's stack runs the megakernel's binary walk)
+        const bool mega = ctx->sched.kernels == PBR_KERNELS_MEGAKERNEL || ctx->host.quadStackNeed > kQuadStackLimit;
         // Whitted through material-less primitives recurses at the same depth without bound
         // (WhittedIntegrator.cpp:26-28): only the megakernel follows such chains to the end
         bool wavefront = d->integrator == PBR_INTEGRATOR_WHITTED && !st && ctx->host.lights.size() <= (size_t)kWfMaxLightsML &&
                          !ctx->host.anyNoMaterial &&
-                         d->max_depth <= kWfMaxDepth && !(wfEnv && wfEnv[0] == '0');
+                         d->max_depth <= kWfMaxDepth && !mega;
         bool wavefrontPath = (d->integrator == PBR_INTEGRATOR_PATH || d->integrator == PBR_INTEGRATOR_VOLPATH) && !st &&
-                             d->max_depth <= 120 && ctx->host.media.size() / 10 < 255 && !(wfEnv && wfEnv[0] == '0');
-        // waves per SIMD the megakernel is compiled for: trades VGPRs for scratch (PBR_OCC=1|2|4)
-        int occ = 2;   // measured: 2 waves/SIMD beats 1 by 1.78x on C2 and ties 4
-        if (const char* e = getenv("PBR_OCC")) occ = atoi(e);
+                             d->max_depth <= 120 && ctx->host.media.size() / 10 < 255 && !mega;
+        // the megakernel at 2 waves per SIMD (it trades VGPRs for scratch): 2 beat 1 by 1.78x on C2
+        // and tied 4
 #define PBR_LAUNCH(I)                                                                                 \
     if (st) hipLaunchKernelGGL((k_render<I, true, 1>), grid, block, 0, s, P);                        \
-    else if (occ >= 4) hipLaunchKernelGGL((k_render<I, false, 4>), grid, block, 0, s, P);            \
-    else if (occ >= 2) hipLaunchKernelGGL((k_render<I, false, 2>), grid, block, 0, s, P);            \
-    else hipLaunchKernelGGL((k_render<I, false, 1>), grid, block, 0, s, P);
+    else hipLaunchKernelGGL((k_render<I, false, 2>), grid, block, 0, s, P);
         if (wavefront || wavefrontPath) {
             int rc = wavefront ? render_wavefront(ctx, P, s) : render_wavefront_path(ctx, P, s, d->integrator == PBR_INTEGRATOR_VOLPATH);
             if (rc) {   // stopped part-way: the forked lane / shadow streams may still run
@@ -1956,6 +1939,23 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         stats->shading_events = hs[3];
         stats->n_launches = blocks > 0 ? 1 : 0;
     }
+    return PBR_OK;
+}
+
+int pbr_hip_set_schedule(pbr_hip_ctx* ctx, const pbr_schedule* sched) {
+    if (!ctx) return PBR_E_INVALID;
+    pbr_schedule s = {};
+    if (sched) s = *sched;
+    if (s.kernels != PBR_KERNELS_AUTO && s.kernels != PBR_KERNELS_MEGAKERNEL)
+        return set_err(ctx, PBR_E_INVALID, "schedule: unknown kernels mode");
+    if (s.chunk_log2 != 0 && (s.chunk_log2 < 10 || s.chunk_log2 > 28))
+        return set_err(ctx, PBR_E_INVALID, "schedule: chunk_log2 must be 0 or 10..28");
+    if (s.lanes < 0 || s.lanes > kWfLanes) return set_err(ctx, PBR_E_INVALID, "schedule: lanes must be 0..4");
+    if (s.fuse_camera < PBR_FUSE_AUTO || s.fuse_camera > PBR_FUSE_ON) return set_err(ctx, PBR_E_INVALID, "schedule: unknown fuse mode");
+    if (s.serial != 0 && s.serial != 1) return set_err(ctx, PBR_E_INVALID, "schedule: serial must be 0 or 1");
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;   // an asynchronous frame may still use the lane buffers
+    ctx->sched = s;
     return PBR_OK;
 }
 

@@ -82,7 +82,7 @@ struct DeviceScene {
     int rootRef;
     const float4* quad;            // 8 float4 per quad node (two binary levels, pbr_scene.cpp build_quad_nodes)
     int quadRootRef;
-    const int* leafParent;         // per leaf's first slot: parentQuad << 2 | raw slot (-1: root)
+    int binaryWalk;                // 1: the quad walk's stack could overflow in this tree (megakernel, binary walk)
     const float4* triVerts;
     const int4* primInfo;
     const float2* triUV;
@@ -112,8 +112,17 @@ struct DeviceScene {
 // (PBR_E_UNSUPPORTED) instead of returning a silently truncated result.
 constexpr int kGuardWhittedPassThrough = 1;   // > kMaxPassThrough material-less crossings in one Whitted Li
 constexpr int kGuardTransmittance = 2;        // > kMaxTrCrossings interfaces on one VisibilityTester::Tr walk
+constexpr int kGuardStack = 4;                // a traversal stack was full (never, given the upload check below)
 constexpr int kMaxPassThrough = 1024;
 constexpr int kMaxTrCrossings = 256;
+// Traversal stacks (pbr_device.h): BVHAccel's 64 entries (BVHAccel.cpp:293).  The binary walk pushes
+// at most one entry per interior level; a quad node (two binary levels) pushes up to three.  The
+// upload measures both needs on the built tree (HostScene::binaryStackNeed / quadStackNeed): a tree
+// the quad walk could overflow renders with the megakernel over the binary layout
+// (DeviceScene::binaryWalk), and one deeper than the reference's own 64-entry stack is refused, so
+// no walk is ever truncated.
+constexpr int kTraversalStack = 64;
+constexpr int kQuadStackLimit = kTraversalStack - 3;   // a quad walk pushes only while sp <= 61
 
 struct DeviceSampler {
     int type;                      // pbr_sampler_type

@@ -7,6 +7,7 @@
 // watertight fallback, gamma(n)), so do we — fp64 is cheap on CDNA4.  Transcendentals are
 // evaluated as (float)f((double)x) on both sides of the parity check.
 #pragma once
+#include "pbr_config.h"
 #include <stdint.h>
 #include <math.h>
 

@@ -71,8 +71,8 @@ template <class Ref>
 void build_quad_nodes(HostScene* S, Ref&& binRef) {
     const std::vector<LinearBVHNode>& L = S->nodes;
     S->quad.clear();
-    S->leafParent.assign(std::max<size_t>(1, S->primIds.size()), -1);
     S->quadRootRef = binRef(0);
+    S->quadStackNeed = 0;
     if (L.empty() || L[0].nPrimitives > 0) return;
     std::vector<int32_t> qid(L.size(), -1);
     int nQuad = 0;
@@ -119,19 +119,26 @@ void build_quad_nodes(HostScene* S, Ref&& binRef) {
         std::memcpy(&w[24], refs, 16);
         int32_t meta = (int32_t)L[i].axis | axes[0] << 2 | axes[1] << 4 | mask << 8;
         std::memcpy(&w[28], &meta, 4);
-        // parent links for the backtracking traversal (pbr_device.h traverse_quad): every slot's
-        // child knows (this node, slot); quad children in w[29], leaves in leafParent[first slot]
+    }
+    // Stack need of the quad walk: entering one slot of node Q pushes at most the other valid
+    // slots, which stay on the stack while any of Q's subtrees is walked, so need(Q) = (valid
+    // slots − 1) + max need of its quad children.  Children follow their parent in preorder.
+    std::vector<int> need(nQuad, 0);
+    for (size_t k = order.size(); k-- > 0;) {
+        const int i = order[k];
+        const float* w = &S->quad[(size_t)qid[i] * 32];
+        int32_t refs[4], meta;
+        std::memcpy(refs, &w[24], 16);
+        std::memcpy(&meta, &w[28], 4);
+        int valid = 0, deeper = 0;
         for (int s = 0; s < 4; ++s) {
-            if (!((mask >> s) & 1)) continue;
-            const int32_t link = qid[i] << 2 | s;
-            if (refs[s] < 0) S->leafParent[refs[s] & 0x7fffffff] = link;
-            else std::memcpy(&S->quad[(size_t)refs[s] * 32 + 29], &link, 4);
+            if (!((meta >> (8 + s)) & 1)) continue;
+            ++valid;
+            if (refs[s] >= 0) deeper = std::max(deeper, need[refs[s]]);
         }
+        need[qid[i]] = valid - 1 + deeper;
     }
-    {
-        const int32_t none = -1;
-        std::memcpy(&S->quad[29], &none, 4);   // the root quad node (qid 0, preorder)
-    }
+    S->quadStackNeed = need[qid[0]];
     S->quadRootRef = qid[0];
 }
 
@@ -143,7 +150,16 @@ void build_wide_nodes(HostScene* S) {
     const std::vector<LinearBVHNode>& L = S->nodes;
     S->wide.clear();
     S->rootRef = 0;
+    S->binaryStackNeed = 0;
     if (L.empty()) return;
+    {   // interior levels on the deepest root-to-leaf path (the binary walk pushes one far child per level)
+        std::vector<int> depth(L.size(), 0);
+        for (size_t i = 0; i < L.size(); ++i) {   // preorder: a parent precedes its children
+            if (L[i].nPrimitives > 0) continue;
+            depth[i + 1] = depth[L[i].offset] = depth[i] + 1;
+            S->binaryStackNeed = std::max(S->binaryStackNeed, depth[i] + 1);
+        }
+    }
     std::vector<int> rank(L.size(), -1);
     int nInterior = 0;
     for (size_t i = 0; i < L.size(); ++i)

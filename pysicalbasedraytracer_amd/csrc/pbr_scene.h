@@ -55,7 +55,10 @@ struct HostScene {
     int32_t quadRootRef = 0;
     std::vector<float> primBounds;          // 6 floats (lo, hi) per primitive in prims order: GeometricPrimitive::WorldBound
     std::vector<int32_t> slotOf;            // prims index → BVH slot
-    std::vector<int32_t> leafParent;        // per primitive slot that starts a leaf: parentQuad << 2 | raw slot, -1 at the root
+    // traversal stack entries the tree can need at most (pbr_layout.h kTraversalStack): the binary
+    // walk's (one per interior level on the deepest root-to-leaf path) and the quad walk's (per quad
+    // node on a path, its valid slots minus the one entered)
+    int binaryStackNeed = 0, quadStackNeed = 0;
     InfiniteHost inf;                       // the InfiniteAreaLight, if any (pbr_infinite.cpp)
     std::vector<TexDev> textures;           // ImageTextures (level 0 + mapping)
     std::vector<float> texTexels;           // their texels, 4 floats each

@@ -191,6 +191,7 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 #define PBR_REFILL_OCC_TR 6
 #endif
 constexpr int kRefill = PBR_REFILL;
+static_assert(kRefill >= 1 && kRefill <= 64, "refill threshold: idle lanes of a 64-wide wave");
 // LDS short-stack entries of the camera kernels.  They have no segment scan, so 7 workgroups per CU
 // would fit 10 entries (20 KB): C2's camera kernel then took 8.95 → 8.02 ms/frame, but the other
 // lane's extend, sharing the CUs, 5.28 → 6.75 and the frame 17.7 → 18.0 ms — kept at 6.
@@ -212,7 +213,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
     int* lref;
     float* lt;
     trav_lds<SHORT>(&lref, &lt);
-    constexpr int PRIV = 64 - SHORT;
+    constexpr int PRIV = kTraversalStack - SHORT;
     int stackRef[PRIV];
     float stackT[PRIV];
     int cursor = 0;              // wave-uniform: the next ray of the wave's sequence
@@ -229,7 +230,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
     while (true) {
         const unsigned long long idle = __ballot(!have);
         const int nIdle = __popcll(idle);
-        if (nIdle >= (kRefill > 0 ? kRefill : 64) && rayOf(cursor) < n) {   // wave-uniform
+        if (nIdle >= kRefill && rayOf(cursor) < n) {   // wave-uniform
             if (!have) {
                 const int i = rayOf(cursor + __popcll(idle & below));
                 if (i < n) {
@@ -294,7 +295,10 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             const float tM = r.tMax;
             const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
                        p3 = q.k[3] && q.t[3] < tM;
-            if ((p0 | p1 | p2 | p3) && sp <= 64 - 3) {
+            if ((p0 | p1 | p2 | p3) && sp > kQuadStackLimit) {   // unreachable (upload check): end the walk
+                atomicOr(S.guard, kGuardStack);
+                done = true;
+            } else if (p0 | p1 | p2 | p3) {
                 const int first = p0 ? 0 : (p1 ? 1 : (p2 ? 2 : 3));
                 auto push = [&](int ref, float t) {
                     if (SHORT && sp < SHORT) { lref[sp * 256] = ref; if (!ANY) lt[sp * 256] = t; }
@@ -651,31 +655,8 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
-    // Whitted's shadow rays keep the plain loop: lane refill measured 5.45 → 5.90 ms/frame on C2
-    // (refill 16), 5.40 (refill 32)
-    if constexpr (false && kRefill > 0 && SHORT > 0 && kQuadTraversal) {
-        traverse_stream<true, SHORT>(
-            W.P.S, n,
-            [&](int i, int* key) {
-                const int q = seg_pos(W.shadowSegCap, i);
-                *key = q;
-                const float4 o = W.so[q], d = W.sd[q];
-                return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
-            },
-            [&](int q, bool hit, const Ray&, const HitRec&) {
-                if (W.prof) atomicAdd(W.prof + KP_WF_SHADOW * kProfFields + 1, (unsigned long long)(hit ? 0 : 1));
-                if (!hit) {
-                    const int id = W.sid[q];
-                    const float4 cc = W.sc[q];
-                    const size_t ri = (size_t)__float_as_int(W.sd[q].w) * W.cap + id;
-                    float4 A = W.recA[ri];
-                    A.x = A.x + cc.x; A.y = A.y + cc.y; A.z = A.z + cc.z;
-                    W.recA[ri] = A;
-                }
-            },
-            W.prof, KP_WF_SHADOW);
-        return;
-    }
+    // Whitted's shadow rays keep the plain loop: lane refill (traverse_stream) measured 5.45 → 5.90
+    // ms/frame on C2 (refill 16), 5.40 (refill 32)
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.shadowSegCap, i);
         float4 o = W.so[q], d = W.sd[q];

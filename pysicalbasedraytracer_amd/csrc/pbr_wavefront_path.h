@@ -80,45 +80,9 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
     W.sampleIndex[q] = st.index;   // the level-0 state (L = 0, beta = 1, etaScale = 1) is implied
 }
 
-// Shading-event sort inside a workgroup (PBR_SHADE_SORT).  A wave that holds events of several
-// materials runs each material's BSDF code for its lanes in turn; past the camera level the paths
-// have scattered and neighbouring queue entries hit different materials (C4's glass / metal /
-// plastic dragons, C5's medium and surfaces).  Each iteration the 256 queue positions of a
-// workgroup are ordered by a key — miss, in-medium ray, or the hit's material — with a stable
-// ballot counting sort in LDS, and thread t shades the t-th position of that order, so waves are
-// mostly one material.  Every event's result goes to its own records and queue entries, so the
-// frame is bit-identical to the unsorted order.  Measured and left off: C4 7711 → 7865 ms,
-// C5 1373 → 1429, C3 269.7 → 270.8 (the barriers and key loads cost more than the divergence).
-#ifndef PBR_SHADE_SORT
-#define PBR_SHADE_SORT 0
-#endif
-constexpr int kSortKeys = 18;   // miss, medium, 16 material classes (material index mod 16)
-__device__ __forceinline__ int shade_sort(int q, bool active, int key) {
-    __shared__ int s_cnt[4][kSortKeys];
-    __shared__ int s_off[4][kSortKeys];
-    __shared__ int s_q[256];
-    const int lane = (int)__lane_id(), w = (int)threadIdx.x >> 6;
-    if (!active) key = kSortKeys - 1;   // inactive threads last (their positions are not read)
-    const unsigned long long below = (1ull << lane) - 1ull;
-    int rank = 0;
-    for (int k = 0; k < kSortKeys; ++k) {
-        const unsigned long long m = __ballot(key == k);
-        if (key == k) rank = __popcll(m & below);
-        if (lane == 0) s_cnt[w][k] = __popcll(m);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {   // key-major, then wave: a stable order
-        int o = 0;
-        for (int k = 0; k < kSortKeys; ++k)
-            for (int ww = 0; ww < 4; ++ww) { s_off[ww][k] = o; o += s_cnt[ww][k]; }
-    }
-    __syncthreads();
-    s_q[s_off[w][key] + rank] = active ? q : -1;
-    __syncthreads();
-    const int r = s_q[threadIdx.x];
-    __syncthreads();   // s_q is rewritten by the next iteration
-    return r;
-}
+// (A workgroup-local stable sort of each iteration's 256 shading events by miss / medium / material
+// before shading was measured and removed: bit-identical, but C4 7711 → 7865 ms, C5 1373 → 1429,
+// C3 269.7 → 270.8 — its barriers and key loads cost more than the divergence they removed.)
 
 // One bounce of PathIntegrator::Li for every queued ray.
 // Waves per SIMD: 3 for either lobe set (all lobes, C4: 2 → 9.58 s, 3 → 8.86 s, 4 → 9.32 s)
@@ -149,18 +113,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
     const int base = wf_block() * W.segCap;
     for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
         const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-        bool active = i < n;
-        int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
-        if (PBR_SHADE_SORT && !level0) {   // camera-level waves hold one pixel's samples: coherent already
-            int key = 0;
-            if (active) {
-                const int slot = __float_as_int(W.cur.hit[q].x);
-                key = slot < 0 ? 0 : 2 + (S.primInfo[slot].y & 15);
-            }
-            q = shade_sort(q, active, key);
-            active = q >= 0;
-            if (!active) q = 0;
-        }
+        const bool active = i < n;
+        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
         // Two phases around the light-estimate pushes: the estimate's record, shadow and probe rays
         // are written as soon as they exist, so their registers are free during the path's BSDF
         // sample; only the record's target (the continuation's position) is written at the end.

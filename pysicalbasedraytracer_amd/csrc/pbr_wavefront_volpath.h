@@ -65,19 +65,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
     const int base = wf_block() * W.segCap;
     for (int it = 0; it < nIter; ++it) {
         const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-        bool active = i < n;
-        int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
-        if (PBR_SHADE_SORT && !level0) {   // rays inside a medium, misses, then by the hit's material
-            int key = 0;
-            if (active) {
-                const int slot = __float_as_int(W.cur.hit[q].x);
-                const int medium = ((__float_as_int(W.cur.d[q].w) >> 24) & 0xff) - 1;
-                key = medium >= 0 ? 1 : (slot < 0 ? 0 : 2 + (S.primInfo[slot].y & 15));
-            }
-            q = shade_sort(q, active, key);
-            active = q >= 0;
-            if (!active) q = 0;
-        }
+        const bool active = i < n;
+        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
         // Two phases around the light-estimate pushes (as k_wfp_shade): the record, the transmittance
         // walk and the probe ray are written before the path's phase-function / BSDF sample.
         bool pushTr = false, pushProbe = false, pushDirect = false, pushNext = false;

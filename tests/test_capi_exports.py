@@ -55,3 +55,18 @@ def test_null_arguments_are_rejected():
     assert lib.pbr_hip_li(None, None, 1, None, None, 0, None) == capi.PBR_E_INVALID
     assert lib.pbr_hip_set_profiling(None, 1) == capi.PBR_E_INVALID
     assert lib.pbr_hip_get_profile(None, None, 0, None) == capi.PBR_E_INVALID
+
+
+def test_release_library_reads_no_environment():
+    """The shipped library has one measured schedule (include/pbr_hip.h pbr_hip_set_schedule is the
+    only run-time switch): it imports no getenv, and it is not a development-knob build."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", capi.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert not [l for l in out.splitlines() if "getenv" in l], "libpbr_hip.so imports getenv"
+    build = capi.load_library().pbr_hip_build_info().decode()
+    assert "dev-knobs" not in build, build
+
+
+def test_schedule_arguments_are_validated():
+    lib = capi.load_library()
+    assert lib.pbr_hip_set_schedule(None, None) == capi.PBR_E_INVALID

@@ -103,9 +103,11 @@ def test_ragged_tiles_and_single_pixel_tiles(hip):
 
 @pytest.mark.parametrize("config", ["C3", "C5"])
 def test_full_size_path_volpath_properties(hip, config):
-    """BASELINE sizes of C3 (1080p, 256 spp, Path, Sobol) and C5 (1080p, 512 spp, VolPath):
-    finite, non-negative, deterministic frames; 24 spot pixels within the L∞ tolerance of the
-    oracle (same sampler indices: the pixels are rendered as one-pixel tiles on the CPU)."""
+    """BASELINE sizes of C3 (1080p, 256 spp, Path, Sobol — the sampler the reference lacks, F3, so
+    the oracle is the only pin) and C5 (1080p, 512 spp, VolPath) on the default (benchmarked)
+    schedule: finite, non-negative, deterministic frames, and 64 spot pixels against the oracle
+    (same sampler indices: one-pixel tiles on the CPU) — L∞ within the north_star tolerance, the
+    8-bit output identical wherever the float pixel is, and at least 95% of the pixels bit-exact."""
     s, rd = scenes.CONFIGS[config]()
     W, H = rd.camera.width, rd.camera.height
     hip.upload(s)
@@ -113,12 +115,14 @@ def test_full_size_path_volpath_properties(hip, config):
     assert g.shape == (W * H, 3) and np.isfinite(g).all() and (g >= 0).all()
     assert st.samples == W * H * rd.spp
     rng = np.random.default_rng(7)
-    picks = rng.integers(0, W * H, 24)
+    picks = rng.choice(W * H, 64, replace=False)
     tiles = [(int(p % W), int(p // W), int(p % W) + 1, int(p // W) + 1) for p in picks]
     rdt = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
                              rd.sampler, tiles=tiles)
     c, c8, _ = O.render(s, rdt)
-    assert np.abs(g[picks] - c).max() <= 1e-3
+    linf, exact = assert_parity(g[picks], c, g8[picks], c8)
+    assert exact >= 0.95, f"{config}: only {exact:.3f} of the pixels bit-identical to the oracle"
+    print(f"{config}: L∞ {linf:.3g}, bit-identical {exact:.3f}")
     again, _, _ = hip.render(rdt)
     assert np.array_equal(again.view(np.uint32), g[picks].view(np.uint32))
 
@@ -137,7 +141,7 @@ def test_spp_beyond_one_finish_tile(hip, integrator):
     assert_parity(g, c, g8, c8)
 
 
-def test_deep_whitted_mirror_box(hip, monkeypatch):
+def test_deep_whitted_mirror_box(hip):
     """Two facing mirrors bounce camera rays until Whitted's depth limit: the wavefront schedule
     (up to 16 levels) and the megakernel (up to 64) agree bit for bit and with the oracle, and a
     deeper maxDepth is refused rather than truncated."""
@@ -157,9 +161,9 @@ def test_deep_whitted_mirror_box(hip, monkeypatch):
         g, g8, _ = hip.render(rd)
         c, c8, _ = O.render(s, rd)
         assert_parity(g, c, g8, c8)
-        monkeypatch.setenv("PBR_WAVEFRONT", "0")
+        hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
         mk, _, _ = hip.render(rd)
-        monkeypatch.delenv("PBR_WAVEFRONT")
+        hip.set_schedule()
         assert np.array_equal(mk.view(np.uint32), g.view(np.uint32)), depth
     with pytest.raises(RuntimeError):
         hip.render(scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 1, 65))

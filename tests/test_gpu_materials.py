@@ -97,7 +97,7 @@ def test_reversed_orientation_mirrored_transform(hip):
 
 
 @pytest.mark.parametrize("integrator", [capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH])
-def test_material_less_medium_interface(hip, integrator, monkeypatch):
+def test_material_less_medium_interface(hip, integrator):
     """A material-less sphere bounding a homogeneous medium (pbrt's interface idiom): rays cross it
     without a bounce (PathIntegrator.cpp:70-75, VolPathIntegrator.cpp:77-82); the wavefront
     schedule equals the megakernel bit for bit."""
@@ -112,7 +112,7 @@ def test_material_less_medium_interface(hip, integrator, monkeypatch):
     cam = scenes.camera(48, 32, CAM["eye"], CAM["look"])
     rd = scenes.render_desc(cam, integrator, 8, 6)
     g = check(hip, s, rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, _, _ = hip.render(rd)
     assert np.array_equal(mk.view(np.uint32), g.view(np.uint32))
 
@@ -135,7 +135,7 @@ def nested_shells(n, r0=0.05, r1=0.6, medium=True, center=(0.0, 0.1, 0.2)):
 
 
 @pytest.mark.parametrize("integrator", [capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH])
-def test_many_material_less_crossings(hip, integrator, monkeypatch):
+def test_many_material_less_crossings(hip, integrator):
     """20 nested material-less shells: a path through the centre crosses 40 surfaces before its
     first bounce, more than the 32 extra levels the wavefront schedules up front.  The schedule
     keeps extending while continuations are queued, so it equals the megakernel (which loops
@@ -144,12 +144,12 @@ def test_many_material_less_crossings(hip, integrator, monkeypatch):
     cam = scenes.camera(40, 28, CAM["eye"], CAM["look"])
     rd = scenes.render_desc(cam, integrator, 4, 5)
     g = check(hip, s, rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, _, _ = hip.render(rd)
     assert np.array_equal(mk.view(np.uint32), g.view(np.uint32))
 
 
-def test_transmittance_walk_bound_fails_loudly(hip, monkeypatch):
+def test_transmittance_walk_bound_fails_loudly(hip):
     """300 nested shells centred on a point of the patch: a shadow ray from there to the light
     crosses 300 interfaces (VisibilityTester::Tr), past the 256-interface safety bound, so the
     render fails with an error (both schedules) instead of returning a truncated transmittance.
@@ -180,7 +180,7 @@ def test_transmittance_walk_bound_fails_loudly(hip, monkeypatch):
                           stream=stream.cuda_stream, sync=False)
     g2, _, _ = hip.render(scenes.render_desc(cam, capi.INTEGRATOR_PATH, 2, 3))   # reported once
     assert np.array_equal(g2.view(np.uint32), g.view(np.uint32))
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     with pytest.raises(RuntimeError, match="transmittance walk"):
         hip.render(rd)
 

@@ -221,14 +221,16 @@ def test_benchmarked_c2_frame_bit_exact(hip):
     assert np.array_equal(g8[picks], c8)
 
 
-def test_whitted_multichunk_two_lanes(hip, monkeypatch):
-    """Single-light wavefront Whitted over many chunks (PBR_CHUNK_LOG2=16: 2^16-sample chunks, so
-    a 160×90×32 frame is 8 chunks alternating over the two lanes and their streams) against the
-    oracle over the whole frame, float and RGBA8 bit for bit, and equal to the one-chunk render."""
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_whitted_multichunk_two_lanes(hip, lanes):
+    """Single-light wavefront Whitted over many chunks (2^16-sample chunks, so a 160×90×32 frame is
+    8 chunks alternating over the lanes and their streams) against the oracle over the whole frame,
+    float and RGBA8 bit for bit, and equal to the one-chunk render."""
     s, rd = scenes.config_c2(160, 90, 32, mesh=small_dragon(64))
     hip.upload(s)
+    hip.set_schedule(chunk_log2=25)   # one chunk
     one, one8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_CHUNK_LOG2", "16")
+    hip.set_schedule(chunk_log2=16, lanes=lanes)
     g, g8, _ = hip.render(rd)
     c, c8, _ = O.render(s, rd)
     assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
@@ -248,30 +250,29 @@ def test_errors_fail_loudly(hip):
     fresh.close()
 
 
-def test_wavefront_equals_megakernel(hip, monkeypatch):
+def test_wavefront_equals_megakernel(hip):
     """The wavefront Whitted schedule and the megakernel produce identical bits."""
     s, rd = scenes.config_c2(160, 90, 8, mesh=small_dragon(64))
     hip.upload(s)
-    monkeypatch.setenv("PBR_WAVEFRONT", "1")
+    hip.set_schedule()
     wf, wf8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32))
     assert np.array_equal(wf8, mk8)
 
 
-def test_fused_level0_shade_equals_camera_kernel(hip, monkeypatch):
+def test_fused_level0_shade_equals_camera_kernel(hip):
     """The level-0 shade that traces its own camera rays (multi-chunk frames) = the camera kernel
     + level-0 queue = the megakernel, bit for bit.  64 spp: a camera wave is one pixel's samples;
     the centre column's pixels hold rays of two direction-sign octants (two packet walks)."""
     s, rd = scenes.config_c2(160, 90, 64, mesh=small_dragon(64))
     hip.upload(s)
-    monkeypatch.setenv("PBR_CHUNK_LOG2", "17")   # 8 chunks over the lanes: the fused schedule
-    monkeypatch.setenv("PBR_FUSED_CAMERA", "1")
+    hip.set_schedule(chunk_log2=17, fuse_camera=capi.FUSE_ON)   # 8 chunks over the lanes
     fu, fu8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_FUSED_CAMERA", "0")
+    hip.set_schedule(chunk_log2=17, fuse_camera=capi.FUSE_OFF)
     ck, ck8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(fu.view(np.uint32), ck.view(np.uint32)) and np.array_equal(fu8, ck8)
     assert np.array_equal(fu.view(np.uint32), mk.view(np.uint32)) and np.array_equal(fu8, mk8)
@@ -302,7 +303,7 @@ def test_sobol_random_queries_bit_exact(hip):
         assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
 
 
-def test_sobol_wide_index_render(hip, monkeypatch):
+def test_sobol_wide_index_render(hip):
     """A Sobol Path render whose sample indices need more than 32 bits (resolution 2^12 from a
     4096-pixel-wide raster, 512 spp → 2^33) through both schedules, against the oracle.  A tile
     keeps the frame small; the sampler still works at the full raster's resolution."""
@@ -314,7 +315,7 @@ def test_sobol_wide_index_render(hip, monkeypatch):
     assert st.samples == 16 * 2 * 512
     c, c8, _ = O.render(s, rd2)
     compare(g, c, g8, c8)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, mk8, _ = hip.render(rd2)
     assert np.array_equal(g.view(np.uint32), mk.view(np.uint32))
 
@@ -342,11 +343,21 @@ def test_sobol_caller_matrices_and_pow2_spp(hip):
     assert st.samples == 64 * 40 * 8
 
 
+# Chunkings of the small Path/VolPath frames below (≈ 33-41 k samples): one chunk (the default
+# there), 2^12-sample chunks over three lanes (8-10 chunks: lanes 1-2's buffers, path state and
+# direct records carried over chunks), and 2^10-sample chunks (33-41 chunks: the balanced chunk size
+# that frames of 24 or more chunks get, as C4's 254 chunks do).
+SCHEDULES = {"one_chunk": {}, "c12_3lanes": {"chunk_log2": 12, "lanes": 3},
+             "c10_balanced": {"chunk_log2": 10, "lanes": 3}, "c12_2lanes": {"chunk_log2": 12, "lanes": 2}}
+
+
+@pytest.mark.parametrize("sched", sorted(SCHEDULES))
 @pytest.mark.parametrize("config", ["c3", "c4", "c3_power"])
-def test_wavefront_path_equals_megakernel(hip, monkeypatch, config):
+def test_wavefront_path_equals_megakernel(hip, config, sched):
     """The wavefront Path schedule (shade / shadow / probe / resolve / extend) and the recursive
     megakernel produce identical bits: matte + area light with Sobol (C3), glass/metal/plastic
-    with all lobe kinds (C4), and the power light distribution."""
+    with all lobe kinds (C4), and the power light distribution — as one chunk and as many chunks
+    over two or three lanes."""
     if config == "c4":
         s, rd = scenes.config_c4(96, 54, 8, mesh=small_dragon(40))
     else:
@@ -355,22 +366,24 @@ def test_wavefront_path_equals_megakernel(hip, monkeypatch, config):
             rd = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold,
                                     capi.LIGHTS_POWER, capi.SAMPLER_HALTON)
     hip.upload(s)
-    monkeypatch.setenv("PBR_WAVEFRONT", "1")
+    hip.set_schedule(**SCHEDULES[sched])
     wf, wf8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
     assert np.array_equal(wf8, mk8)
 
 
-def test_wavefront_volpath_equals_megakernel(hip, monkeypatch):
+@pytest.mark.parametrize("sched", sorted(SCHEDULES))
+def test_wavefront_volpath_equals_megakernel(hip, sched):
     """The wavefront VolPath schedule (medium sampling, HG phase, transmittance walks through the
-    glass dragon's medium interface) matches the megakernel bit for bit (C5 shape)."""
+    glass dragon's medium interface) matches the megakernel bit for bit (C5 shape), as one chunk
+    and as many chunks over two or three lanes."""
     s, rd = scenes.config_c5(80, 45, 8, mesh=small_dragon(40))
     hip.upload(s)
-    monkeypatch.setenv("PBR_WAVEFRONT", "1")
+    hip.set_schedule(**SCHEDULES[sched])
     wf, wf8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
     assert np.array_equal(wf8, mk8)
@@ -404,12 +417,11 @@ def test_async_device_frames(hip):
 
 
 @pytest.mark.parametrize("lights", ["sky+point", "area+points", "none"])
-def test_multilight_whitted_wavefront(hip, monkeypatch, lights):
+def test_multilight_whitted_wavefront(hip, lights):
     """Whitted with several lights (or none) on the wavefront schedule (k_wf_shade_ml: per-light
     contributions and visibility, summed in light order by the fold) equals the megakernel bit for
     bit and the oracle within the tolerance.  2^16-sample chunks make the frame four chunks over
     the two lanes, so records left by an earlier chunk must not leak into a later one."""
-    monkeypatch.setenv("PBR_CHUNK_LOG2", "16")
     s, rd = scenes.config_c2(160, 90, 16, mesh=small_dragon(40), sky=scenes.procedural_sky(64, 32))
     if lights == "sky+point":
         s.point_light((1.0, 2.0, 1.5), (6.0, 5.0, 4.0))
@@ -422,9 +434,9 @@ def test_multilight_whitted_wavefront(hip, monkeypatch, lights):
     else:
         s.lights.clear()
     hip.upload(s)
-    monkeypatch.setenv("PBR_WAVEFRONT", "1")
+    hip.set_schedule(chunk_log2=16)
     wf, wf8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
     c, c8, _ = O.render(s, rd)

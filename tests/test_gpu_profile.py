@@ -4,7 +4,7 @@ profiling must not change the image."""
 import numpy as np
 import pytest
 
-from pysicalbasedraytracer_amd import HipRenderer, scenes
+from pysicalbasedraytracer_amd import HipRenderer, capi, scenes
 
 
 @pytest.fixture(scope="module")
@@ -20,10 +20,10 @@ def _c2_small():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fused", ["0", "1"])
-def test_whitted_profile_counts_are_consistent(hip, monkeypatch, fused):
-    monkeypatch.setenv("PBR_CHUNK_LOG2", "16")   # several chunks over the lanes
-    # fused: the level-0 shade traces its own camera rays (multi-chunk frames, the default)
-    monkeypatch.setenv("PBR_FUSED_CAMERA", fused)
+def test_whitted_profile_counts_are_consistent(hip, fused):
+    # several chunks over the lanes; fused: the level-0 shade traces its own camera rays
+    # (multi-chunk frames, the default)
+    hip.set_schedule(chunk_log2=16, fuse_camera=capi.FUSE_ON if fused == "1" else capi.FUSE_OFF)
     s, rd = _c2_small()
     hip.upload(s)
     ref, ref8, _ = hip.render(rd)

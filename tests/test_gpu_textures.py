@@ -44,12 +44,12 @@ def test_textured_scene_device_equals_oracle(hip, integrator):
 
 
 @pytest.mark.parametrize("integrator", [capi.INTEGRATOR_WHITTED, capi.INTEGRATOR_PATH, capi.INTEGRATOR_VOLPATH])
-def test_textured_wavefront_equals_megakernel(hip, monkeypatch, integrator):
+def test_textured_wavefront_equals_megakernel(hip, integrator):
     s, rd = textured_scene(integrator, 128, 72, 8, 6)
     hip.upload(s)
-    monkeypatch.setenv("PBR_WAVEFRONT", "1")
+    hip.set_schedule()
     wf, wf8, _ = hip.render(rd)
-    monkeypatch.setenv("PBR_WAVEFRONT", "0")
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
     mk, mk8, _ = hip.render(rd)
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
     assert np.array_equal(wf8, mk8)

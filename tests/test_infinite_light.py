@@ -151,15 +151,15 @@ def test_infinite_light_device_vs_oracle(hip, case):
 
 
 @pytest.mark.gpu
-def test_infinite_light_wavefront_equals_megakernel(hip, monkeypatch):
+def test_infinite_light_wavefront_equals_megakernel(hip):
     cam = scenes.camera(64, 40, CAM["eye"], CAM["look"])
     for integ, mat in ((capi.INTEGRATOR_WHITTED, lambda sc: sc.matte((0.1, 0.8, 0.2))),
                        (capi.INTEGRATOR_PATH, lambda sc: sc.plastic())):
         s = dragon_scene(mat)
         rd = scenes.render_desc(cam, integ, 8, 6)
         hip.upload(s)
-        monkeypatch.setenv("PBR_WAVEFRONT", "1")
+        hip.set_schedule()
         wf, _, _ = hip.render(rd)
-        monkeypatch.setenv("PBR_WAVEFRONT", "0")
+        hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
         mk, _, _ = hip.render(rd)
         assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())

@@ -88,3 +88,40 @@ def test_device_matches_reference_fullsize(hip, name):
     got, got8, _ = hip.render(rd)
     linf, exact = check(name, got, got8, ref, ref8)
     print(f"{name}: L∞ {linf:.3g}, bit-identical {exact:.3f}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_production_schedule_matches_reference_fullsize(hip, name):
+    """The frame exactly as bench.py renders it — the bench's own scene (scenes.CONFIGS), the whole
+    raster as one tile, the default schedule (C2: 4 chunks over 3 lanes with the fused level-0
+    shade; C3: 8 chunks; C4: 254 balanced chunks; C5: 32 chunks), asynchronous into device buffers
+    on a caller stream — and then the fixture's 64 pixels picked out of it and held to the same
+    gates against the reference as the one-pixel-tile renders above (Integrator.cpp:286-344).
+    C3 runs on Halton here (the reference has no Sobol sampler, F3); its Sobol frame is checked
+    against the oracle in tests/test_gpu_edges.py."""
+    import torch
+    from pysicalbasedraytracer_amd import scenes
+    s_fix, rd_fix = CASES[name]
+    ref, ref8 = fixture(name, s_fix, rd_fix)
+    config = {"c2": "C2", "c3_halton": "C3", "c4": "C4", "c5": "C5"}[name]
+    s, rd = scenes.CONFIGS[config]()
+    # the bench's scene is the fixture's scene (same descriptors and arrays)
+    assert RS.scene_digest(s, rd_fix) == FIX["cases"][name]["digest"]
+    W, H = rd.camera.width, rd.camera.height
+    assert (W, H, rd.spp, rd.max_depth) == (rd_fix.camera.width, rd_fix.camera.height, rd_fix.spp, rd_fix.max_depth)
+    full = scenes.render_desc(rd.camera, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                              rd_fix.sampler, tiles=[(0, 0, W, H)])
+    hip.upload(s)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    rgb = torch.empty((W * H, 3), dtype=torch.float32, device=dev)
+    rgba = torch.empty((W * H, 4), dtype=torch.uint8, device=dev)
+    assert hip.render_device(full, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False) is None
+    hip.sync()
+    torch.cuda.synchronize(dev)
+    idx = torch.tensor([t[1] * W + t[0] for t in FIX["cases"][name]["tiles"]], dtype=torch.long, device=dev)
+    got = rgb.index_select(0, idx).cpu().numpy()
+    got8 = rgba.index_select(0, idx).cpu().numpy()
+    linf, exact = check(name, got, got8, ref, ref8)
+    print(f"{name} production schedule: L∞ {linf:.3g}, bit-identical {exact:.3f}")
