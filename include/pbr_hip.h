@@ -203,6 +203,15 @@ typedef struct pbr_scene_desc {
     int n_textures;
     const pbr_texture_desc* textures;
     int split_method;           /* pbr_split_method (BVHAccel.h:18); Middle / EqualCounts build on the host */
+    /* A BVHAccel already built over the primitives IN THE ORDER GIVEN HERE — the reference's own
+     * flattened node array (LinearBVHNode, BVHAccel.cpp:46-55, 32 B each), as a Scene's aggregate
+     * holds it after its constructor reordered `primitives` into leaf order.  The upload then uses
+     * that tree as is instead of building one: the traversal tests the reference's boxes in the
+     * reference's order.  It is checked to be a preorder tree whose leaves hold primitives 0..n-1
+     * in order, each leaf box the union of its primitives' bounds (PBR_E_INVALID otherwise).
+     * NULL = build one (split_method, max_prims_in_node). */
+    const void* bvh_nodes;
+    int n_bvh_nodes;
 } pbr_scene_desc;
 
 /* CreatePerspectiveCamera (Camera/Perspective.cpp:84-104) inputs. */

@@ -1537,6 +1537,8 @@ static int mat_index(const pbr_scene_desc* d, int m) {
 
 static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
     if (!d || d->abi_version != PBR_HIP_ABI_VERSION) throw std::runtime_error("bad scene desc");
+    // the restatement always builds its own BVHAccel (a caller-built tree is a product upload option)
+    if (d->bvh_nodes) throw std::runtime_error("the oracle builds its own BVH (bvh_nodes unsupported)");
     std::unique_ptr<Scene> s(new Scene);
     std::vector<Prim> prims;
     int ns = d->n_shapes;

@@ -453,6 +453,13 @@ int ref_render_frame(const pbr_scene_desc* sd, const pbr_render_desc* rd, uint8_
     }
 }
 
+// The frame arena of ref_render_frame for callers that run the reference's own Integrator::Render
+// themselves (oracle/ref/refbind_scenes.cpp): on before Render, off after it.
+void ref_frame_arena(int on) {
+    g_frameArena = on != 0;
+    if (!on && tl_frame) { arena_off(); tl_frame = false; }
+}
+
 // BVHAccel's flattened nodes (32-B LinearBVHNode, BVHAccel.cpp:46-55) and the original index of
 // each primitive in BVH order; NULL buffers query the counts.
 int ref_build_bvh(const pbr_scene_desc* sd, void* nodes_out, int* n_nodes, int32_t* prim_ids_out, int* n_prims) {

@@ -134,6 +134,8 @@ class SceneDesc(C.Structure):
         ("n_textures", C.c_int),
         ("textures", C.POINTER(TextureDesc)),
         ("split_method", C.c_int),
+        ("bvh_nodes", C.c_void_p),
+        ("n_bvh_nodes", C.c_int),
     ]
 
 

@@ -396,6 +396,53 @@ void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vec
     interior_bounds_from_children(nodes);
 }
 
+// A caller-built BVHAccel (pbr_scene_desc::bvh_nodes): the reference's flattened tree over the
+// primitives in the given (leaf) order.  Checked before use: a preorder tree (first child right after
+// its parent, the second at `offset`), every node reached once, leaves covering primitives 0..n-1
+// in order, each leaf box bit-equal to the union of its primitives' bounds (BVHAccel.cpp:189-196
+// computes it with the same Union as Triangle::WorldBound here, so a flattening that moved a vertex
+// fails).  Interior boxes are kept as given.
+void adopt_bvh(const pbr_scene_desc* d, const std::vector<float>& primBounds, std::vector<LinearBVHNode>* nodes,
+               std::vector<int32_t>* primIds) {
+    const size_t np = primBounds.size() / 6;
+    if (d->n_bvh_nodes <= 0 || (size_t)d->n_bvh_nodes > 2 * np + 1) fail("bvh_nodes: bad node count");
+    const LinearBVHNode* in = static_cast<const LinearBVHNode*>(d->bvh_nodes);
+    nodes->assign(in, in + d->n_bvh_nodes);
+    const std::vector<LinearBVHNode>& L = *nodes;
+    size_t nextPrim = 0;
+    int visited = 0;
+    std::vector<int> stack{0};
+    while (!stack.empty()) {
+        const int i = stack.back();
+        stack.pop_back();
+        if (i < 0 || i >= d->n_bvh_nodes || visited++ >= d->n_bvh_nodes) fail("bvh_nodes: not a tree");
+        const LinearBVHNode& n = L[i];
+        if (n.nPrimitives > 0) {
+            if ((size_t)n.offset != nextPrim || nextPrim + n.nPrimitives > np) fail("bvh_nodes: leaves do not hold the primitives in order");
+            Box b;
+            for (int k = 0; k < n.nPrimitives; ++k) {
+                const float* p = &primBounds[(nextPrim + k) * 6];
+                Box pb;
+                pb.lo = mk(p[0], p[1], p[2]);
+                pb.hi = mk(p[3], p[4], p[5]);
+                if (k == 0) b = pb;
+                else { b.lo = vmin(b.lo, pb.lo); b.hi = vmax(b.hi, pb.hi); }
+            }
+            const float box[6] = {b.lo.x, b.lo.y, b.lo.z, b.hi.x, b.hi.y, b.hi.z};
+            if (std::memcmp(box, n.pMin, 12) != 0 || std::memcmp(box + 3, n.pMax, 12) != 0)
+                fail("bvh_nodes: a leaf box is not its primitives' bounds");
+            nextPrim += n.nPrimitives;
+        } else {
+            if (n.offset <= i + 1 || n.axis > 2) fail("bvh_nodes: bad interior node");
+            stack.push_back(n.offset);   // second child after the first one's subtree (preorder)
+            stack.push_back(i + 1);
+        }
+    }
+    if (visited != d->n_bvh_nodes || nextPrim != np) fail("bvh_nodes: the tree does not cover every node and primitive");
+    primIds->resize(np);
+    for (size_t i = 0; i < np; ++i) (*primIds)[i] = (int32_t)i;
+}
+
 void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* bvh) {
     if (!d) fail("null scene");
     if (d->abi_version != PBR_HIP_ABI_VERSION) fail("abi_version mismatch");
@@ -473,7 +520,8 @@ void build_host_scene(const pbr_scene_desc* d, HostScene* S, const BvhBuildFn* b
     if (d->split_method < PBR_SPLIT_SAH || d->split_method > PBR_SPLIT_EQUAL_COUNTS) fail("unknown split method");
     // the device builder is the SAH one (HLBVH is SAH in the reference); Middle / EqualCounts build here
     const bool sah = d->split_method == PBR_SPLIT_SAH || d->split_method == PBR_SPLIT_HLBVH;
-    if (bvh && sah) (*bvh)(S->primBounds, maxPrims, &S->nodes, &S->primIds);
+    if (d->bvh_nodes) adopt_bvh(d, S->primBounds, &S->nodes, &S->primIds);
+    else if (bvh && sah) (*bvh)(S->primBounds, maxPrims, &S->nodes, &S->primIds);
     else host_build_bvh(S->primBounds, maxPrims, &S->nodes, &S->primIds, d->split_method);
     if (S->primIds.size() != (size_t)np) fail("BVH build returned a wrong primitive count");
     // 3. primitive payloads in BVH order

@@ -339,6 +339,8 @@ def _fields(h, st):
         v = getattr(st, name)
         if isinstance(typ, type) and issubclass(typ, (C._Pointer, C.c_void_p, C.c_char_p)) or typ is C.c_void_p:
             continue
+        if name == "n_bvh_nodes" and v == 0:
+            continue   # added after the fixtures were digested; hashed only when a tree is supplied
         if name == "abi_version":
             # the descriptor layout the fixtures were digested with: ABI v4 added an entry point
             # (pbr_hip_set_schedule), no descriptor field, so scene digests stay comparable
