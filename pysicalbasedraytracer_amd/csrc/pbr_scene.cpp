@@ -397,11 +397,12 @@ void host_build_bvh(const std::vector<float>& primBounds, int maxPrims, std::vec
 }
 
 // A caller-built BVHAccel (pbr_scene_desc::bvh_nodes): the reference's flattened tree over the
-// primitives in the given (leaf) order.  Checked before use: a preorder tree (first child right after
-// its parent, the second at `offset`), every node reached once, leaves covering primitives 0..n-1
-// in order, each leaf box bit-equal to the union of its primitives' bounds (BVHAccel.cpp:189-196
-// computes it with the same Union as Triangle::WorldBound here, so a flattening that moved a vertex
-// fails).  Interior boxes are kept as given.
+// primitives in the given (orderedPrims) order.  Checked before use: a preorder tree (first child
+// right after its parent, the second at `offset`), every node reached once, the leaves' primitive
+// ranges tiling 0..n-1 (recursiveBuild's arguments are evaluated right to left, so preorder leaves
+// need not be in offset order), each leaf box bit-equal to the union of its primitives' bounds
+// (BVHAccel.cpp:189-196 computes it with the same Union as Triangle::WorldBound here, so a flattening
+// that moved a vertex fails).  Interior boxes are kept as given.
 void adopt_bvh(const pbr_scene_desc* d, const std::vector<float>& primBounds, std::vector<LinearBVHNode>* nodes,
                std::vector<int32_t>* primIds) {
     const size_t np = primBounds.size() / 6;
@@ -409,7 +410,8 @@ void adopt_bvh(const pbr_scene_desc* d, const std::vector<float>& primBounds, st
     const LinearBVHNode* in = static_cast<const LinearBVHNode*>(d->bvh_nodes);
     nodes->assign(in, in + d->n_bvh_nodes);
     const std::vector<LinearBVHNode>& L = *nodes;
-    size_t nextPrim = 0;
+    std::vector<unsigned char> covered(np, 0);
+    size_t nCovered = 0;
     int visited = 0;
     std::vector<int> stack{0};
     while (!stack.empty()) {
@@ -418,27 +420,29 @@ void adopt_bvh(const pbr_scene_desc* d, const std::vector<float>& primBounds, st
         if (i < 0 || i >= d->n_bvh_nodes || visited++ >= d->n_bvh_nodes) fail("bvh_nodes: not a tree");
         const LinearBVHNode& n = L[i];
         if (n.nPrimitives > 0) {
-            if ((size_t)n.offset != nextPrim || nextPrim + n.nPrimitives > np) fail("bvh_nodes: leaves do not hold the primitives in order");
+            if (n.offset < 0 || (size_t)n.offset + n.nPrimitives > np) fail("bvh_nodes: a leaf indexes past the primitives");
             Box b;
             for (int k = 0; k < n.nPrimitives; ++k) {
-                const float* p = &primBounds[(nextPrim + k) * 6];
-                Box pb;
-                pb.lo = mk(p[0], p[1], p[2]);
-                pb.hi = mk(p[3], p[4], p[5]);
-                if (k == 0) b = pb;
-                else { b.lo = vmin(b.lo, pb.lo); b.hi = vmax(b.hi, pb.hi); }
+                const size_t p = (size_t)n.offset + k;
+                if (covered[p]++) fail("bvh_nodes: a primitive in two leaves");
+                ++nCovered;
+                const float* pb = &primBounds[p * 6];
+                Box e;
+                e.lo = mk(pb[0], pb[1], pb[2]);
+                e.hi = mk(pb[3], pb[4], pb[5]);
+                if (k == 0) b = e;
+                else b.add(e);
             }
             const float box[6] = {b.lo.x, b.lo.y, b.lo.z, b.hi.x, b.hi.y, b.hi.z};
             if (std::memcmp(box, n.pMin, 12) != 0 || std::memcmp(box + 3, n.pMax, 12) != 0)
                 fail("bvh_nodes: a leaf box is not its primitives' bounds");
-            nextPrim += n.nPrimitives;
         } else {
             if (n.offset <= i + 1 || n.axis > 2) fail("bvh_nodes: bad interior node");
             stack.push_back(n.offset);   // second child after the first one's subtree (preorder)
             stack.push_back(i + 1);
         }
     }
-    if (visited != d->n_bvh_nodes || nextPrim != np) fail("bvh_nodes: the tree does not cover every node and primitive");
+    if (visited != d->n_bvh_nodes || nCovered != np) fail("bvh_nodes: the tree does not cover every node and primitive");
     primIds->resize(np);
     for (size_t i = 0; i < np; ++i) (*primIds)[i] = (int32_t)i;
 }

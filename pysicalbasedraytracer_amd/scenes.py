@@ -453,6 +453,11 @@ class Scene:
         d.materials = C.cast(self._arrays[1], C.POINTER(capi.MaterialDesc))
         d.lights = C.cast(self._arrays[2], C.POINTER(capi.LightDesc))
         d.media = C.cast(self._arrays[3], C.POINTER(capi.MediumDesc))
+        if getattr(self, "bvh_nodes", None) is not None:   # a caller-built BVHAccel (pbr_scene_desc::bvh_nodes)
+            nodes = np.ascontiguousarray(self.bvh_nodes, dtype=np.uint8)
+            self._arrays = self._arrays + (nodes,)
+            d.bvh_nodes = nodes.ctypes.data
+            d.n_bvh_nodes = nodes.size // 32
         return d
 
 

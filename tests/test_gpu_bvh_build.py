@@ -132,3 +132,38 @@ def test_signed_zero_bounds_match_the_oracle(hip):
         gn, gi = hip.get_bvh()
         assert np.array_equal(gi, ci) and np.array_equal(gn, cn), where
     hip.set_bvh_build(capi.BVH_BUILD_DEVICE)
+
+
+def test_upload_adopts_a_caller_built_tree(hip):
+    """pbr_scene_desc::bvh_nodes (the reference-side binding hands over its BVHAccel this way): the
+    primitives in leaf order plus the reference's LinearBVHNode array are used as given — the device's
+    node array is that array, the frame equals the one of the device-built tree over the original
+    order bit for bit — and a tree whose leaf box is not its primitives' bounds is refused."""
+    import oracle_lib as O
+    s, rd = scenes.config_c1(48, 32, 4)
+    m = scenes.dragon_standin(n=24)
+    s = scenes.Scene()
+    s.mesh(m[0], m[1], s.matte((0.3, 0.7, 0.2)))
+    s.point_light((1.0, 2.0, 2.0), (6.0, 6.0, 6.0))
+    cam = scenes.camera(48, 32, (0.0, 0.4, 2.6), (0.0, 0.0, 0.0))
+    rd = scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 4, 5)
+    cn, ci = O.build_bvh(s)
+    hip.upload(s)
+    want, want8, _ = hip.render(rd)
+    leaf = scenes.Scene()
+    leaf.mesh(m[0], np.ascontiguousarray(m[1][ci]), leaf.matte((0.3, 0.7, 0.2)))
+    leaf.point_light((1.0, 2.0, 2.0), (6.0, 6.0, 6.0))
+    leaf.bvh_nodes = cn
+    hip.upload(leaf)
+    gn, gi = hip.get_bvh()
+    assert np.array_equal(gn, cn) and np.array_equal(gi, np.arange(len(ci)))
+    got, got8, _ = hip.render(rd)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)) and np.array_equal(got8, want8)
+    bad = cn.copy().view(np.float32).reshape(-1, 8)
+    rec = np.frombuffer(cn.tobytes(), dtype=[("b", "<f4", 6), ("off", "<i4"), ("np", "<u2"), ("ax", "u1"), ("pad", "u1")])
+    k = int(np.nonzero(rec["np"] > 0)[0][0])
+    bad[k, 0] -= 1.0                               # a leaf box no longer its triangle's bounds
+    leaf.bvh_nodes = bad.view(np.uint8).reshape(-1)
+    with pytest.raises(RuntimeError, match="leaf box"):
+        hip.upload(leaf)
+    hip.upload(s)   # the context stays usable
