@@ -15,11 +15,14 @@
 //  * Render writes the whole W×H frame (the reference's loop renders min(W,H)², finding F1) and
 //    also fills the float buffer (getFCbuffer, F7).
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
+
+#include "../pbr_hip.h"   // pbr_sampler_type (Sampler::DeviceSampler)
 
 struct pbr_hip_ctx;
 struct pbr_scene_desc;
@@ -561,11 +564,39 @@ class PerspectiveCamera : public Camera {   // Camera/Perspective.h
 PerspectiveCamera* CreatePerspectiveCamera(int RasterWidth, int RasterHeight, const Transform& cam2world, Medium* media);
 
 // ---------------------------------------------------------------------------- Sampler/
+// PCG32 (Sampler/RNG.h): pbrt's RNG, the fallback of PixelSampler beyond its sampled dimensions.
+class RNG {
+  public:
+    RNG() : state(0x853c49e6748fea9bULL), inc(0xda3e39cb94b95bdbULL) {}
+    explicit RNG(uint64_t sequenceIndex) { SetSequence(sequenceIndex); }
+    void SetSequence(uint64_t initseq) {
+        state = 0u;
+        inc = (initseq << 1u) | 1u;
+        UniformUInt32();
+        state += 0x853c49e6748fea9bULL;
+        UniformUInt32();
+    }
+    uint32_t UniformUInt32() {
+        const uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        const uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        const uint32_t rot = (uint32_t)(old >> 59u);
+        return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+    }
+    float UniformFloat() { return std::min(0.99999994f, float(UniformUInt32() * 2.3283064365386963e-10f)); }
+
+  private:
+    uint64_t state, inc;
+};
+
 // Sampler (Sampler/Sampler.h:13-43) with the reference's interface — Get1D/Get2D/Clone pure
-// virtual, GetCameraSample from them (Sampler.cpp:10-21), the 1D/2D sample arrays — and
-// GlobalSampler's dimension bookkeeping (Sampler.h:62-82, Sampler.cpp:97-143).  The values come
-// from the device (pbr_hip_sampler_values), one query per block of kValueBlock dimensions of the
-// current sample, so the reference's per-pixel loop (Integrator.cpp:290-313) runs unchanged.
+// virtual, GetCameraSample from them (Sampler.cpp:10-21), the 1D/2D sample arrays — plus
+// PixelSampler (Sampler.h:46-60) and GlobalSampler (Sampler.h:62-82) with its pure
+// GetIndexForSample / SampleDimension, so a sampler subclass written against the reference compiles
+// here.  HaltonSampler and SobolSampler compute their values on the device
+// (pbr_hip_sample_index / pbr_hip_sample_dimensions, batched per block of dimensions); any other
+// GlobalSampler subclass renders too: Render tabulates its SampleDimension values for the frame
+// (PBR_SAMPLER_TABLE) and the device reads them.
 class Sampler {
   public:
     explicit Sampler(int64_t samplesPerPixel) : samplesPerPixel(samplesPerPixel) {}
@@ -584,12 +615,15 @@ class Sampler {
     virtual bool SetSampleNumber(int64_t sampleNum);
     int64_t CurrentSampleNumber() const { return currentPixelSampleIndex; }
     const int64_t samplesPerPixel;
-    // Extensions: where the sampler stands — SamplerIntegrator::Li continues the sample on the
-    // device from (pixel, sample number, next dimension) — and which device sampler it is.
+    // Extensions, with defaults for samplers written against the reference's interface: where the
+    // sampler stands (SamplerIntegrator::Li continues the sample on the device from pixel, sample
+    // number and next dimension; -1: not tracked), which device sampler serves it
+    // (PBR_SAMPLER_TABLE: none — Render tabulates a GlobalSampler's values), and the raster its
+    // sample indices are defined on ((0, 0): the camera's).
     const Point2i& CurrentPixel() const { return currentPixel; }
-    virtual int CurrentDimension() const = 0;
-    virtual int DeviceSampler() const = 0;         // PBR_SAMPLER_HALTON / PBR_SAMPLER_SOBOL
-    virtual Point2i SampleRaster() const = 0;      // the raster the sample indices are defined on
+    virtual int CurrentDimension() const { return -1; }
+    virtual int DeviceSampler() const { return PBR_SAMPLER_TABLE; }
+    virtual Point2i SampleRaster() const { return Point2i(0, 0); }
 
   protected:
     Point2i currentPixel;
@@ -601,6 +635,23 @@ class Sampler {
   private:
     size_t array1DOffset = 0, array2DOffset = 0;
 };
+// PixelSampler (Sampler.h:46-60, Sampler.cpp:67-95): a subclass fills samples1D / samples2D in its
+// StartPixel; dimensions beyond them come from rng.  Its 1D and 2D values are separate streams,
+// which the device's single dimension counter cannot reproduce: Render refuses it (per-pixel API only).
+class PixelSampler : public Sampler {
+  public:
+    PixelSampler(int64_t samplesPerPixel, int nSampledDimensions);
+    bool StartNextSample() override;
+    bool SetSampleNumber(int64_t) override;
+    float Get1D() override;
+    Point2f Get2D() override;
+
+  protected:
+    std::vector<std::vector<float>> samples1D;
+    std::vector<std::vector<Point2f>> samples2D;
+    int current1DDimension = 0, current2DDimension = 0;
+    RNG rng;
+};
 class GlobalSampler : public Sampler {
   public:
     explicit GlobalSampler(int64_t samplesPerPixel) : Sampler(samplesPerPixel) {}
@@ -609,13 +660,24 @@ class GlobalSampler : public Sampler {
     bool SetSampleNumber(int64_t sampleNum) override;
     float Get1D() override;
     Point2f Get2D() override;
+    // Sampler.h:69-70: the global index of the current pixel's sample `sampleNum`, and that index's
+    // value in `dimension`
+    virtual int64_t GetIndexForSample(int64_t sampleNum) const = 0;
+    virtual float SampleDimension(int64_t index, int dimension) const = 0;
+    // Extensions: batched forms (defaults: one call each; the device samplers answer a whole batch
+    // with one query), the current interval sample index, the number of dimensions the sampler has
     int CurrentDimension() const override { return dimension; }
-    // The value of dimension `dim` for sample `sampleNum` of the current pixel —
-    // SampleDimension(GetIndexForSample(sampleNum), dim) — and a batch of them, on the device.
+    int64_t CurrentIndex() const { return intervalSampleIndex; }
+    virtual void SampleDimensions(int64_t index, int firstDim, int n, float* out) const;
+    virtual void GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const;
+    virtual int MaxDimensions() const { return 1 << 30; }
+    // the value of dimension `dim` for sample `sampleNum` of the current pixel, and a batch of them
     float SampleValue(int64_t sampleNum, int dim) const;
     void SampleValues(const std::vector<int64_t>& sampleNums, const std::vector<int>& dims, float* out) const;
-    virtual int MaxDimensions() const = 0;
     static constexpr int kValueBlock = 32;
+
+  protected:
+    int64_t intervalSampleIndex = 0;
 
   private:
     float value(int dim);
@@ -629,6 +691,10 @@ class HaltonSampler : public GlobalSampler {   // Sampler/Halton.h
   public:
     HaltonSampler(int nsamp, const Bounds2i& sampleBounds, bool sampleAtCenter = false);
     std::unique_ptr<Sampler> Clone(int seed) override;   // Halton.cpp: a copy (the sequence has no seed)
+    int64_t GetIndexForSample(int64_t sampleNum) const override;   // Halton.cpp:61-81, on the device
+    float SampleDimension(int64_t index, int dimension) const override;   // Halton.cpp:83-92, on the device
+    void SampleDimensions(int64_t index, int firstDim, int n, float* out) const override;
+    void GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const override;
     int DeviceSampler() const override;
     Point2i SampleRaster() const override;
     int MaxDimensions() const override { return 1000; }   // PrimeTableSize
@@ -642,6 +708,10 @@ class SobolSampler : public GlobalSampler {
   public:
     SobolSampler(int64_t samplesPerPixel, const Bounds2i& sampleBounds);
     std::unique_ptr<Sampler> Clone(int seed) override;
+    int64_t GetIndexForSample(int64_t sampleNum) const override;   // SobolIntervalToIndex, on the device
+    float SampleDimension(int64_t index, int dimension) const override;   // pbrt-v3 sobol.cpp, on the device
+    void SampleDimensions(int64_t index, int firstDim, int n, float* out) const override;
+    void GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const override;
     int DeviceSampler() const override;
     Point2i SampleRaster() const override;
     int MaxDimensions() const override { return 1024; }   // NumSobolDimensions

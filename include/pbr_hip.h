@@ -81,7 +81,10 @@ enum pbr_integrator_type {
     PBR_INTEGRATOR_PATH = 1,    /* Integrator/PathIntegrator.cpp:32-110 */
     PBR_INTEGRATOR_VOLPATH = 2  /* Integrator/VolPathIntegrator.cpp:21-107 */
 };
-enum pbr_sampler_type { PBR_SAMPLER_HALTON = 0, PBR_SAMPLER_SOBOL = 1 };
+/* HALTON: Sampler/Halton.cpp; SOBOL: pbrt-v3's SobolSampler over the reference's SobolMatrices32;
+ * TABLE: values supplied by the caller — a host sampler the device cannot compute, e.g. a custom
+ * GlobalSampler subclass (Sampler/Sampler.h:62-82): see pbr_render_desc::sample_table. */
+enum pbr_sampler_type { PBR_SAMPLER_HALTON = 0, PBR_SAMPLER_SOBOL = 1, PBR_SAMPLER_TABLE = 2 };
 enum pbr_light_strategy { PBR_LIGHTS_UNIFORM = 0, PBR_LIGHTS_POWER = 1 };
 /* BVHAccel::SplitMethod (Accelerator/BVHAccel.h:18); HLBVH falls through to SAH (BVHAccel.cpp:135-160). */
 enum pbr_split_method { PBR_SPLIT_SAH = 0, PBR_SPLIT_HLBVH = 1, PBR_SPLIT_MIDDLE = 2, PBR_SPLIT_EQUAL_COUNTS = 3 };
@@ -257,6 +260,14 @@ typedef struct pbr_render_desc {
      * (2·log2(resolution) + log2(spp) <= 52). */
     const uint32_t* sobol_matrices;
     int sobol_dims;
+    /* PBR_SAMPLER_TABLE: every sample's dimensions as the caller's sampler gives them —
+     * sample_table[((y * camera.width + x) * spp + s) * table_dims + d] = SampleDimension(
+     * GetIndexForSample(s), d) at pixel (x, y), host memory, rows of pixels outside the tiles unused.
+     * GlobalSampler's bookkeeping (a Get2D at dimension 4 moves to 5, Sampler.cpp:131-143) applies as
+     * for the device samplers.  A path that asks for a dimension >= table_dims fails the frame
+     * (PBR_E_UNSUPPORTED).  Frames with a table are synchronous; camera.width·height·spp < 2^32. */
+    const float* sample_table;
+    int table_dims;
 } pbr_render_desc;
 
 typedef struct pbr_render_stats {
@@ -338,6 +349,15 @@ int pbr_hip_get_bvh(pbr_hip_ctx* ctx, void* nodes_out, int* n_nodes, int32_t* pr
 /* Halton/Sobol samples computed ON THE DEVICE for (pixel, sample, dim) triples. */
 int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height, int spp,
                            int n, const int32_t* px_py_sample_dim, float* out);
+/* GlobalSampler::GetIndexForSample (Sampler.h:69; Halton.cpp:61-81, pbrt-v3 SobolSampler) on the
+ * device: px_py_sample = 3 ints per query, out = the 64-bit interval sample index. */
+int pbr_hip_sample_index(pbr_hip_ctx* ctx, int sampler, int width, int height, int spp, int n,
+                         const int32_t* px_py_sample, int64_t* out);
+/* GlobalSampler::SampleDimension(index, dimension) (Sampler.h:70; Halton.cpp:83-92, pbrt-v3
+ * SobolSampler, whose dimensions 0 and 1 are taken relative to the current pixel: px_py_dim = 3 ints
+ * per query, pixel then dimension). */
+int pbr_hip_sample_dimensions(pbr_hip_ctx* ctx, int sampler, int width, int height, int n, const int64_t* index,
+                              const int32_t* px_py_dim, float* out);
 /* Camera rays computed on the device for raster samples (pFilm.x, pFilm.y): out = o.xyz, d.xyz */
 int pbr_hip_camera_rays(pbr_hip_ctx* ctx, const pbr_camera_desc* cam, int n, const float* pfilm, float* out);
 /* Closest-hit queries on the device: rays = o.xyz d.xyz tmax; out = {hit, t, prim_id, b1, b2} as floats */

@@ -148,6 +148,25 @@ class HipRenderer:
                                                     capi.fptr(out)), "sampler_values")
         return out
 
+    def sample_index(self, width, height, spp, px_py_sample, sampler=capi.SAMPLER_HALTON):
+        """GlobalSampler::GetIndexForSample on the device: int64 [n]."""
+        q = np.ascontiguousarray(px_py_sample, dtype=np.int32).reshape(-1, 3)
+        out = np.empty(q.shape[0], dtype=np.int64)
+        self._check(self.lib.pbr_hip_sample_index(self.ctx, sampler, width, height, spp, q.shape[0], capi.iptr(q),
+                                                  out.ctypes.data_as(C.POINTER(C.c_int64))), "sample_index")
+        return out
+
+    def sample_dimensions(self, width, height, index, px_py_dim, sampler=capi.SAMPLER_HALTON):
+        """GlobalSampler::SampleDimension(index, dim) on the device (pixel for Sobol's dims 0, 1): float32 [n]."""
+        idx = np.ascontiguousarray(index, dtype=np.int64).reshape(-1)
+        q = np.ascontiguousarray(px_py_dim, dtype=np.int32).reshape(-1, 3)
+        assert idx.shape[0] == q.shape[0]
+        out = np.empty(q.shape[0], dtype=np.float32)
+        self._check(self.lib.pbr_hip_sample_dimensions(self.ctx, sampler, width, height, q.shape[0],
+                                                       idx.ctypes.data_as(C.POINTER(C.c_int64)), capi.iptr(q),
+                                                       capi.fptr(out)), "sample_dimensions")
+        return out
+
     def camera_rays(self, cam, pfilm):
         pf = np.ascontiguousarray(pfilm, dtype=np.float32).reshape(-1, 2)
         out = np.empty((pf.shape[0], 6), dtype=np.float32)

@@ -21,7 +21,7 @@ SHAPE_TRIANGLE_MESH, SHAPE_SPHERE = 0, 1
 MAT_NONE, MAT_MATTE, MAT_MIRROR, MAT_GLASS, MAT_METAL, MAT_PLASTIC = range(6)
 LIGHT_POINT, LIGHT_DIFFUSE_AREA, LIGHT_SKYBOX, LIGHT_INFINITE_AREA = 0, 1, 2, 3
 INTEGRATOR_WHITTED, INTEGRATOR_PATH, INTEGRATOR_VOLPATH = 0, 1, 2
-SAMPLER_HALTON, SAMPLER_SOBOL = 0, 1
+SAMPLER_HALTON, SAMPLER_SOBOL, SAMPLER_TABLE = 0, 1, 2
 LIGHTS_UNIFORM, LIGHTS_POWER = 0, 1
 BVH_BUILD_HOST, BVH_BUILD_DEVICE = 0, 1
 SPLIT_SAH, SPLIT_HLBVH, SPLIT_MIDDLE, SPLIT_EQUAL_COUNTS = 0, 1, 2, 3
@@ -175,6 +175,8 @@ class RenderDesc(C.Structure):
         ("collect_stats", C.c_int),
         ("sobol_matrices", C.POINTER(C.c_uint32)),
         ("sobol_dims", C.c_int),
+        ("sample_table", C.POINTER(C.c_float)),
+        ("table_dims", C.c_int),
     ]
 
 
@@ -234,6 +236,10 @@ EXPORTS = {
                                   C.POINTER(C.c_int)]),
     "pbr_hip_sampler_values": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.POINTER(C.c_int32), C.POINTER(C.c_float)]),
+    "pbr_hip_sample_index": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
+    "pbr_hip_sample_dimensions": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int64),
+                                            C.POINTER(C.c_int32), C.POINTER(C.c_float)]),
     "pbr_hip_camera_rays": (C.c_int, [C.c_void_p, C.POINTER(CameraDesc), C.c_int, C.POINTER(C.c_float),
                                       C.POINTER(C.c_float)]),
     "pbr_hip_intersect": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
@@ -262,7 +268,7 @@ _lib = None
 
 OPTIONAL_FOR_AB = ("pbr_hip_sync", "pbr_hip_set_profiling", "pbr_hip_get_profile", "pbr_hip_query", "pbr_hip_bounds",
                    "pbr_hip_li", "pbr_hip_set_bvh_build", "pbr_hip_bvh_build_info", "pbr_hip_build_bvh",
-                   "pbr_hip_set_schedule")
+                   "pbr_hip_set_schedule", "pbr_hip_sample_index", "pbr_hip_sample_dimensions")
 
 
 def load_library(path: str | None = None) -> C.CDLL:

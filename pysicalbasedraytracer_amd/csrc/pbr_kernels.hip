@@ -63,6 +63,7 @@ __device__ __forceinline__ int sobol_lds_dims(const DeviceSampler& s) {
 // out-of-line call taking the sampler by reference makes the compiler copy the whole by-value kernel
 // parameter block into per-lane scratch and read every parameter back from there.
 __device__ __forceinline__ void stage_halton_lds(const DeviceSampler& s) {
+    if (s.type == PBR_SAMPLER_TABLE) return;
     if (s.type == PBR_SAMPLER_SOBOL) {
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_halton_perm);
         const int n = sobol_lds_dims(s) * kSobolNib;
@@ -93,22 +94,33 @@ __device__ __noinline__ uint32_t sobol_nibbles_hi(const uint32_t* T, uint32_t hi
     return T[hi & 15u] ^ T[16 + ((hi >> 4) & 15u)] ^ T[32 + ((hi >> 8) & 15u)] ^ T[48 + ((hi >> 12) & 15u)] ^
            T[64 + ((hi >> 16) & 15u)];
 }
+// SobolSampler::SampleDimension for a 64-bit index (lo, hi): dimensions 0 and 1 relative to the pixel
 template <bool LDS = false>
-__device__ __forceinline__ float sobol_dimension(const DeviceSampler& s, uint32_t index, int sid, int dim, int px, int py) {
+__device__ __forceinline__ float sobol_value(const DeviceSampler& s, uint32_t lo, uint32_t hi, int dim, int px, int py) {
     if (dim >= s.nSobolDims) return 0.f;
     uint32_t v;
-    if (LDS && dim < sobol_lds_dims(s)) v = sobol_nibbles(reinterpret_cast<const uint32_t*>(s_halton_perm) + dim * kSobolNib, index);
-    else v = sobol_nibbles(s.sobol + (size_t)dim * kSobolNib, index);
-    if (s.wideIndex) {   // index bits 32..51: the frame's bits above 31 - 2m (spp is a power of two)
-        const uint32_t hi = ((uint32_t)sid & (uint32_t)(s.spp - 1)) >> s.hiShift;
-        if (hi) v ^= sobol_nibbles_hi(s.sobolHi + (size_t)dim * kSobolNibHi, hi);
-    }
+    if (LDS && dim < sobol_lds_dims(s)) v = sobol_nibbles(reinterpret_cast<const uint32_t*>(s_halton_perm) + dim * kSobolNib, lo);
+    else v = sobol_nibbles(s.sobol + (size_t)dim * kSobolNib, lo);
+    if (hi) v ^= sobol_nibbles_hi(s.sobolHi + (size_t)dim * kSobolNibHi, hi);
     float f = mn((float)v * 2.3283064365386963e-10f, kOneMinusEpsilon);
     if (dim <= 1) {
         f = f * (float)s.sobolRes;   // + sampleBounds.pMin[dim] == 0
         f = clampf(f - (float)(dim == 0 ? px : py), 0.f, kOneMinusEpsilon);
     }
     return f;
+}
+template <bool LDS = false>
+__device__ __forceinline__ float sobol_dimension(const DeviceSampler& s, uint32_t index, int sid, int dim, int px, int py) {
+    // index bits 32..51: the frame's bits above 31 - 2m (spp is a power of two)
+    const uint32_t hi = s.wideIndex ? ((uint32_t)sid & (uint32_t)(s.spp - 1)) >> s.hiShift : 0u;
+    return sobol_value<LDS>(s, index, hi, dim, px, py);
+}
+// PBR_SAMPLER_TABLE: the caller's SampleDimension values (pbr_render_desc::sample_table); a
+// dimension the table lacks fails the frame instead of reading past it
+__device__ __forceinline__ float table_dimension(const DeviceSampler& s, uint32_t index, int dim) {
+    if (dim < s.tableDims) return s.table[(size_t)index * s.tableDims + dim];
+    atomicOr(s.guard, kGuardSampleTable);
+    return 0.f;
 }
 // SobolIntervalToIndex (LowDiscrepancy.h) via the GF(2) tables of sobol_pixel_tables; the index is
 // (frame << 2m) | j, 64-bit as pbrt-v3's (bits >= 32 come from the frame alone)
@@ -128,12 +140,15 @@ __device__ __forceinline__ SIndex sobol_index(const DeviceSampler& s, int px, in
 // GlobalSampler::StartPixel / SetSampleNumber: the global index of sample s of pixel (x, y)
 __device__ __forceinline__ SIndex sample_index(const DeviceSampler& smp, int x, int y, int s) {
     if (smp.type == PBR_SAMPLER_SOBOL) return sobol_index(smp, x, y, (uint32_t)s);
+    if (smp.type == PBR_SAMPLER_TABLE)   // the table row of (pixel, sample)
+        return SIndex{((uint32_t)y * (uint32_t)smp.tableW + (uint32_t)x) * (uint32_t)smp.spp + (uint32_t)s, 0u};
     return SIndex{halton_pixel_offset(hparams(smp), x, y) + (uint32_t)s * (uint32_t)smp.stride, 0u};   // Halton.cpp:61-81
 }
 
 template <bool LDS = false>
 __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int sid, int dim, int px = 0, int py = 0) {
     if (s.type == PBR_SAMPLER_SOBOL) return sobol_dimension<LDS>(s, index, sid, dim, px, py);
+    if (s.type == PBR_SAMPLER_TABLE) return table_dimension(s, index, dim);
     // HaltonSampler::SampleDimension (Halton.cpp:83-92)
     if (dim == 0) return radical_inverse_2(index >> s.baseExp0);
     if (dim == 1) return radical_inverse_b(3u, 0x55555555u, div_prime(index, (uint32_t)s.baseScale1, 0xffffffffu / (uint32_t)s.baseScale1));
@@ -619,6 +634,26 @@ __global__ void k_sampler_values(DeviceSampler smp, HaltonParams hp, int n, cons
     const SIndex idx = sample_index(smp, q[4 * i], q[4 * i + 1], q[4 * i + 2]);
     out[i] = sample_dimension(smp, idx.lo, q[4 * i + 2], q[4 * i + 3], q[4 * i], q[4 * i + 1]);
 }
+// GlobalSampler::GetIndexForSample / SampleDimension for (pixel, sample) and (index, pixel, dim) queries
+__global__ void k_sample_index(DeviceSampler smp, int n, const int32_t* q, long long* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int x = q[3 * i], y = q[3 * i + 1], s = q[3 * i + 2];
+    if (smp.type == PBR_SAMPLER_SOBOL) {
+        const SIndex k = sobol_index(smp, x, y, (uint32_t)s);
+        out[i] = (long long)(((uint64_t)k.hi << 32) | k.lo);
+    } else {   // Halton.cpp:61-81 in 64 bits: offsetForCurrentPixel + sampleNum * sampleStride
+        out[i] = (long long)((uint64_t)halton_pixel_offset(hparams(smp), x, y) + (uint64_t)s * (uint64_t)smp.stride);
+    }
+}
+__global__ void k_sample_dimensions(DeviceSampler smp, int n, const long long* idx, const int32_t* q, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t index = (uint64_t)idx[i];
+    const int px = q[3 * i], py = q[3 * i + 1], dim = q[3 * i + 2];
+    if (smp.type == PBR_SAMPLER_SOBOL) out[i] = sobol_value(smp, (uint32_t)index, (uint32_t)(index >> 32), dim, px, py);
+    else out[i] = sample_dimension(smp, (uint32_t)index, 0, dim, px, py);
+}
 __global__ void k_camera_rays(DeviceCamera cam, int n, const float* pf, float* out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -810,6 +845,7 @@ struct pbr_hip_ctx {
     uint64_t sobolKey = 0;               // FNV-1a of the matrices dSobol was built from
     int sobolSrcDims = 0, sobolPixM = -1;
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
+    DevBuf dTable;                       // PBR_SAMPLER_TABLE values of the current frame
     std::vector<int32_t> tilesHost;      // what dTiles / dTileStart hold (re-uploaded on change only)
     std::vector<long long> startsHost;
     hipStream_t lastStream = nullptr;    // stream of the last asynchronous render (may still run)
@@ -899,6 +935,7 @@ int check_guard(pbr_hip_ctx* ctx) {
     if (g & kGuardWhittedPassThrough) what += "a Whitted path crossed more than 1024 material-less surfaces; ";
     if (g & kGuardTransmittance) what += "a transmittance walk crossed more than 256 medium interfaces; ";
     if (g & kGuardStack) what += "a BVH traversal stack was full; ";
+    if (g & kGuardSampleTable) what += "a path asked the sample table for a dimension beyond table_dims; ";
     return set_err(ctx, PBR_E_UNSUPPORTED, what + "the frame is incomplete");
 }
 
@@ -949,6 +986,7 @@ DeviceSampler device_sampler(pbr_hip_ctx* ctx, int type, int spp, int w, int h) 
     s.recips = (const uint32_t*)ctx->dRecips.p;
     s.primeSums = (const uint32_t*)ctx->dPrimeSums.p;
     s.perms = (const uint16_t*)ctx->dPerms.p;
+    s.guard = (int*)ctx->dGuard.p;
     return s;
 }
 
@@ -1474,7 +1512,8 @@ int make_params(pbr_hip_ctx* ctx, const pbr_render_desc* d, KParams* out) {
         return set_err(ctx, PBR_E_UNSUPPORTED, "Whitted max_depth above 64 is not supported");
     if (d->integrator < PBR_INTEGRATOR_WHITTED || d->integrator > PBR_INTEGRATOR_VOLPATH)
         return set_err(ctx, PBR_E_INVALID, "unknown integrator");
-    if (d->sampler != PBR_SAMPLER_HALTON && d->sampler != PBR_SAMPLER_SOBOL) return set_err(ctx, PBR_E_INVALID, "unknown sampler");
+    if (d->sampler != PBR_SAMPLER_HALTON && d->sampler != PBR_SAMPLER_SOBOL && d->sampler != PBR_SAMPLER_TABLE)
+        return set_err(ctx, PBR_E_INVALID, "unknown sampler");
     // SobolSampler rounds spp up to a power of two (GlobalSampler(RoundUpPow2(spp)), Sobol.h)
     int spp = d->spp;
     if (d->sampler == PBR_SAMPLER_SOBOL) {
@@ -1488,6 +1527,10 @@ int make_params(pbr_hip_ctx* ctx, const pbr_render_desc* d, KParams* out) {
         // the device index keeps (px << m) | py and its low 32 bits in 32-bit words, and bits >= 32
         // come from frame >> (32 - 2m): rasters of 2^16 or more (max(w, h) > 32768) are refused
         if (m >= 16) return set_err(ctx, PBR_E_UNSUPPORTED, "Sobol raster above 32768 pixels per side");
+    } else if (d->sampler == PBR_SAMPLER_TABLE) {
+        if (!d->sample_table || d->table_dims < 1) return set_err(ctx, PBR_E_INVALID, "PBR_SAMPLER_TABLE needs sample_table and table_dims");
+        if ((long long)d->camera.width * d->camera.height * spp >= (1ll << 32))
+            return set_err(ctx, PBR_E_UNSUPPORTED, "sample table rows beyond 32-bit indices");
     } else if ((long long)spp * (long long)31104 >= (1ll << 32)) {
         return set_err(ctx, PBR_E_UNSUPPORTED, "spp too large for 32-bit sample indices");
     }
@@ -1504,6 +1547,16 @@ int make_params(pbr_hip_ctx* ctx, const pbr_render_desc* d, KParams* out) {
     }
     P.S = device_scene(ctx);
     P.smp = device_sampler(ctx, d->sampler, spp, d->camera.width, d->camera.height);
+    if (d->sampler == PBR_SAMPLER_TABLE) {   // the caller's values, copied before the call returns
+        const size_t bytes = (size_t)d->camera.width * d->camera.height * spp * d->table_dims * sizeof(float);
+        if (int rc = drain(ctx)) return rc;
+        HIP_TRY(ctx->dTable.ensure(bytes));
+        HIP_TRY(hipMemcpyAsync(ctx->dTable.p, d->sample_table, bytes, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        P.smp.table = (const float*)ctx->dTable.p;
+        P.smp.tableDims = d->table_dims;
+        P.smp.tableW = d->camera.width;
+    }
     if (d->sampler == PBR_SAMPLER_SOBOL) {
         int rc = prepare_sobol(ctx, d->sobol_matrices, d->sobol_dims, d->camera.width, d->camera.height, &P.smp);
         if (rc) return rc;
@@ -1597,7 +1650,8 @@ int pbr_hip_li(pbr_hip_ctx* ctx, const pbr_render_desc* d, int n, const float* r
     else hipLaunchKernelGGL(k_li<PBR_INTEGRATOR_VOLPATH>, g, b, 0, ctx->stream, P, n, (const float*)in, qd, o);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(rgb_out, o, ob, hipMemcpyDeviceToHost, ctx->stream));
-    if (ctx->host.anyNoMaterial) HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->host.anyNoMaterial || d->sampler == PBR_SAMPLER_TABLE)
+        HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return check_guard(ctx);
 }
@@ -1810,9 +1864,11 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(ctx->device));
     // An earlier asynchronous frame that stopped at a safety bound fails this call.  Only scenes with
-    // material-less primitives can trip one (and copy the flag out at the end of their frames), so
-    // only those wait for the previous frame here; every other frame stays queued back to back.
-    if (ctx->host.anyNoMaterial) {
+    // material-less primitives can trip one in an asynchronous frame (and copy the flag out at the
+    // end of their frames), so only those wait for the previous frame here; every other frame stays
+    // queued back to back.  Frames with a caller's sample table run synchronously.
+    const bool guardFrame = ctx->host.anyNoMaterial || d->sampler == PBR_SAMPLER_TABLE;
+    if (guardFrame) {
         if (int rc = drain(ctx)) return rc;
     }
     if (int rc = check_guard(ctx)) return rc;
@@ -1915,8 +1971,8 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     }
     unsigned long long hs[4] = {0, 0, 0, 0};
     if (d->collect_stats) HIP_TRY(hipMemcpyAsync(hs, ctx->dStats.p, sizeof(hs), hipMemcpyDeviceToHost, s));
-    if (ctx->host.anyNoMaterial) HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    if (!d->outputs_on_device || d->collect_stats || stats) {
+    if (guardFrame) HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (!d->outputs_on_device || d->collect_stats || stats || d->sampler == PBR_SAMPLER_TABLE) {
         HIP_TRY(hipStreamSynchronize(s));
         if (int rc = check_guard(ctx)) return rc;
     } else {
@@ -2088,6 +2144,69 @@ int pbr_hip_sampler_values(pbr_hip_ctx* ctx, int sampler, int width, int height,
     HIP_TRY(hipMemcpyAsync(ctx->dScratchIn.p, q, (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
     if (n > 0) hipLaunchKernelGGL(k_sampler_values, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, s, hp, n,
                                   (const int32_t*)ctx->dScratchIn.p, (float*)ctx->dScratchOut.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->dScratchOut.p, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PBR_OK;
+}
+
+// The device samplers as queried by the host API's GlobalSampler (include/pbr/pbr.h): the
+// sampler tables for a raster, as pbr_hip_sampler_values prepares them.
+static int query_sampler(pbr_hip_ctx* ctx, int sampler, int width, int height, int spp, DeviceSampler* s) {
+    if (sampler != PBR_SAMPLER_HALTON && sampler != PBR_SAMPLER_SOBOL) return set_err(ctx, PBR_E_INVALID, "sampler queries: Halton or Sobol");
+    if (width <= 0 || height <= 0 || spp <= 0) return set_err(ctx, PBR_E_INVALID, "sampler queries: empty raster or spp");
+    *s = device_sampler(ctx, sampler, spp, width, height);
+    if (sampler == PBR_SAMPLER_SOBOL) {
+        if (int rc = prepare_sobol(ctx, nullptr, 0, width, height, s)) return rc;
+        int p2 = 1;
+        while (p2 < spp) p2 <<= 1;
+        s->spp = p2;
+    }
+    return PBR_OK;
+}
+
+int pbr_hip_sample_index(pbr_hip_ctx* ctx, int sampler, int width, int height, int spp, int n, const int32_t* q, int64_t* out) {
+    if (!ctx || n < 0 || (n > 0 && (!q || !out))) return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    DeviceSampler s;
+    if (int rc = query_sampler(ctx, sampler, width, height, spp, &s)) return rc;
+    for (int i = 0; i < n; ++i)
+        if (q[3 * i] < 0 || q[3 * i + 1] < 0 || q[3 * i + 2] < 0) return set_err(ctx, PBR_E_INVALID, "sample_index: negative pixel or sample");
+    if (n == 0) return PBR_OK;
+    HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 12));
+    HIP_TRY(ctx->dScratchOut.ensure((size_t)n * 8));
+    HIP_TRY(hipMemcpyAsync(ctx->dScratchIn.p, q, (size_t)n * 12, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_sample_index, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, s, n, (const int32_t*)ctx->dScratchIn.p,
+                       (long long*)ctx->dScratchOut.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->dScratchOut.p, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PBR_OK;
+}
+
+int pbr_hip_sample_dimensions(pbr_hip_ctx* ctx, int sampler, int width, int height, int n, const int64_t* index, const int32_t* q,
+                              float* out) {
+    if (!ctx || n < 0 || (n > 0 && (!index || !q || !out))) return PBR_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = drain(ctx)) return rc;
+    DeviceSampler s;
+    if (int rc = query_sampler(ctx, sampler, width, height, 1, &s)) return rc;
+    const int maxDims = sampler == PBR_SAMPLER_SOBOL ? s.nSobolDims : 1000;
+    for (int i = 0; i < n; ++i) {
+        if (q[3 * i + 2] < 0 || q[3 * i + 2] >= maxDims) return set_err(ctx, PBR_E_INVALID, "sample_dimensions: dimension beyond the tables");
+        // the device Halton evaluates 32-bit indices (pbr_hip_render refuses spp that would need more)
+        if (index[i] < 0 || (sampler == PBR_SAMPLER_HALTON && index[i] >= (1ll << 32)) || index[i] >= (1ll << 52))
+            return set_err(ctx, PBR_E_INVALID, "sample_dimensions: index out of range");
+    }
+    if (n == 0) return PBR_OK;
+    HIP_TRY(ctx->dScratchIn.ensure((size_t)n * 20));
+    HIP_TRY(ctx->dScratchOut.ensure((size_t)n * 4));
+    char* in = (char*)ctx->dScratchIn.p;
+    HIP_TRY(hipMemcpyAsync(in, index, (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(in + (size_t)n * 8, q, (size_t)n * 12, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_sample_dimensions, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, s, n, (const long long*)in,
+                       (const int32_t*)(in + (size_t)n * 8), (float*)ctx->dScratchOut.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, ctx->dScratchOut.p, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

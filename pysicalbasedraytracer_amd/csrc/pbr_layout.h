@@ -113,6 +113,7 @@ struct DeviceScene {
 constexpr int kGuardWhittedPassThrough = 1;   // > kMaxPassThrough material-less crossings in one Whitted Li
 constexpr int kGuardTransmittance = 2;        // > kMaxTrCrossings interfaces on one VisibilityTester::Tr walk
 constexpr int kGuardStack = 4;                // a traversal stack was full (never, given the upload check below)
+constexpr int kGuardSampleTable = 8;          // a path asked a PBR_SAMPLER_TABLE sampler for a dimension it lacks
 constexpr int kMaxPassThrough = 1024;
 constexpr int kMaxTrCrossings = 256;
 // Traversal stacks (pbr_device.h): BVHAccel's 64 entries (BVHAccel.cpp:293).  The binary walk pushes
@@ -141,6 +142,10 @@ struct DeviceSampler {
     int wideIndex;                 // some sample index of this render needs bits >= 32
     int hiShift;                   // 32 - 2m: sample number >> hiShift = the index's bits >= 32
     int ldsDims;                   // Halton dimensions a kernel may stage in LDS (<= 64)
+    // PBR_SAMPLER_TABLE: the caller's values, [((y * tableW + x) * spp + s) * tableDims + dim]
+    const float* table;
+    int tableDims, tableW;
+    int* guard;                    // DeviceScene::guard: a dimension beyond the table fails the frame
 };
 
 struct DeviceCamera {

@@ -609,34 +609,53 @@ const Point2f* Sampler::Get2DArray(int n) {
     return &sampleArray2D[array2DOffset++][currentPixelSampleIndex * n];
 }
 
-// ---- GlobalSampler (Sampler/Sampler.cpp:97-143); SampleDimension on the device
+// ---- PixelSampler (Sampler/Sampler.cpp:67-95)
+PixelSampler::PixelSampler(int64_t samplesPerPixel, int nSampledDimensions) : Sampler(samplesPerPixel) {
+    for (int i = 0; i < nSampledDimensions; ++i) {
+        samples1D.push_back(std::vector<float>(samplesPerPixel));
+        samples2D.push_back(std::vector<Point2f>(samplesPerPixel));
+    }
+}
+bool PixelSampler::StartNextSample() {
+    current1DDimension = current2DDimension = 0;
+    return Sampler::StartNextSample();
+}
+bool PixelSampler::SetSampleNumber(int64_t sampleNum) {
+    current1DDimension = current2DDimension = 0;
+    return Sampler::SetSampleNumber(sampleNum);
+}
+float PixelSampler::Get1D() {
+    if (current1DDimension < (int)samples1D.size()) return samples1D[current1DDimension++][currentPixelSampleIndex];
+    return rng.UniformFloat();
+}
+Point2f PixelSampler::Get2D() {
+    if (current2DDimension < (int)samples2D.size()) return samples2D[current2DDimension++][currentPixelSampleIndex];
+    const float x = rng.UniformFloat(), y = rng.UniformFloat();   // Point2f(rng.UniformFloat(), rng.UniformFloat())
+    return Point2f(x, y);
+}
+
+// ---- GlobalSampler (Sampler/Sampler.cpp:97-143)
+void GlobalSampler::SampleDimensions(int64_t index, int firstDim, int n, float* out) const {
+    for (int k = 0; k < n; ++k) out[k] = SampleDimension(index, firstDim + k);
+}
+void GlobalSampler::GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const {
+    for (int k = 0; k < n; ++k) out[k] = GetIndexForSample(firstSample + k);
+}
 void GlobalSampler::SampleValues(const std::vector<int64_t>& sampleNums, const std::vector<int>& dims, float* out) const {
     if (sampleNums.size() != dims.size()) throw std::invalid_argument("SampleValues: sizes differ");
-    if (sampleNums.empty()) return;
-    const Point2i R = SampleRaster();
-    std::vector<int32_t> q(4 * dims.size());
-    for (size_t i = 0; i < dims.size(); ++i) {
-        if (dims[i] < 0 || dims[i] >= MaxDimensions()) throw std::out_of_range("sampler dimension beyond the sampler's tables");
-        if (sampleNums[i] < 0 || sampleNums[i] > 0x7fffffff) throw std::out_of_range("sample number beyond 31 bits");
-        q[4 * i] = currentPixel.x; q[4 * i + 1] = currentPixel.y;
-        q[4 * i + 2] = (int32_t)sampleNums[i]; q[4 * i + 3] = dims[i];
-    }
-    pbr_hip_ctx* h = helper_ctx();
-    check(h, pbr_hip_sampler_values(h, DeviceSampler(), R.x, R.y, (int)samplesPerPixel, (int)dims.size(), q.data(), out),
-          "pbr_hip_sampler_values");
+    for (size_t i = 0; i < dims.size(); ++i) SampleDimensions(GetIndexForSample(sampleNums[i]), dims[i], 1, &out[i]);
 }
 float GlobalSampler::SampleValue(int64_t sampleNum, int dim) const {
     float v = 0;
-    SampleValues({sampleNum}, {dim}, &v);
+    SampleDimensions(GetIndexForSample(sampleNum), dim, 1, &v);
     return v;
 }
+// SampleDimension(intervalSampleIndex, dim) through a block cache: a device sampler answers the
+// block with one query
 float GlobalSampler::value(int dim) {
     if (cacheBase < 0 || dim < cacheBase || dim >= cacheBase + kValueBlock) {
         const int n = std::max(1, std::min(kValueBlock, MaxDimensions() - dim));
-        std::vector<int64_t> nums(n, currentPixelSampleIndex);
-        std::vector<int> dims(n);
-        for (int k = 0; k < n; ++k) dims[k] = dim + k;
-        SampleValues(nums, dims, cache);
+        SampleDimensions(intervalSampleIndex, dim, n, cache);
         cacheBase = dim;
     }
     return cache[dim - cacheBase];
@@ -645,32 +664,37 @@ void GlobalSampler::StartPixel(const Point2i& p) {
     Sampler::StartPixel(p);
     dimension = 0;
     cacheBase = -1;
+    intervalSampleIndex = GetIndexForSample(0);
     arrayEndDim = arrayStartDim + (int)sampleArray1D.size() + 2 * (int)sampleArray2D.size();
-    // the arrays of every sample of the pixel, in one device query
-    std::vector<int64_t> nums;
-    std::vector<int> dims;
-    for (size_t i = 0; i < samples1DArraySizes.size(); ++i)
-        for (int64_t j = 0; j < samples1DArraySizes[i] * samplesPerPixel; ++j) { nums.push_back(j); dims.push_back(arrayStartDim + (int)i); }
+    // the arrays of every sample of the pixel (Sampler.cpp:103-122)
+    for (size_t i = 0; i < samples1DArraySizes.size(); ++i) {
+        const int nSamples = samples1DArraySizes[i] * (int)samplesPerPixel;
+        std::vector<int64_t> idx(nSamples);
+        GetIndicesForSamples(0, nSamples, idx.data());
+        for (int j = 0; j < nSamples; ++j) SampleDimensions(idx[j], arrayStartDim + (int)i, 1, &sampleArray1D[i][j]);
+    }
     int dim = arrayStartDim + (int)samples1DArraySizes.size();
-    for (size_t i = 0; i < samples2DArraySizes.size(); ++i, dim += 2)
-        for (int64_t j = 0; j < samples2DArraySizes[i] * samplesPerPixel; ++j)
-            for (int k = 0; k < 2; ++k) { nums.push_back(j); dims.push_back(dim + k); }
-    std::vector<float> v(nums.size());
-    SampleValues(nums, dims, v.data());
-    size_t k = 0;
-    for (size_t i = 0; i < samples1DArraySizes.size(); ++i)
-        for (auto& x : sampleArray1D[i]) x = v[k++];
-    for (size_t i = 0; i < samples2DArraySizes.size(); ++i)
-        for (auto& pt : sampleArray2D[i]) { pt.x = v[k++]; pt.y = v[k++]; }
+    for (size_t i = 0; i < samples2DArraySizes.size(); ++i, dim += 2) {
+        const int nSamples = samples2DArraySizes[i] * (int)samplesPerPixel;
+        std::vector<int64_t> idx(nSamples);
+        GetIndicesForSamples(0, nSamples, idx.data());
+        for (int j = 0; j < nSamples; ++j) {
+            float v[2];
+            SampleDimensions(idx[j], dim, 2, v);
+            sampleArray2D[i][j] = Point2f(v[0], v[1]);
+        }
+    }
 }
 bool GlobalSampler::StartNextSample() {
     dimension = 0;
     cacheBase = -1;
+    intervalSampleIndex = GetIndexForSample(currentPixelSampleIndex + 1);
     return Sampler::StartNextSample();
 }
 bool GlobalSampler::SetSampleNumber(int64_t sampleNum) {
     dimension = 0;
     cacheBase = -1;
+    intervalSampleIndex = GetIndexForSample(sampleNum);
     return Sampler::SetSampleNumber(sampleNum);
 }
 float GlobalSampler::Get1D() {
@@ -682,6 +706,62 @@ Point2f GlobalSampler::Get2D() {
     const float x = value(dimension), y = value(dimension + 1);
     dimension += 2;
     return Point2f(x, y);
+}
+
+// ---- the device samplers' GetIndexForSample / SampleDimension (pbr_hip_sample_index /
+// pbr_hip_sample_dimensions; Halton.cpp:61-92, pbrt-v3 SobolSampler)
+namespace {
+void device_indices(int type, Point2i raster, int64_t spp, const Point2i& pixel, int64_t first, int n, int64_t* out) {
+    if (n <= 0) return;
+    std::vector<int32_t> q(3 * (size_t)n);
+    for (int k = 0; k < n; ++k) {
+        if (first + k < 0 || first + k > 0x7fffffff) throw std::out_of_range("sample number beyond 31 bits");
+        q[3 * k] = pixel.x; q[3 * k + 1] = pixel.y; q[3 * k + 2] = (int32_t)(first + k);
+    }
+    pbr_hip_ctx* h = helper_ctx();
+    check(h, pbr_hip_sample_index(h, type, raster.x, raster.y, (int)spp, n, q.data(), out), "pbr_hip_sample_index");
+}
+void device_dimensions(int type, Point2i raster, const Point2i& pixel, int64_t index, int first, int n, int maxDims, float* out) {
+    if (n <= 0) return;
+    if (first < 0 || first + n > maxDims) throw std::out_of_range("sampler dimension beyond the sampler's tables");
+    std::vector<int64_t> idx((size_t)n, index);
+    std::vector<int32_t> q(3 * (size_t)n);
+    for (int k = 0; k < n; ++k) { q[3 * k] = pixel.x; q[3 * k + 1] = pixel.y; q[3 * k + 2] = first + k; }
+    pbr_hip_ctx* h = helper_ctx();
+    check(h, pbr_hip_sample_dimensions(h, type, raster.x, raster.y, n, idx.data(), q.data(), out), "pbr_hip_sample_dimensions");
+}
+}  // namespace
+int64_t HaltonSampler::GetIndexForSample(int64_t sampleNum) const {
+    int64_t v = 0;
+    device_indices(PBR_SAMPLER_HALTON, SampleRaster(), samplesPerPixel, currentPixel, sampleNum, 1, &v);
+    return v;
+}
+void HaltonSampler::GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const {
+    device_indices(PBR_SAMPLER_HALTON, SampleRaster(), samplesPerPixel, currentPixel, firstSample, n, out);
+}
+float HaltonSampler::SampleDimension(int64_t index, int dimension) const {
+    float v = 0;
+    device_dimensions(PBR_SAMPLER_HALTON, SampleRaster(), currentPixel, index, dimension, 1, MaxDimensions(), &v);
+    return v;
+}
+void HaltonSampler::SampleDimensions(int64_t index, int firstDim, int n, float* out) const {
+    device_dimensions(PBR_SAMPLER_HALTON, SampleRaster(), currentPixel, index, firstDim, n, MaxDimensions(), out);
+}
+int64_t SobolSampler::GetIndexForSample(int64_t sampleNum) const {
+    int64_t v = 0;
+    device_indices(PBR_SAMPLER_SOBOL, SampleRaster(), samplesPerPixel, currentPixel, sampleNum, 1, &v);
+    return v;
+}
+void SobolSampler::GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const {
+    device_indices(PBR_SAMPLER_SOBOL, SampleRaster(), samplesPerPixel, currentPixel, firstSample, n, out);
+}
+float SobolSampler::SampleDimension(int64_t index, int dimension) const {
+    float v = 0;
+    device_dimensions(PBR_SAMPLER_SOBOL, SampleRaster(), currentPixel, index, dimension, 1, MaxDimensions(), &v);
+    return v;
+}
+void SobolSampler::SampleDimensions(int64_t index, int firstDim, int n, float* out) const {
+    device_dimensions(PBR_SAMPLER_SOBOL, SampleRaster(), currentPixel, index, firstDim, n, MaxDimensions(), out);
 }
 
 // ============================================================================ flattening
@@ -1010,8 +1090,10 @@ void camera_desc(const PerspectiveCamera& cam, pbr_camera_desc* c) {
 // The samplers the device runs: HaltonSampler (any raster: its values depend on the pixel only) and
 // SobolSampler, whose resolution must be the camera's raster (the device derives it from there).
 void check_sampler(const Sampler& s, const PerspectiveCamera& cam, const char* who) {
-    if (!dynamic_cast<const HaltonSampler*>(&s) && !dynamic_cast<const SobolSampler*>(&s))
-        throw std::invalid_argument(std::string(who) + ": only HaltonSampler and SobolSampler are on the GPU path");
+    const bool device = dynamic_cast<const HaltonSampler*>(&s) || dynamic_cast<const SobolSampler*>(&s);
+    if (!device && (s.DeviceSampler() != PBR_SAMPLER_TABLE || !dynamic_cast<const GlobalSampler*>(&s)))
+        throw std::invalid_argument(std::string(who) + ": HaltonSampler, SobolSampler or a GlobalSampler subclass "
+                                                       "(PixelSampler's separate 1D / 2D streams are not on the GPU path)");
     if (s.DeviceSampler() == PBR_SAMPLER_SOBOL && (s.SampleRaster().x != cam.RasterWidth || s.SampleRaster().y != cam.RasterHeight))
         throw std::invalid_argument(std::string(who) + ": SobolSampler bounds must be the camera raster");
 }
@@ -1056,6 +1138,35 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
         for (const Bounds2i& b : tiles) tl.push_back({b.pMin.x, b.pMin.y, b.pMax.x, b.pMax.y});
     } else {
         tl.push_back({0, 0, W, H});
+    }
+    std::vector<float> table;
+    if (rd.sampler == PBR_SAMPLER_TABLE) {
+        // A GlobalSampler the device cannot compute: its values for every pixel and sample of the
+        // frame, taken the way Render's loop takes them (Integrator.cpp:290-300: Clone(offset),
+        // StartPixel, then sample after sample), for the dimensions the integrator can reach — 5
+        // camera dimensions, then per bounce at most 2 per light + 2 (Whitted), 8 (Path: light choice,
+        // light and BSDF samples, its own BSDF sample, roulette) or 10 (VolPath: + medium sampling).
+        // The device fails the frame if a path asks for more (kGuardSampleTable).
+        const int depth = std::max(1, MaxDepth()), nl = (int)scene.lights.size();
+        const int dims = IntegratorType() == PBR_INTEGRATOR_WHITTED ? 5 + depth * (2 * std::max(1, nl) + 2) + 2
+                         : IntegratorType() == PBR_INTEGRATOR_PATH ? 5 + (depth + 1) * 8 + 2
+                                                                   : 5 + (depth + 1) * 10 + 2;
+        const int Wr = cam->RasterWidth, Hr = cam->RasterHeight, spp = rd.spp;
+        table.assign((size_t)Wr * Hr * spp * dims, 0.f);
+        for (const pbr_tile& t : tl)
+            for (int y = t.y0; y < t.y1; ++y)
+                for (int x = t.x0; x < t.x1; ++x) {
+                    std::unique_ptr<Sampler> ps = sampler->Clone(pixelBounds.pMax.x * y + x);
+                    auto* g = dynamic_cast<GlobalSampler*>(ps.get());
+                    if (!g) throw std::invalid_argument("Render: Clone of a GlobalSampler must be a GlobalSampler");
+                    g->StartPixel(Point2i(x, y));
+                    for (int k = 0; k < spp; ++k) {
+                        if (k > 0) g->StartNextSample();
+                        g->SampleDimensions(g->CurrentIndex(), 0, dims, &table[(((size_t)y * Wr + x) * spp + k) * dims]);
+                    }
+                }
+        rd.sample_table = table.data();
+        rd.table_dims = dims;
     }
     rd.n_tiles = (int)tl.size();
     rd.tiles = tl.data();
@@ -1271,6 +1382,9 @@ std::vector<Spectrum> SamplerIntegrator::LiWith(const Sampler& smp, const std::v
                                                 int dimension, const Scene& scene, int depth) const {
     if (pixels.size() != rays.size() || samples.size() != rays.size())
         throw std::invalid_argument("Li: rays, pixels and samples differ in length");
+    if (smp.DeviceSampler() != PBR_SAMPLER_HALTON && smp.DeviceSampler() != PBR_SAMPLER_SOBOL)
+        throw std::invalid_argument("Li: only HaltonSampler and SobolSampler continue a sample on the device "
+                                    "(other samplers render through Render)");
     ensure_scene(scene);
     pbr_render_desc rd;
     std::memset(&rd, 0, sizeof(rd));
@@ -1381,6 +1495,8 @@ void SamplerIntegrator::RenderMulti(const Scene& scene, double& timeConsume) {
     auto* cam = dynamic_cast<const PerspectiveCamera*>(camera.get());
     if (!cam) throw std::invalid_argument("Render: only PerspectiveCamera is on the GPU path");
     check_sampler(*sampler, *cam, "Render");
+    if (sampler->DeviceSampler() == PBR_SAMPLER_TABLE)
+        throw std::invalid_argument("Render on several devices: custom GlobalSamplers render on one device");
     if (!tiles.empty()) throw std::invalid_argument("Render: SetTiles and SetDevices are exclusive");
     const int W = pixelBounds.pMax.x, H = pixelBounds.pMax.y;
     if (W <= 0 || H <= 0 || W > cam->RasterWidth || H > cam->RasterHeight)

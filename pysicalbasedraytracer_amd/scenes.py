@@ -469,11 +469,17 @@ def camera(width, height, eye, look, up=(0.0, 1.0, 0.0), fov=90.0):
 
 
 def render_desc(cam, integrator, spp, max_depth, rr_threshold=1.0, light_strategy=capi.LIGHTS_UNIFORM,
-                sampler=capi.SAMPLER_HALTON, tiles=None, sobol_matrices=None):
+                sampler=capi.SAMPLER_HALTON, tiles=None, sobol_matrices=None, sample_table=None):
     """sobol_matrices: optional uint32 array in SobolMatrices32 layout ([dims][52]); None → the
-    library's built-in matrices."""
+    library's built-in matrices.  sample_table: float32 [height, width, spp, dims] of a caller's
+    sampler (capi.SAMPLER_TABLE)."""
     d = capi.RenderDesc(integrator=integrator, max_depth=max_depth, rr_threshold=rr_threshold,
                         light_strategy=light_strategy, sampler=sampler, spp=spp, camera=cam)
+    if sample_table is not None:
+        arr = np.ascontiguousarray(sample_table, dtype=np.float32)
+        d.sample_table = arr.ctypes.data_as(C.POINTER(C.c_float))
+        d.table_dims = arr.shape[-1]
+        d._table_keep = arr
     if sobol_matrices is not None:
         arr = np.ascontiguousarray(sobol_matrices, dtype=np.uint32)
         d.sobol_matrices = arr.ctypes.data_as(C.POINTER(C.c_uint32))

@@ -436,6 +436,111 @@ void sampler_surface() {
     }
 }
 
+// Sampler subclasses written against the reference's interface (Sampler/Sampler.h:13-82).
+// A GlobalSampler that answers GetIndexForSample / SampleDimension itself — here by forwarding to
+// a HaltonSampler, so the expected frame is known — renders through Render (the values are
+// tabulated, PBR_SAMPLER_TABLE) bit for bit like the HaltonSampler; one shaped like the reference's
+// ClockRandSampler (ClockRand.h: index 0, a value per call) renders a finite, deterministic frame; a
+// PixelSampler subclass keeps the reference's 1D / 2D streams and RNG fallback and is refused by
+// Render (its streams are not one dimension counter).
+class ForwardingHalton : public GlobalSampler {
+  public:
+    ForwardingHalton(int spp, const Bounds2i& b) : GlobalSampler(spp), inner(spp, b) {}
+    void StartPixel(const Point2i& p) override {
+        inner.StartPixel(p);   // the inner sampler's pixel first: GetIndexForSample reads it
+        GlobalSampler::StartPixel(p);
+    }
+    int64_t GetIndexForSample(int64_t sampleNum) const override { return inner.GetIndexForSample(sampleNum); }
+    float SampleDimension(int64_t index, int dimension) const override { return inner.SampleDimension(index, dimension); }
+    std::unique_ptr<Sampler> Clone(int) override { return std::unique_ptr<Sampler>(new ForwardingHalton(*this)); }
+
+  private:
+    HaltonSampler inner;
+};
+class HashSampler : public GlobalSampler {   // ClockRandSampler's shape with a deterministic value
+  public:
+    explicit HashSampler(int spp) : GlobalSampler(spp) {}
+    int64_t GetIndexForSample(int64_t sampleNum) const override {
+        return ((int64_t)currentPixel.y * 4096 + currentPixel.x) * samplesPerPixel + sampleNum;
+    }
+    float SampleDimension(int64_t index, int dimension) const override {
+        uint64_t h = (uint64_t)index * 0x9E3779B97F4A7C15ull ^ (uint64_t)(dimension + 1) * 0xC2B2AE3D27D4EB4Full;
+        h ^= h >> 31; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 29;
+        return std::min(0.99999994f, (float)(h >> 40) * (1.f / 16777216.f));
+    }
+    std::unique_ptr<Sampler> Clone(int) override { return std::unique_ptr<Sampler>(new HashSampler(*this)); }
+};
+class FilledPixelSampler : public PixelSampler {
+  public:
+    FilledPixelSampler(int spp, int nDims) : PixelSampler(spp, nDims) {}
+    void StartPixel(const Point2i& p) override {
+        for (auto& d : samples1D) for (float& v : d) v = 0.25f;
+        for (auto& d : samples2D) for (Point2f& v : d) v = Point2f(0.5f, 0.75f);
+        Sampler::StartPixel(p);
+    }
+    std::unique_ptr<Sampler> Clone(int seed) override {
+        auto c = std::unique_ptr<FilledPixelSampler>(new FilledPixelSampler(*this));
+        c->rng.SetSequence(seed);
+        return std::unique_ptr<Sampler>(c.release());
+    }
+};
+void custom_samplers() {
+    const int W = 40, H = 30, spp = 8;
+    const Bounds2i bounds(Point2i(0, 0), Point2i(W, H));
+    for (int itype = 0; itype < 2; ++itype) {
+        Built b;
+        if (itype == 0) build_c1(b, W, H);
+        else build_area(b, W, H, false);
+        auto render = [&](std::shared_ptr<Sampler> smp, FrameBuffer& fb) {
+            std::shared_ptr<SamplerIntegrator> integ;
+            if (itype == 0) integ = std::make_shared<WhittedIntegrator>(5, b.cam, smp, bounds, &fb);
+            else integ = std::make_shared<PathIntegrator>(8, b.cam, smp, bounds, 0.8f, "uniform", &fb);
+            double t = 0;
+            integ->Render(*b.scene, t);
+        };
+        FrameBuffer ref, fwd, h1, h2;
+        for (FrameBuffer* f : {&ref, &fwd, &h1, &h2}) f->InitBuffer(W, H, 4);
+        render(std::make_shared<HaltonSampler>(spp, bounds), ref);
+        render(std::make_shared<ForwardingHalton>(spp, bounds), fwd);
+        const size_t nb = (size_t)W * H * 4;
+        expect(std::memcmp(ref.getUCbuffer(), fwd.getUCbuffer(), nb) == 0 &&
+                   std::memcmp(ref.getFCbuffer(), fwd.getFCbuffer(), nb * sizeof(float)) == 0,
+               itype ? "Path: a GlobalSampler subclass (forwarding SampleDimension) renders = HaltonSampler, bit for bit"
+                     : "Whitted: a GlobalSampler subclass (forwarding SampleDimension) renders = HaltonSampler, bit for bit");
+        render(std::make_shared<HashSampler>(spp), h1);
+        render(std::make_shared<HashSampler>(spp), h2);
+        bool finite = true;
+        double sum = 0;
+        for (size_t k = 0; k < nb; ++k) { finite = finite && std::isfinite(h1.getFCbuffer()[k]); sum += h1.getFCbuffer()[k]; }
+        expect(finite && sum > 0 && std::memcmp(h1.getFCbuffer(), h2.getFCbuffer(), nb * sizeof(float)) == 0,
+               itype ? "Path: a ClockRandSampler-shaped GlobalSampler renders a finite, deterministic frame"
+                     : "Whitted: a ClockRandSampler-shaped GlobalSampler renders a finite, deterministic frame");
+    }
+    // PixelSampler: the reference's streams (Sampler.cpp:67-95), refused by Render
+    FilledPixelSampler ps(4, 2);
+    auto c = ps.Clone(7);
+    c->StartPixel(Point2i(1, 2));
+    const float a = c->Get1D(), bb = c->Get1D();
+    const Point2f p2 = c->Get2D();
+    const float beyond = c->Get1D();   // past nSampledDimensions: rng
+    RNG rng;
+    rng.SetSequence(7);
+    const float want = rng.UniformFloat();
+    expect(a == 0.25f && bb == 0.25f && p2.x == 0.5f && p2.y == 0.75f && beyond == want,
+           "PixelSampler: sampled dimensions, then the RNG (Sampler.cpp:83-95)");
+    bool threw = false;
+    try {
+        Built b;
+        build_c1(b, W, H);
+        FrameBuffer fb;
+        fb.InitBuffer(W, H, 4);
+        WhittedIntegrator w(5, b.cam, std::make_shared<FilledPixelSampler>(4, 2), bounds, &fb);
+        double t = 0;
+        w.Render(*b.scene, t);
+    } catch (const std::invalid_argument&) { threw = true; }
+    expect(threw, "Render refuses a PixelSampler (its 1D / 2D streams are not on the GPU path)");
+}
+
 // An ingested mesh through the C++ surface on the device: tests/golden/mesh_small.3d
 // read by plyInfo and built as main.cpp:332-348 builds the dragon (TriangleMesh with an
 // object-to-world translation, one Triangle per face, GeometricPrimitive with a glass material),
@@ -629,6 +734,7 @@ int run_gpu() {
     decomposed_render_loop();
     sampler_surface();
     sobol_render();
+    custom_samplers();
     ply3d_render();
     multi_gpu_render();
     return failures ? 1 : 0;

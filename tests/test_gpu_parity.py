@@ -441,3 +441,52 @@ def test_multilight_whitted_wavefront(hip, lights):
     assert np.array_equal(wf.view(np.uint32), mk.view(np.uint32)), float(np.abs(wf - mk).max())
     c, c8, _ = O.render(s, rd)
     compare(wf, c, wf8, c8)
+
+
+@pytest.mark.parametrize("sampler", [capi.SAMPLER_HALTON, capi.SAMPLER_SOBOL])
+def test_global_sampler_queries_match_the_oracle(hip, sampler):
+    """GlobalSampler::GetIndexForSample and SampleDimension(index, dim) served by the device (the
+    host API's HaltonSampler / SobolSampler implement the reference's pure virtuals with them) equal
+    the oracle's sampler for the same (pixel, sample, dimension), bit for bit; Sobol at a raster
+    whose indices need more than 32 bits."""
+    rng = np.random.default_rng(17)
+    W, H, spp = (1920, 1080, 16) if sampler == capi.SAMPLER_HALTON else (3840, 2160, 1024)
+    n = 3000
+    px, py = rng.integers(0, W, n), rng.integers(0, H, n)
+    smp, dim = rng.integers(0, spp, n), rng.integers(0, 128, n)
+    idx = hip.sample_index(W, H, spp, np.stack([px, py, smp], 1), sampler=sampler)
+    got = hip.sample_dimensions(W, H, idx, np.stack([px, py, dim], 1), sampler=sampler)
+    q = np.stack([px, py, smp, dim], 1)
+    if sampler == capi.SAMPLER_HALTON:
+        want = O.halton(W, H, spp, q)
+    else:
+        want, widx = O.sobol(W, H, q)
+        assert np.array_equal(idx, widx) and (idx >= 2 ** 32).any()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_table_sampler_renders_the_callers_values(hip):
+    """PBR_SAMPLER_TABLE (a caller's GlobalSampler, e.g. a custom subclass in the host API): a table
+    holding the Halton sampler's own values renders the Halton frame bit for bit (Path, both
+    schedules); a table with too few dimensions fails the frame instead of reading past it."""
+    s, rd = scenes.config_c3(48, 32, 8, mesh=small_dragon(24))
+    W, H, spp, D = 48, 32, 8, 5 + 9 * 8 + 2
+    rdh = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                             capi.SAMPLER_HALTON)
+    hip.upload(s)
+    want, want8, _ = hip.render(rdh)
+    y, x, k, d = np.meshgrid(np.arange(H), np.arange(W), np.arange(spp), np.arange(D), indexing="ij")
+    q = np.stack([x.ravel(), y.ravel(), k.ravel(), d.ravel()], 1)
+    table = hip.sampler_values(W, H, spp, q).reshape(H, W, spp, D)
+    rdt = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                             capi.SAMPLER_TABLE, sample_table=table)
+    got, got8, _ = hip.render(rdt)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)) and np.array_equal(got8, want8)
+    hip.set_schedule(kernels=capi.KERNELS_MEGAKERNEL)
+    mk, _, _ = hip.render(rdt)
+    assert np.array_equal(mk.view(np.uint32), want.view(np.uint32))
+    hip.set_schedule()
+    short = scenes.render_desc(rd.camera, rd.integrator, spp, rd.max_depth, rd.rr_threshold, rd.light_strategy,
+                               capi.SAMPLER_TABLE, sample_table=np.ascontiguousarray(table[..., :9]))
+    with pytest.raises(RuntimeError, match="sample table"):
+        hip.render(short)
