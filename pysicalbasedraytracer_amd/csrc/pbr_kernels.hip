@@ -863,7 +863,6 @@ struct pbr_hip_ctx {
     // per-kernel profile (pbr_hip_set_profiling): a HIP event pair around every launch, on the
     // launch's stream, and the work counters of each kernel family (device rows + host-known counts)
     bool profOn = false, profCount = false;
-    bool wfFused = false;                // the last Whitted frame traced in its shade kernels (profile bytes)
     struct ProfEv { int kind; hipEvent_t a, b; };
     std::vector<ProfEv> profEv;
     size_t profUsed = 0;
@@ -1197,7 +1196,6 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const int fuse = ctx->sched.fuse_camera;
     const bool fuseCamera = kPacket && kQuadTraversal && fuse != PBR_FUSE_OFF && (mm || simple) && matsLds && !textured &&
                             !ml && (nChunks >= std::max(2, ch.lanes) || fuse == PBR_FUSE_ON);
-    ctx->wfFused = fuseCamera;
     // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
     const int maxLevels = levels;   // no material-less primitives here (those scenes run the megakernel)
     // Shadow rays of level L run on a second stream, overlapping extend(L+1) and shade(L+1) (they
@@ -1312,6 +1310,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, st, W, l0);
             else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, st, W, l0));
             if (l0) prof_host(ctx, KP_WF_SHADE, 0, (unsigned long long)W.nSamples);
+            if (l0 && fuseCamera && !textured && !ml) prof_host(ctx, KP_WF_SHADE, 6, (unsigned long long)W.nSamples);
             if (int rc = prof_sums(ctx, st, KP_WF_SHADE, {l0 ? nullptr : W.cur.segCount, W.shadowSeg, nullptr, nullptr,
                                                           W.next.segCount, l0 ? nullptr : W.cur.segCount})) return rc;
             if (shadowOverlap) {
@@ -2064,9 +2063,9 @@ int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int*
         switch (k) {
         case KP_WF_CAMERA: return 52 * f[0];                                   // o, d, hit, index
         case KP_WF_SHADE:   // ray + hit + index + recA + depth; shadow; next + recF/P
-            // (fused: level 0 reads no ray, hit or index; it writes the index, 4 B)
-            if (ctx->wfFused) return 72 * f[0] - 48 * c[KP_WF_CAMERA][0] + 4 * f[5] + 52 * f[1] + 52 * f[4];
-            return 72 * f[0] + 4 * f[5] + 52 * f[1] + 52 * f[4];
+            // (f[6] level-0 samples of fused launches: those read no ray, hit or index; they write the
+            // index, 4 B)
+            return 72 * f[0] - 48 * f[6] + 4 * f[5] + 52 * f[1] + 52 * f[4];
         case KP_WF_SHADOW: return 52 * f[0] + 32 * f[1];                       // o, d, contribution, id; recA RMW
         case KP_WF_EXTEND: return 64 * f[0];                                   // o, d read; o, hit written
         case KP_WF_FINISH: return 16 * f[0] + 4 * f[1] + 16 * c[KP_WF_SHADE][0] + 20 * c[KP_WF_SHADE][4];
