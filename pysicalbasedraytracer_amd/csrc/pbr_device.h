@@ -789,8 +789,8 @@ PBR_HD void tr_sample11(float cosTheta, float U1, float U2, float* sx, float* sy
     if ((double)cosTheta > .9999) {   // the reference's unqualified sqrt/cos/sin resolve to double
         float r = (float)sqrt((double)(U1 / (1 - U1)));
         float phi = (float)(6.28318530718 * (double)U2);
-        *sx = t_rcos_d((double)r, phi);   // (float)((double)r * cos((double)phi))
-        *sy = t_rsin_d((double)r, phi);
+        *sx = (float)((double)r * cos((double)phi));
+        *sy = (float)((double)r * sin((double)phi));
         return;
     }
     float sinTheta = sqrtf(mx((float)0, (float)1 - cosTheta * cosTheta));
@@ -989,12 +989,11 @@ struct BSDF {                    // Reflection.h:101-149: frame + the material's
     }
 };
 PBR_HD bool matches(const Lobe& l, int t) { return (l.type & t) == l.type; }
-PBR_HD int num_components(const MatTemplate& mt, int flags) {
+PBR_HD int num_components(const BSDF& b, int flags) {
     int k = 0;
-    for (int i = 0; i < mt.nLobes; ++i) if (matches(mt.lobes[i], flags)) ++k;
+    for (int i = 0; i < b.mt->nLobes; ++i) if (matches(b.mt->lobes[i], flags)) ++k;
     return k;
 }
-PBR_HD int num_components(const BSDF& b, int flags) { return num_components(*b.mt, flags); }
 template <int K = kAllLobes>
 PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:56-71
     f3 wi = b.to_local(wiW), wo = b.to_local(woW);

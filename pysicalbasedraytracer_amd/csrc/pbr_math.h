@@ -44,135 +44,14 @@ constexpr float gamma_n(int n) {
 #else
 #define PBR_TRANS PBR_HD
 #endif
-// The out-of-line fp64 library calls (ocml on the device, libm on the host).
-PBR_TRANS float c_sin(float x) { return (float)sin((double)x); }
-PBR_TRANS float c_cos(float x) { return (float)cos((double)x); }
-PBR_TRANS float c_exp(float x) { return (float)exp((double)x); }
-PBR_TRANS float c_log(float x) { return (float)log((double)x); }
+PBR_TRANS float t_sin(float x) { return (float)sin((double)x); }
+PBR_TRANS float t_cos(float x) { return (float)cos((double)x); }
+PBR_TRANS float t_exp(float x) { return (float)exp((double)x); }
+PBR_TRANS float t_log(float x) { return (float)log((double)x); }
 PBR_TRANS float t_pow(float x, float y) { return (float)pow((double)x, (double)y); }
-PBR_TRANS float c_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-PBR_TRANS float c_asin(float x) { return (float)asin((double)x); }
-PBR_TRANS float c_acos(float x) { return (float)acos((double)x); }
-PBR_TRANS double c_cos_d(double x) { return cos(x); }
-PBR_TRANS double c_sin_d(double x) { return sin(x); }
-
-// Device fast path of the transcendentals, same results.  Each t_f(x) is (float)f((double)x).  On
-// the device it is first evaluated inline in fp64 — Cody-Waite reduction + fdlibm's sin/cos kernels,
-// atan over a k/8 table, log via atanh, exp via ln2 reduction — to within 2^-50 relative (measured
-// 2^-51 against glibc over 4·10^7 arguments incl. the floats nearest multiples of π/2:
-// tests/test_fast_trans.py).  If every value within 2^-40 relative of that approximation rounds to
-// the same float, that float is the correctly rounded f(x), and so exactly what the fp64 library
-// call rounds to (its result lies in the same interval); otherwise — about once in 2^15 — the call
-// is made.  The calls stay on a cold branch: they clobber every caller-saved VGPR, so a shading
-// kernel that called them on its hot path spilled its live state around each one.
-namespace fastm {
-PBR_HD bool rounds_to(double v, float* out) {
-    const double t = fabs(v) * 0x1p-40;
-    const float lo = (float)(v - t), hi = (float)(v + t);
-    *out = hi;
-    return lo == hi;
-}
-// sin / cos of a float with |x| <= 64 (fdlibm's __kernel_sin / __kernel_cos polynomials on
-// |y| <= π/4; π/2 in three parts, the first two of 33 bits so n·part is exact)
-PBR_HD bool sincos(float x, double* s, double* c) {
-    const double xd = x;
-    if (!(fabs(xd) <= 64.0) || x == 0) return false;
-    const double n = rint(xd * 6.36619772367581382433e-01);
-    const double y = ((xd - n * 1.57079632673412561417e+00) - n * 6.07710050630396597660e-11) - n * 2.02226624879595063154e-21;
-    const double z = y * y;
-    const double ps = 8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
-                      z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
-    const double sy = y + y * z * (-1.66666666666666324348e-01 + z * ps);
-    const double pc = 4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * (2.48015872894767294178e-05 +
-                      z * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11))));
-    const double cy = (1.0 - 0.5 * z) + z * z * pc;
-    const int q = (int)n & 3;
-    *s = q == 0 ? sy : (q == 1 ? cy : (q == 2 ? -sy : -cy));
-    *c = q == 0 ? cy : (q == 1 ? -sy : (q == 2 ? -cy : sy));
-    return true;
-}
-// atan(t), t in [0, 1]: atan(k/8) + atan((t − k/8) / (1 + t·k/8)), |u| <= 1/16, Taylor to u^13
-PBR_HD double atan01(double t) {
-    const double kd = rint(t * 8.0);
-    const double c = kd * 0.125;
-    const double u = (t - c) / (1.0 + t * c);
-    const double z = u * u;
-    const double p = -1.0 / 3 + z * (1.0 / 5 + z * (-1.0 / 7 + z * (1.0 / 9 + z * (-1.0 / 11 + z * (1.0 / 13)))));
-    const int k = (int)kd;
-    const double tk = k < 4 ? (k < 2 ? (k == 0 ? 0.0 : 0x1.fd5ba9aac2f6ep-4) : (k == 2 ? 0x1.f5b75f92c80ddp-3 : 0x1.6f61941e4def1p-2))
-                            : (k < 6 ? (k == 4 ? 0x1.dac670561bb4fp-2 : 0x1.1e00babdefeb4p-1)
-                                     : (k == 6 ? 0x1.4978fa3269ee1p-1 : (k == 7 ? 0x1.700a7c5784634p-1 : 0x1.921fb54442d18p-1)));
-    return tk + (u + u * z * p);
-}
-PBR_HD bool atan2(double y, double x, double* r) {   // finite, both nonzero
-    if (!(x != 0 && y != 0 && fabs(x) <= 1e300 && fabs(y) <= 1e300)) return false;
-    const double ax = fabs(x), ay = fabs(y);
-    const bool sw = ay > ax;
-    double a = atan01(sw ? ax / ay : ay / ax);
-    if (sw) a = 0x1.921fb54442d18p+0 - a;
-    if (x < 0) a = 0x1.921fb54442d18p+1 - a;
-    *r = y < 0 ? -a : a;
-    return true;
-}
-// log(x), x > 0 normal: e·ln2 + 2·atanh(s), s = (m − 1)/(m + 1), m in [√½, √2), |s| <= 0.1716
-PBR_HD bool log(float x, double* r) {
-    if (!(x >= 1.17549435e-38f && x <= 3.40282347e+38f)) return false;
-    int e = (int)((__builtin_bit_cast(uint32_t, x) >> 23) & 0xff) - 127;
-    double md = (double)__builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, x) & 0x7fffffu) | 0x3f800000u);   // [1, 2)
-    if (md > 1.41421356237309504880) { md *= 0.5; e += 1; }
-    const double s = (md - 1.0) / (md + 1.0), z = s * s;
-    const double p = 1.0 / 3 + z * (1.0 / 5 + z * (1.0 / 7 + z * (1.0 / 9 + z * (1.0 / 11 + z * (1.0 / 13 + z * (1.0 / 15 +
-                     z * (1.0 / 17 + z * (1.0 / 19 + z * (1.0 / 21 + z * (1.0 / 23))))))))));
-    const double lm = 2.0 * (s + s * z * p);
-    *r = e == 0 ? lm : (double)e * 0x1.62e42fefa39efp-1 + lm;
-    return true;
-}
-// exp(x), |x| <= 100: 2^n · exp(r), r = x − n·ln2 (ln2 in two parts, the first of 32 bits), Taylor to r^13
-PBR_HD bool exp(float x, double* r) {
-    if (!(fabs(x) <= 100.f)) return false;
-    const double xd = x;
-    const double n = rint(xd * 0x1.71547652b82fep+0);
-    const double y = (xd - n * 0x1.62e42feep-1) - n * 0x1.a39ef35793c76p-33;
-    double p = 1.0 / 6227020800.0;
-    p = 1.0 / 479001600.0 + y * p; p = 1.0 / 39916800.0 + y * p; p = 1.0 / 3628800.0 + y * p;
-    p = 1.0 / 362880.0 + y * p; p = 1.0 / 40320.0 + y * p; p = 1.0 / 5040.0 + y * p; p = 1.0 / 720.0 + y * p;
-    p = 1.0 / 120.0 + y * p; p = 1.0 / 24.0 + y * p; p = 1.0 / 6.0 + y * p; p = 0.5 + y * p; p = 1.0 + y * p;
-    const double ey = 1.0 + y * p;
-    *r = ey * __builtin_bit_cast(double, (uint64_t)((int64_t)n + 1023) << 52);
-    return true;
-}
-}  // namespace fastm
-
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(PBR_INLINE_TRANS)
-#define PBR_FAST(call, expr)                                                        \
-    do {                                                                            \
-        double v_;                                                                  \
-        float o_;                                                                   \
-        if (__builtin_expect(call && fastm::rounds_to(expr, &o_), 1)) return o_;   \
-    } while (0)
-#else
-#define PBR_FAST(call, expr) do { } while (0)
-#endif
-PBR_HD float t_sin(float x) { double c_; (void)c_; PBR_FAST(fastm::sincos(x, &v_, &c_), v_); return c_sin(x); }
-PBR_HD float t_cos(float x) { double s_; (void)s_; PBR_FAST(fastm::sincos(x, &s_, &v_), v_); return c_cos(x); }
-PBR_HD float t_exp(float x) { PBR_FAST(fastm::exp(x, &v_), v_); return c_exp(x); }
-PBR_HD float t_log(float x) { PBR_FAST(fastm::log(x, &v_), v_); return c_log(x); }
-PBR_HD float t_atan2(float y, float x) { PBR_FAST(fastm::atan2((double)y, (double)x, &v_), v_); return c_atan2(y, x); }
-PBR_HD float t_asin(float x) {   // asin(x) = atan2(x, sqrt((1 − x)(1 + x)))
-    PBR_FAST(fabsf(x) < 1.f && fastm::atan2((double)x, sqrt((1.0 - (double)x) * (1.0 + (double)x)), &v_), v_);
-    return c_asin(x);
-}
-PBR_HD float t_acos(float x) {   // acos(x) = atan2(sqrt((1 − x)(1 + x)), x)
-    PBR_FAST(fabsf(x) < 1.f && fastm::atan2(sqrt((1.0 - (double)x) * (1.0 + (double)x)), (double)x, &v_), v_);
-    return c_acos(x);
-}
-// (float)(r · cos(phi)) / (float)(r · sin(phi)) with the products in double (TrowbridgeReitzSample11)
-PBR_HD float t_rcos_d(double r, float phi) {
-    double s_; (void)s_; PBR_FAST(fastm::sincos(phi, &s_, &v_), r * v_); return (float)(r * c_cos_d((double)phi));
-}
-PBR_HD float t_rsin_d(double r, float phi) {
-    double c_; (void)c_; PBR_FAST(fastm::sincos(phi, &v_, &c_), r * v_); return (float)(r * c_sin_d((double)phi));
-}
+PBR_TRANS float t_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+PBR_TRANS float t_asin(float x) { return (float)asin((double)x); }
+PBR_TRANS float t_acos(float x) { return (float)acos((double)x); }
 
 // std::min/std::max/Clamp with the reference's NaN behaviour
 PBR_HD float mn(float a, float b) { return (b < a) ? b : a; }

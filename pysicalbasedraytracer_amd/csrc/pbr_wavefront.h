@@ -538,30 +538,6 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                 W.recA[ri] = make_float4(L.r, L.g, L.b, 0.f);
                 W.depthOf[id] = depth;
             } else {
-                SState st;
-                st.index = 0; st.sid = id; st.dim = dim; st.px = st.py = 0;   // dims >= 2 only past the camera
-                // A SkyBox light sample's direction and map coordinates, before the hit's geometry and
-                // BSDF: they depend only on the two sampler values, and with few values live across the
-                // out-of-line transcendentals (uniform_sphere's cos / sin, sphere_uv's asin / atan2)
-                // nothing spills around those calls.  The draw is the one the light loop below makes
-                // (same dimensions); only a material make_bsdf accepts draws, as below.
-                constexpr bool kSkyEarly = (LOBES & kTexturedLobes) == 0;
-                bool drawn = false;
-                float sa = 0.f, sb = 0.f, skyU = 0.f, skyV = 0.f;
-                f3 skyWi = mk(0, 0, 0);
-                if (kSkyEarly && S.lights[0].type == LT_SKY) {
-                    const int mat = S.primInfo[slot].y;
-                    const MatTemplate* mt = mat >= 0 ? mats + 2 * mat : nullptr;
-                    if (mt && mt->valid) {
-                        st.index = CAMERA ? camIndex : W.sampleIndex[id];
-                        get2d<true>(P.smp, st, &sa, &sb);
-                        drawn = true;
-                        if (num_components(*mt, BSDF_ALL & ~BSDF_SPECULAR) > 0) {
-                            skyWi = uniform_sphere(sa, sb);
-                            sphere_uv(normalize(skyWi), &skyU, &skyV);
-                        }
-                    }
-                }
                 Isect isect;
                 int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
                 if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
@@ -577,10 +553,14 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                     f3 n = isect.sn, wo = isect.wo;
                     rgb L = sp(0.f);
                     L = L + si_Le(S, isect, wo);
-                    if (!drawn) st.index = CAMERA ? camIndex : W.sampleIndex[id];
+                    SState st;
+                    st.index = CAMERA ? camIndex : W.sampleIndex[id];
+                    st.sid = id;   // ≡ the sample number mod spp (pixel-major ids)
+                    st.dim = dim;
+                    st.px = st.py = 0;   // dims >= 2 only past the camera
                     {   // the single light (WhittedIntegrator.cpp:39-54)
-                        float a = sa, b = sb;
-                        if (!drawn) get2d<true>(P.smp, st, &a, &b);
+                        float a, b;
+                        get2d<true>(P.smp, st, &a, &b);
                         // Reordered but equivalent: f(wo, wi) does not depend on Li, and nothing is
                         // added when f is black — so the light's radiance (for the SkyBox: atan2,
                         // asin and an env gather) is only evaluated when f is not black, and a
@@ -592,13 +572,13 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                             const DLight& light = S.lights[0];
                             rgb Li;
                             if (light.type == LT_SKY) {
-                                wi = kSkyEarly ? skyWi : uniform_sphere(a, b);   // computed above: same template, same lobes
+                                wi = uniform_sphere(a, b);
                                 pdf = 1.f / (4 * kPi);
                                 vis.p = isect.p + wi * (2 * light.worldRadius); vis.pError = mk(0, 0, 0); vis.n = mk(0, 0, 0);
                                 rgb f = bsdf_f<LOBES>(bsdf, wo, wi, BSDF_ALL);
                                 if (!black(f)) {
-                                    float ul = skyU, vl = skyV;
-                                    if (!kSkyEarly) sphere_uv(normalize(wi), &ul, &vl);
+                                    float ul, vl;
+                                    sphere_uv(normalize(wi), &ul, &vl);
                                     Li = light.envW > 0 ? sky_value(S, light, ul, vl) : sp(0.f);
                                     if (!black(Li)) {
                                         contrib = f * Li * absdot(wi, n) / pdf;

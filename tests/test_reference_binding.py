@@ -8,8 +8,13 @@ pbrhip::Hip{Whitted,Path,VolPath}Integrator â€” the same constructor arguments â
 reference Scene (its BVHAccel's tree included) into pbr_scene_desc and renders through the C-ABI.
 
 Bar: the device walks the reference's own tree (its LinearBVHNode array, uploaded byte for byte);
-the FrameBuffers are identical except where a last-bit libm difference (glibc in the reference,
-correctly rounded transcendentals on the device, DESIGN Â§1) moves a byte by one."""
+the FrameBuffers are identical except where a last-bit libm difference (glibc's float sinf/expf/logf
+in the reference, correctly rounded transcendentals on the device, DESIGN Â§1) moves a byte by one â€”
+or, rarely, flips one sample's discrete decision (Russian roulette, a lobe or medium-event choice) and
+moves its pixel further.  The oracle, which follows the device's rounding policy, shows the same
+against the reference on its own scenes: C3 at 96Ã—96Ã—16 on Halton, 68 of 9216 float pixels differ,
+one u8 byte by 4; C3 64Ã—64Ã—16 and C5 48Ã—48Ã—8, u8 identical (tests/ref_lib vs tests/oracle_lib, CPU).
+So at most 0.1% of the pixels may differ by more than one."""
 import ctypes as C
 import os
 
@@ -68,6 +73,6 @@ def test_reference_render_equals_binding_render(config, res, spp):
     print(f"config {config}: {same:.4f} of the pixels identical, max |Î”| {int(diff.max())}, "
           f"reference {secs[0]:.2f} s, binding {secs[1]:.3f} s")
     assert (r[:, 3] == 255).all() and (h[:, 3] == 255).all()
-    assert diff.max() <= 1, f"a byte differs by {int(diff.max())}"
+    assert (diff <= 1).mean() >= 0.999, f"{int((diff > 1).sum())} pixels differ by more than one"
     assert same >= 0.98, f"only {same:.4f} of the pixels identical"
     assert r[:, :3].std() > 1.0   # a real image, not a blank frame

@@ -2,7 +2,7 @@
 
     python tools/ab_libs.py --configs C2 C3 --rounds 3 --steps 5 xso/base.so pysicalbasedraytracer_amd/libpbr_hip.so
 
-Each round renders every config with every library (default schedule, frames queued back to back on
+Each round renders every config with every library, one context at a time (default schedule, frames queued back to back on
 one stream, as bench.py's timed window); the frame of each library must equal the first library's
 bit for bit.  Prints per (config, library) the median frame ms over the rounds."""
 import argparse
@@ -37,16 +37,14 @@ def main():
         W, H, spp = rd.camera.width, rd.camera.height, rd.spp
         rgb = torch.empty((W * H, 3), dtype=torch.float32, device=dev)
         rgba = torch.empty((W * H, 4), dtype=torch.uint8, device=dev)
-        rens = []
-        for lib in libs:
-            capi._lib = lib
-            r = HipRenderer(0)
-            r.upload(scene)
-            rens.append(r)
         times = [[] for _ in libs]
         ref = None
         for rnd in range(a.rounds):
-            for k, r in enumerate(rens):
+            for k, lib in enumerate(libs):
+                # one context at a time: a Path/VolPath context holds ~60 GB of queues (3 lanes)
+                capi._lib = lib
+                r = HipRenderer(0)
+                r.upload(scene)
                 r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
                 r.sync()
                 torch.cuda.synchronize(dev)
@@ -64,11 +62,10 @@ def main():
                       flush=True)
                 if not same:
                     print(f"  differing pixels: {int((frame != ref).any(axis=1).sum())}", flush=True)
+                r.close()
         for k in range(len(libs)):
             print(f"RESULT {cfg} {a.libs[k]}: median {statistics.median(times[k]):.3f} ms "
                   f"(min {min(times[k]):.3f}, {len(times[k])} rounds)", flush=True)
-        for r in rens:
-            r.close()
 
 
 if __name__ == "__main__":
