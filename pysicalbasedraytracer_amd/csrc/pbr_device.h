@@ -303,7 +303,7 @@ struct QuadSlots {   // one quad node's four slots in visit order
     int ref[4];
     bool k[4];       // slab passes (box valid)
 };
-template <bool ANY>
+template <bool ANY, bool SCALAR = kScalarLoads>
 __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const Ray& r, f3 inv, bool n0, bool n1, bool n2,
                                            QuadSlots* q) {
     float4 LX, LY, LZ, HX, HY, HZ, R;
@@ -311,7 +311,7 @@ __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const 
     // Coherent waves (a pixel's samples share a wave) often have every active lane at the
     // same node: then it is fetched once through the scalar cache.
     const int ucur = __builtin_amdgcn_readfirstlane(cur);
-    if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
+    if (SCALAR && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
         const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
         LX = as_f4(w[0]); LY = as_f4(w[1]); LZ = as_f4(w[2]); HX = as_f4(w[3]); HY = as_f4(w[4]);
         HZ = as_f4(w[5]); R = as_f4(w[6]);
@@ -908,8 +908,9 @@ PBR_HD void concentric_disk(float u0, float u1, float* dx, float* dy) {
     float theta, r;
     if (fabsf(ox) > fabsf(oy)) { r = ox; theta = kPiOver4 * (oy / ox); }
     else { r = oy; theta = kPiOver2 - kPiOver4 * (ox / oy); }
-    *dx = r * t_cos(theta);
-    *dy = r * t_sin(theta);
+    const SinCos sc = t_sincos(theta);
+    *dx = r * sc.c;
+    *dy = r * sc.s;
 }
 PBR_HD f3 cosine_hemisphere(float u0, float u1) {
     float dx, dy;
@@ -989,11 +990,12 @@ struct BSDF {                    // Reflection.h:101-149: frame + the material's
     }
 };
 PBR_HD bool matches(const Lobe& l, int t) { return (l.type & t) == l.type; }
-PBR_HD int num_components(const BSDF& b, int flags) {
+PBR_HD int num_components(const MatTemplate& mt, int flags) {
     int k = 0;
-    for (int i = 0; i < b.mt->nLobes; ++i) if (matches(b.mt->lobes[i], flags)) ++k;
+    for (int i = 0; i < mt.nLobes; ++i) if (matches(mt.lobes[i], flags)) ++k;
     return k;
 }
+PBR_HD int num_components(const BSDF& b, int flags) { return num_components(*b.mt, flags); }
 template <int K = kAllLobes>
 PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:56-71
     f3 wi = b.to_local(wiW), wo = b.to_local(woW);
@@ -1208,7 +1210,8 @@ PBR_HD f3 uniform_sphere(float u0, float u1) {   // Sampling.cpp:59-64
     float z = 1 - 2 * u0;
     float r = sqrtf(mx((float)0, (float)1 - z * z));
     float phi = 2 * kPi * u1;
-    return mk(r * t_cos(phi), r * t_sin(phi), z);
+    const SinCos sc = t_sincos(phi);
+    return mk(r * sc.c, r * sc.s, z);
 }
 struct VisPt { f3 p, pError, n; int medIn, medOut; };
 __device__ __forceinline__ void tri_verts(const DeviceScene& S, int slot, f3* p0, f3* p1, f3* p2) {
@@ -1237,8 +1240,9 @@ __device__ __noinline__ InfLiSample inf_sample_li(const InfDev* Ep, float u0, fl
     if (mapPdf == 0) { o.pdf = 0; return o; }
     o.mapped = true;
     float theta = d1 * kPi, phi = d0 * 2 * kPi;
-    float cosTheta = t_cos(theta), sinTheta = t_sin(theta);
-    float sinPhi = t_sin(phi), cosPhi = t_cos(phi);
+    const SinCos st = t_sincos(theta), sp_ = t_sincos(phi);
+    float cosTheta = st.c, sinTheta = st.s;
+    float sinPhi = sp_.s, cosPhi = sp_.c;
     o.wi = xf_vector(E.l2w, mk(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
     o.pdf = mapPdf / (2 * kPi * kPi * sinTheta);
     if (sinTheta == 0) o.pdf = 0;

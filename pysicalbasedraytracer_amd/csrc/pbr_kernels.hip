@@ -811,6 +811,7 @@ struct DevBuf {
 struct WfBufs {
     DevBuf wqO[2], wqD[2], wqId[2], wqHit[2], wsO, wsD, wsC, wsId, wRecA, wRecF, wRecP, wDepth, wIndex, wCnt;
     DevBuf wsO2, wsD2, wsC2, wsId2;   // Whitted: second shadow queue (levels alternate)
+    DevBuf wsW, wsW2;                 // Whitted under a SkyBox: the shadow entries' directions
     DevBuf wRecC, wRecV;              // multi-light Whitted: per-light contributions, visibility
     // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
     DevBuf wqS0[2], wqS1[2];          // Path/VolPath: the path state carried with the ray
@@ -1175,6 +1176,8 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     // nL shadow rays per shading event; the chunk shrinks so those stay near 6 GB per lane
     const int nL = (int)ctx->host.lights.size();
     const bool ml = nL != 1;
+    // one SkyBox light: its radiance is looked up by the shadow kernel (k_wf_shade)
+    const bool skyDeferred = !ml && ctx->host.lights[0].type == LT_SKY;
     // records per sample and level: A, F+cos, pdf (36 B) + per light 17 B; the chunk shrinks so
     // they stay under 8 GB per lane (C2: 5 levels × 36 B × 2^25 = 6 GB)
     int maxLog2 = 25;
@@ -1213,6 +1216,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         }
         HIP_TRY(B.wsO.ensure(sqcap * 16)); HIP_TRY(B.wsD.ensure(sqcap * 16));
         HIP_TRY(B.wsC.ensure(qcap * 16)); HIP_TRY(B.wsId.ensure(sqcap * 4));
+        if (skyDeferred) HIP_TRY(B.wsW.ensure(sqcap * 16));
         if (ml) { HIP_TRY(B.wRecC.ensure(cap * 16 * levels * nL)); HIP_TRY(B.wRecV.ensure(cap * levels * nL)); }
         HIP_TRY(B.wRecA.ensure(cap * 16 * levels)); HIP_TRY(B.wRecF.ensure(cap * 16 * levels));
         HIP_TRY(B.wRecP.ensure(cap * 4 * levels)); HIP_TRY(B.wDepth.ensure(cap * 4));
@@ -1220,6 +1224,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         if (shadowOverlap) {
             HIP_TRY(B.wsO2.ensure(sqcap * 16)); HIP_TRY(B.wsD2.ensure(sqcap * 16));
             HIP_TRY(B.wsC2.ensure(qcap * 16)); HIP_TRY(B.wsId2.ensure(sqcap * 4));
+            if (skyDeferred) HIP_TRY(B.wsW2.ensure(sqcap * 16));
             if (!ctx->shadowStream[l]) {
                 HIP_TRY(hipStreamCreateWithFlags(&ctx->shadowStream[l], hipStreamNonBlocking));
                 for (int k = 0; k < kWfMaxDepth + 2; ++k) {
@@ -1234,6 +1239,8 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         std::memset(&W, 0, sizeof(W));
         W.P = P;
         W.so = (float4*)B.wsO.p; W.sd = (float4*)B.wsD.p; W.sc = (float4*)B.wsC.p; W.sid = (int*)B.wsId.p;
+        W.sw = (float4*)B.wsW.p;
+        W.skyDeferred = skyDeferred ? 1 : 0;
         W.shadowSeg = cnt + 2 * kWfBlocks;
         W.segCap = ch.segCap;
         W.shadowSegCap = ch.segCap * lightsPerShade;
@@ -1288,6 +1295,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 const bool odd = level & 1;
                 W.so = (float4*)(odd ? B.wsO2.p : B.wsO.p); W.sd = (float4*)(odd ? B.wsD2.p : B.wsD.p);
                 W.sc = (float4*)(odd ? B.wsC2.p : B.wsC.p); W.sid = (int*)(odd ? B.wsId2.p : B.wsId.p);
+                W.sw = (float4*)(odd ? B.wsW2.p : B.wsW.p);
                 W.shadowSeg = cntL[l] + (odd ? 3 : 2) * kWfBlocks;
                 // shade(L) refills the queue shadow(L-2) read
                 if (level >= 2) HIP_TRY(hipStreamWaitEvent(st, ctx->evShadow[l][level - 2], 0));
@@ -1302,8 +1310,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 else if (simple) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
                 else if (matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, true>), gstride, blk, 0, st, W, l0);
                 else hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, false>), gstride, blk, 0, st, W, l0);
-            } else if (fuseCamera && l0 && mm) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
+            } else if (fuseCamera && l0 && mm && skyDeferred) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true, true>), gstride, blk, 0, st, W, l0);
+            else if (fuseCamera && l0 && mm) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
             else if (fuseCamera && l0) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
+            else if (mm && matsLds && skyDeferred) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_SHADE_OCC_MM, false, true>), gstride, blk, 0, st, W, l0);
             else if (mm && matsLds) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
@@ -1312,7 +1322,8 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             if (l0) prof_host(ctx, KP_WF_SHADE, 0, (unsigned long long)W.nSamples);
             if (l0 && fuseCamera && !textured && !ml) prof_host(ctx, KP_WF_SHADE, 6, (unsigned long long)W.nSamples);
             if (int rc = prof_sums(ctx, st, KP_WF_SHADE, {l0 ? nullptr : W.cur.segCount, W.shadowSeg, nullptr, nullptr,
-                                                          W.next.segCount, l0 ? nullptr : W.cur.segCount})) return rc;
+                                                          W.next.segCount, l0 ? nullptr : W.cur.segCount, nullptr,
+                                                          skyDeferred ? W.shadowSeg : nullptr})) return rc;
             if (shadowOverlap) {
                 HIP_TRY(hipEventRecord(ctx->evShade[l][level], st));
                 HIP_TRY(hipStreamWaitEvent(sst, ctx->evShade[l][level], 0));
@@ -2064,9 +2075,10 @@ int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int*
         case KP_WF_CAMERA: return 52 * f[0];                                   // o, d, hit, index
         case KP_WF_SHADE:   // ray + hit + index + recA + depth; shadow; next + recF/P
             // (f[6] level-0 samples of fused launches: those read no ray, hit or index; they write the
-            // index, 4 B)
-            return 72 * f[0] - 48 * f[6] + 4 * f[5] + 52 * f[1] + 52 * f[4];
-        case KP_WF_SHADOW: return 52 * f[0] + 32 * f[1];                       // o, d, contribution, id; recA RMW
+            // index, 4 B; f[7] shadow pushes carrying a SkyBox direction, 16 B)
+            return 72 * f[0] - 48 * f[6] + 4 * f[5] + 52 * f[1] + 52 * f[4] + 16 * f[7];
+        case KP_WF_SHADOW:   // o, d, contribution, id; recA RMW (f[2] of the visible: + the SkyBox direction)
+            return 52 * f[0] + 32 * f[1] + 16 * f[2];
         case KP_WF_EXTEND: return 64 * f[0];                                   // o, d read; o, hit written
         case KP_WF_FINISH: return 16 * f[0] + 4 * f[1] + 16 * c[KP_WF_SHADE][0] + 20 * c[KP_WF_SHADE][4];
         case KP_WFP_CAMERA: return 52 * f[0];                                  // o, d, hit, index

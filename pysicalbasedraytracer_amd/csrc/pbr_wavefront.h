@@ -58,6 +58,10 @@ struct WfParams {
     WfQueue cur, next;
     // shadow queue (segmented like the ray queues)
     float4* so; float4* sd; float4* sc; int* sid; int* shadowSeg;
+    // SkyBox light (single-light schedule): the sampled direction wi of each shadow entry; the sky's
+    // radiance is looked up in k_wf_shadow, for visible rays only (skyDeferred)
+    float4* sw;
+    int skyDeferred;
     // per-sample records, [depth * cap + sample]
     float4* recA;          // A.rgb, flags (bit0: add +0 at the end)
     float4* recF;          // F.rgb, cos term
@@ -191,6 +195,10 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 #define PBR_REFILL_OCC_TR 6
 #endif
 constexpr int kRefill = PBR_REFILL;
+#ifndef PBR_STREAM_SCALAR
+#define PBR_STREAM_SCALAR 1
+#endif
+constexpr bool kStreamScalar = kScalarLoads && PBR_STREAM_SCALAR != 0;
 static_assert(kRefill >= 1 && kRefill <= 64, "refill threshold: idle lanes of a 64-wide wave");
 // LDS short-stack entries of the camera kernels.  They have no segment scan, so 7 workgroups per CU
 // would fit 10 entries (20 KB): C2's camera kernel then took 8.95 → 8.02 ms/frame, but the other
@@ -268,7 +276,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             while (true) {
                 float4 v0, v1, v2;
                 const int uslot = __builtin_amdgcn_readfirstlane(slot);
-                if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {
+                if (kStreamScalar && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {
                     const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
                     v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
                 } else {
@@ -291,7 +299,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             }
         } else {
             QuadSlots q;
-            quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
+            quad_slots<ANY, kStreamScalar>(S, cur, r, inv, n0, n1, n2, &q);
             const float tM = r.tMax;
             const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
                        p3 = q.k[3] && q.t[3] < tM;
@@ -488,10 +496,18 @@ __device__ __forceinline__ void camera_trace(const WfParams& W, bool active, int
 // The walk is the camera kernel's wave packet.  Measured (bit-identical, C2 frame ms): 17.33-17.39
 // → 17.18 (profiles/r3_fused_ab.log).  Tracing the continuations inside the later shades as well
 // (no extend launch) was slower: 17.46.
+//
+// SKY (untextured lobes, the scene's one light is a SkyBox — C2): the kernel holds only the SkyBox
+// branches, and the light sample's direction wi = UniformSampleSphere(u) is computed before the hit's
+// geometry, where few values are live across its out-of-line sin/cos call (the calls clobber every
+// caller-saved VGPR; around the late call the shade spilled its whole shading state).  The draw is
+// the light loop's own (same dimensions, same sample index), made under the same condition: a
+// material make_bsdf accepts, with a non-specular lobe.
 template <int LOBES, bool MATS_LDS,
           int OCC = (LOBES & ~kSimpleLobes) ? 2 : (LOBES == kMatteMirrorLobes ? PBR_WF_SHADE_OCC_MM : PBR_WF_SHADE_OCC),
-          bool CAMERA = false>
+          bool CAMERA = false, bool SKY = false>
 __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
+    static_assert(!SKY || (LOBES & kTexturedLobes) == 0, "the SkyBox variant is untextured");
     const KParams& P = W.P;
     const DeviceScene& S = P.S;
     stage_halton_lds(P.smp);
@@ -519,6 +535,8 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
         int id = 0, depth = 0, dim = 0, emitDepth = 0;
         Ray ray, shadow, cont;
         rgb contrib = sp(0.f);
+        float skyCos = 0.f;
+        f3 skyWi = mk(0, 0, 0);
         float4 o = make_float4(0.f, 0.f, 0.f, 0.f), d = o, hr = o;
         uint32_t camIndex = 0;
         if constexpr (CAMERA) camera_trace(W, active, q, &o, &d, &hr, &camIndex);   // level 0 only
@@ -534,10 +552,23 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
             size_t ri = (size_t)depth * W.cap + id;
             if (slot < 0) {   // miss: Σ over all lights of Le (F4)
                 rgb L = sp(0.f);
-                for (int i = 0; i < S.nLights; ++i) L = L + light_Le(S, S.lights[i], ray);
+                if constexpr (SKY) L = L + light_Le(S, S.lights[0], ray);
+                else for (int i = 0; i < S.nLights; ++i) L = L + light_Le(S, S.lights[i], ray);
                 W.recA[ri] = make_float4(L.r, L.g, L.b, 0.f);
                 W.depthOf[id] = depth;
             } else {
+                f3 skyDir = mk(0, 0, 0);
+                if constexpr (SKY) {
+                    const int mat = S.primInfo[slot].y;
+                    if (mat >= 0 && mats[2 * mat].valid && num_components(mats[2 * mat], BSDF_ALL & ~BSDF_SPECULAR) > 0) {
+                        SState t;
+                        t.index = CAMERA ? camIndex : W.sampleIndex[id];
+                        t.sid = id; t.dim = dim; t.px = t.py = 0;
+                        float a, b;
+                        get2d<true>(P.smp, t, &a, &b);
+                        skyDir = uniform_sphere(a, b);
+                    }
+                }
                 Isect isect;
                 int flags = __float_as_int(S.triVerts[3 * (size_t)slot].w);
                 if (flags & PRIM_SPHERE) sphere_si(S.spheres[__float_as_int(S.triVerts[3 * (size_t)slot].x)], ray, ray.tMax, &isect);
@@ -571,22 +602,24 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                             VisPt vis;
                             const DLight& light = S.lights[0];
                             rgb Li;
-                            if (light.type == LT_SKY) {
-                                wi = uniform_sphere(a, b);
-                                pdf = 1.f / (4 * kPi);
+                            if (SKY || light.type == LT_SKY) {
+                                // The sky's radiance Li(wi) (atan2, asin and a texel gather) moves to the
+                                // shadow kernel, evaluated for the rays that get through: the term is
+                                // f·Li·|wi·n|/pdf added when Li is not black and the ray is unoccluded,
+                                // and neither test has side effects, so the order does not matter.  The
+                                // entry carries f, |wi·n| and wi (W.sw); the sum is formed there in the
+                                // same operation order.
+                                wi = SKY ? skyDir : uniform_sphere(a, b);   // SKY: drawn above, same (a, b)
                                 vis.p = isect.p + wi * (2 * light.worldRadius); vis.pError = mk(0, 0, 0); vis.n = mk(0, 0, 0);
                                 rgb f = bsdf_f<LOBES>(bsdf, wo, wi, BSDF_ALL);
-                                if (!black(f)) {
-                                    float ul, vl;
-                                    sphere_uv(normalize(wi), &ul, &vl);
-                                    Li = light.envW > 0 ? sky_value(S, light, ul, vl) : sp(0.f);
-                                    if (!black(Li)) {
-                                        contrib = f * Li * absdot(wi, n) / pdf;
-                                        shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
-                                        pushShadow = true;
-                                    }
+                                if (!black(f) && light.envW > 0) {
+                                    contrib = f;
+                                    skyCos = absdot(wi, n);
+                                    skyWi = wi;
+                                    shadow = spawn_ray_to(isect, vis.p, vis.pError, vis.n);
+                                    pushShadow = true;
                                 }
-                            } else {
+                            } else if constexpr (!SKY) {
                                 Li = sample_li(S, light, isect, a, b, &wi, &pdf, &vis);
                                 if (!(black(Li) || pdf == 0)) {
                                     rgb f = bsdf_f<LOBES>(bsdf, wo, wi, BSDF_ALL);
@@ -635,8 +668,9 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
         if (pushShadow) {   // the visibility result lands in the level that emitted the ray
             W.so[si] = make_float4(shadow.o.x, shadow.o.y, shadow.o.z, shadow.tMax);
             W.sd[si] = make_float4(shadow.d.x, shadow.d.y, shadow.d.z, __int_as_float(emitDepth));
-            W.sc[si] = make_float4(contrib.r, contrib.g, contrib.b, 0.f);
+            W.sc[si] = make_float4(contrib.r, contrib.g, contrib.b, skyCos);
             W.sid[si] = id;
+            if (W.skyDeferred) W.sw[si] = make_float4(skyWi.x, skyWi.y, skyWi.z, 0.f);
         }
         int ni = base + wave_push(&s_push[1], pushNext);
         if (pushNext) {
@@ -666,9 +700,20 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
         const bool visible = !traverse<true, false, SHORT>(W.P.S, r, &h, &c);
         trav_diag(W.prof, KP_WF_SHADOW, h);
         if (W.prof) prof_count(W.prof + KP_WF_SHADOW * kProfFields + 1, visible);
+        if (W.prof && W.skyDeferred) prof_count(W.prof + KP_WF_SHADOW * kProfFields + 2, visible);
         if (visible) {
             int id = W.sid[q];
             float4 cc = W.sc[q];
+            if (W.skyDeferred) {   // SkyBox light: cc = (f, |wi·n|), the term f·Li·|wi·n|/pdf (k_wf_shade)
+                const DLight& light = W.P.S.lights[0];
+                const float4 w4 = W.sw[q];
+                float ul, vl;
+                sphere_uv(normalize(mk(w4.x, w4.y, w4.z)), &ul, &vl);
+                const rgb Li = sky_value(W.P.S, light, ul, vl);
+                if (black(Li)) continue;
+                const rgb c = sp3(cc.x, cc.y, cc.z) * Li * cc.w / (1.f / (4 * kPi));
+                cc = make_float4(c.r, c.g, c.b, 0.f);
+            }
             size_t ri = (size_t)__float_as_int(d.w) * W.cap + id;
             float4 A = W.recA[ri];
             A.x = A.x + cc.x; A.y = A.y + cc.y; A.z = A.z + cc.z;
