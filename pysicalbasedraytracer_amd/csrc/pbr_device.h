@@ -303,7 +303,7 @@ struct QuadSlots {   // one quad node's four slots in visit order
     int ref[4];
     bool k[4];       // slab passes (box valid)
 };
-template <bool ANY, bool SCALAR = kScalarLoads>
+template <bool ANY>
 __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const Ray& r, f3 inv, bool n0, bool n1, bool n2,
                                            QuadSlots* q) {
     float4 LX, LY, LZ, HX, HY, HZ, R;
@@ -311,7 +311,7 @@ __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const 
     // Coherent waves (a pixel's samples share a wave) often have every active lane at the
     // same node: then it is fetched once through the scalar cache.
     const int ucur = __builtin_amdgcn_readfirstlane(cur);
-    if (SCALAR && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
+    if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
         const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
         LX = as_f4(w[0]); LY = as_f4(w[1]); LZ = as_f4(w[2]); HX = as_f4(w[3]); HY = as_f4(w[4]);
         HZ = as_f4(w[5]); R = as_f4(w[6]);
@@ -908,9 +908,8 @@ PBR_HD void concentric_disk(float u0, float u1, float* dx, float* dy) {
     float theta, r;
     if (fabsf(ox) > fabsf(oy)) { r = ox; theta = kPiOver4 * (oy / ox); }
     else { r = oy; theta = kPiOver2 - kPiOver4 * (ox / oy); }
-    const SinCos sc = t_sincos(theta);
-    *dx = r * sc.c;
-    *dy = r * sc.s;
+    *dx = r * t_cos(theta);
+    *dy = r * t_sin(theta);
 }
 PBR_HD f3 cosine_hemisphere(float u0, float u1) {
     float dx, dy;
@@ -1123,8 +1122,9 @@ __device__ __forceinline__ bool make_bsdf(const DeviceScene& S, const MatTemplat
 // ---------------------------------------------------------------- lights (Light/*.cpp)
 PBR_HD rgb area_L(const DLight& l, f3 n, f3 w) { return (l.twoSided || dot(n, w) > 0) ? ld3(l.L) : sp(0.f); }
 PBR_HD void sphere_uv(f3 p, float* u, float* v) {   // SkyBoxLight.cpp:12-17
-    float phi = t_atan2(p.z, p.x);
-    float theta = t_asin(p.y);
+    const Atan2Asin a = t_atan2_asin(p.z, p.x, p.y);
+    float phi = a.phi;
+    float theta = a.theta;
     *u = 1 - (phi + kPi) * kInv2Pi;
     *v = (theta + kPiOver2) * kInvPi;
 }
@@ -1240,9 +1240,8 @@ __device__ __noinline__ InfLiSample inf_sample_li(const InfDev* Ep, float u0, fl
     if (mapPdf == 0) { o.pdf = 0; return o; }
     o.mapped = true;
     float theta = d1 * kPi, phi = d0 * 2 * kPi;
-    const SinCos st = t_sincos(theta), sp_ = t_sincos(phi);
-    float cosTheta = st.c, sinTheta = st.s;
-    float sinPhi = sp_.s, cosPhi = sp_.c;
+    float cosTheta = t_cos(theta), sinTheta = t_sin(theta);
+    float sinPhi = t_sin(phi), cosPhi = t_cos(phi);
     o.wi = xf_vector(E.l2w, mk(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
     o.pdf = mapPdf / (2 * kPi * kPi * sinTheta);
     if (sinTheta == 0) o.pdf = 0;

@@ -90,7 +90,7 @@ __device__ __forceinline__ uint32_t sobol_nibbles(const uint32_t* T, uint32_t in
 }
 // index bits 32..51 (columns 32..51 of the 52-column matrices): five more nibble tables, read from
 // global memory only when a sample's index needs them
-__device__ __noinline__ uint32_t sobol_nibbles_hi(const uint32_t* T, uint32_t hi) {
+__device__ __forceinline__ uint32_t sobol_nibbles_hi(const uint32_t* T, uint32_t hi) {
     return T[hi & 15u] ^ T[16 + ((hi >> 4) & 15u)] ^ T[32 + ((hi >> 8) & 15u)] ^ T[48 + ((hi >> 12) & 15u)] ^
            T[64 + ((hi >> 16) & 15u)];
 }

@@ -195,10 +195,7 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 #define PBR_REFILL_OCC_TR 6
 #endif
 constexpr int kRefill = PBR_REFILL;
-#ifndef PBR_STREAM_SCALAR
-#define PBR_STREAM_SCALAR 1
-#endif
-constexpr bool kStreamScalar = kScalarLoads && PBR_STREAM_SCALAR != 0;
+
 static_assert(kRefill >= 1 && kRefill <= 64, "refill threshold: idle lanes of a 64-wide wave");
 // LDS short-stack entries of the camera kernels.  They have no segment scan, so 7 workgroups per CU
 // would fit 10 entries (20 KB): C2's camera kernel then took 8.95 → 8.02 ms/frame, but the other
@@ -276,7 +273,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             while (true) {
                 float4 v0, v1, v2;
                 const int uslot = __builtin_amdgcn_readfirstlane(slot);
-                if (kStreamScalar && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {
+                if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {
                     const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
                     v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
                 } else {
@@ -299,7 +296,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             }
         } else {
             QuadSlots q;
-            quad_slots<ANY, kStreamScalar>(S, cur, r, inv, n0, n1, n2, &q);
+            quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
             const float tM = r.tMax;
             const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
                        p3 = q.k[3] && q.t[3] < tM;
@@ -552,7 +549,12 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
             size_t ri = (size_t)depth * W.cap + id;
             if (slot < 0) {   // miss: Σ over all lights of Le (F4)
                 rgb L = sp(0.f);
-                if constexpr (SKY) L = L + light_Le(S, S.lights[0], ray);
+                if constexpr (SKY) {   // light_Le's SkyBox branch
+                    const DLight& light = S.lights[0];
+                    float u, v;
+                    sphere_uv(normalize(ray.d), &u, &v);
+                    L = L + (light.envW > 0 ? sky_value(S, light, u, v) : sp(0.f));
+                }
                 else for (int i = 0; i < S.nLights; ++i) L = L + light_Le(S, S.lights[i], ray);
                 W.recA[ri] = make_float4(L.r, L.g, L.b, 0.f);
                 W.depthOf[id] = depth;
