@@ -138,17 +138,19 @@ __device__ __forceinline__ SIndex sobol_index(const DeviceSampler& s, int px, in
     return SIndex{(uint32_t)idx, (uint32_t)(idx >> 32)};
 }
 // GlobalSampler::StartPixel / SetSampleNumber: the global index of sample s of pixel (x, y)
+// KIND: the sampler type when the caller knows it (the other types' code is compiled out), else -1
+template <int KIND = -1>
 __device__ __forceinline__ SIndex sample_index(const DeviceSampler& smp, int x, int y, int s) {
-    if (smp.type == PBR_SAMPLER_SOBOL) return sobol_index(smp, x, y, (uint32_t)s);
-    if (smp.type == PBR_SAMPLER_TABLE)   // the table row of (pixel, sample)
+    if (KIND == PBR_SAMPLER_SOBOL || (KIND < 0 && smp.type == PBR_SAMPLER_SOBOL)) return sobol_index(smp, x, y, (uint32_t)s);
+    if (KIND == PBR_SAMPLER_TABLE || (KIND < 0 && smp.type == PBR_SAMPLER_TABLE))   // the table row of (pixel, sample)
         return SIndex{((uint32_t)y * (uint32_t)smp.tableW + (uint32_t)x) * (uint32_t)smp.spp + (uint32_t)s, 0u};
     return SIndex{halton_pixel_offset(hparams(smp), x, y) + (uint32_t)s * (uint32_t)smp.stride, 0u};   // Halton.cpp:61-81
 }
 
-template <bool LDS = false>
+template <bool LDS = false, int KIND = -1>
 __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32_t index, int sid, int dim, int px = 0, int py = 0) {
-    if (s.type == PBR_SAMPLER_SOBOL) return sobol_dimension<LDS>(s, index, sid, dim, px, py);
-    if (s.type == PBR_SAMPLER_TABLE) return table_dimension(s, index, dim);
+    if (KIND == PBR_SAMPLER_SOBOL || (KIND < 0 && s.type == PBR_SAMPLER_SOBOL)) return sobol_dimension<LDS>(s, index, sid, dim, px, py);
+    if (KIND == PBR_SAMPLER_TABLE || (KIND < 0 && s.type == PBR_SAMPLER_TABLE)) return table_dimension(s, index, dim);
     // HaltonSampler::SampleDimension (Halton.cpp:83-92)
     if (dim == 0) return radical_inverse_2(index >> s.baseExp0);
     if (dim == 1) return radical_inverse_b(3u, 0x55555555u, div_prime(index, (uint32_t)s.baseScale1, 0xffffffffu / (uint32_t)s.baseScale1));
@@ -163,24 +165,26 @@ __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32
 }
 // GlobalSampler::Get1D/Get2D (Sampler.cpp:131-143): with no requested sample arrays
 // arrayStartDim == arrayEndDim == 5, so only a Get2D that would straddle dimension 5 is moved.
-template <bool LDS = false>
+template <bool LDS = false, int KIND = -1>
 __device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) {
-    return sample_dimension<LDS>(s, st.index, st.sid, st.dim++, st.px, st.py);
+    return sample_dimension<LDS, KIND>(s, st.index, st.sid, st.dim++, st.px, st.py);
 }
-template <bool LDS = false>
+template <bool LDS = false, int KIND = -1>
 __device__ __forceinline__ void get2d(const DeviceSampler& s, SState& st, float* a, float* b) {
     if (st.dim == 4) st.dim = 5;
-    *a = sample_dimension<LDS>(s, st.index, st.sid, st.dim, st.px, st.py);
-    *b = sample_dimension<LDS>(s, st.index, st.sid, st.dim + 1, st.px, st.py);
+    *a = sample_dimension<LDS, KIND>(s, st.index, st.sid, st.dim, st.px, st.py);
+    *b = sample_dimension<LDS, KIND>(s, st.index, st.sid, st.dim + 1, st.px, st.py);
     st.dim += 2;
 }
 
 // ---------------------------------------------------------------- camera (Perspective.cpp:44-80)
+// PINHOLE: the caller knows lensRadius == 0 (the lens branch is compiled out)
+template <bool PINHOLE = false>
 __device__ __forceinline__ Ray camera_ray(const DeviceCamera& c, float fx, float fy, float l0, float l1) {
     f3 pCam = xf_point(c.rasterToCamera, mk(fx, fy, 0));
     f3 dir = normalize(pCam);
     Ray r = mkray(mk(0, 0, 0), dir, PBR_INF, -1);
-    if (c.lensRadius > 0) {
+    if (!PINHOLE && c.lensRadius > 0) {
         float dx, dy;
         concentric_disk(l0, l1, &dx, &dy);
         float lx = c.lensRadius * dx, ly = c.lensRadius * dy;
@@ -212,16 +216,17 @@ struct KParams {
 // GetCameraSample (Sampler.cpp:10-21) + GenerateRay: pFilm = dims 0,1; time = dim 2 (no motion
 // blur: never read); pLens = dims 3,4, read only by a camera with an aperture (lensRadius > 0), so
 // a pinhole camera skips their scrambled radical inverses and only advances the dimension to 5.
+template <bool PINHOLE = false, int KIND = -1>
 __device__ __forceinline__ Ray camera_sample_ray(const KParams& P, SState& st, int x, int y) {
     float u0, u1, l0 = 0.f, l1 = 0.f;
-    get2d(P.smp, st, &u0, &u1);
-    if (P.cam.lensRadius > 0) {
+    get2d<false, KIND>(P.smp, st, &u0, &u1);
+    if (!PINHOLE && P.cam.lensRadius > 0) {
         get1d(P.smp, st);
         get2d(P.smp, st, &l0, &l1);
     } else {
         st.dim = 5;
     }
-    return camera_ray(P.cam, (float)x + u0, (float)y + u1, l0, l1);
+    return camera_ray<PINHOLE>(P.cam, (float)x + u0, (float)y + u1, l0, l1);
 }
 
 // ---------------------------------------------------------------- direct lighting (Integrator.cpp:46-177)
@@ -1178,6 +1183,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const bool ml = nL != 1;
     // one SkyBox light: its radiance is looked up by the shadow kernel (k_wf_shade)
     const bool skyDeferred = !ml && ctx->host.lights[0].type == LT_SKY;
+    const bool skyHalton = skyDeferred && P.smp.type == PBR_SAMPLER_HALTON;   // the SkyBox shade variants (C2)
     // records per sample and level: A, F+cos, pdf (36 B) + per light 17 B; the chunk shrinks so
     // they stay under 8 GB per lane (C2: 5 levels × 36 B × 2^25 = 6 GB)
     int maxLog2 = 25;
@@ -1310,10 +1316,10 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 else if (simple) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
                 else if (matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, true>), gstride, blk, 0, st, W, l0);
                 else hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, false>), gstride, blk, 0, st, W, l0);
-            } else if (fuseCamera && l0 && mm && skyDeferred) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true, true>), gstride, blk, 0, st, W, l0);
+            } else if (fuseCamera && l0 && mm && skyHalton && !(P.cam.lensRadius > 0)) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true, true>), gstride, blk, 0, st, W, l0);
             else if (fuseCamera && l0 && mm) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
             else if (fuseCamera && l0) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
-            else if (mm && matsLds && skyDeferred) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_SHADE_OCC_MM, false, true>), gstride, blk, 0, st, W, l0);
+            else if (mm && matsLds && skyHalton) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_SHADE_OCC_MM, false, true>), gstride, blk, 0, st, W, l0);
             else if (mm && matsLds) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);

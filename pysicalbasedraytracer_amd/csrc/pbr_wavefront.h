@@ -455,6 +455,7 @@ __shared__ MatTemplate s_mats[kLdsMats];
 // k_wf_camera_extend's work for queue position q inside the level-0 shade (CAMERA): the camera
 // sample's ray and its closest hit, as the queue entry the shade would have read.  Every lane of
 // the wave calls it (the packet walk is wave-wide); `active` lanes hold a sample.
+template <bool PINHOLE = false, int KIND = -1>
 __device__ __forceinline__ void camera_trace(const WfParams& W, bool active, int q, float4* o, float4* d, float4* hr,
                                              uint32_t* index) {
     const KParams& P = W.P;
@@ -466,12 +467,12 @@ __device__ __forceinline__ void camera_trace(const WfParams& W, bool active, int
         int x, y;
         pixel_xy(P, W.chunkPix0 + lp, &x, &y);
         SState st;
-        st.index = sample_index(P.smp, x, y, s).lo;
+        st.index = sample_index<KIND>(P.smp, x, y, s).lo;
         st.sid = s;
         st.dim = 0;
         st.px = x;
         st.py = y;
-        r = camera_sample_ray(P, st, x, y);
+        r = camera_sample_ray<PINHOLE, KIND>(P, st, x, y);
         dim = st.dim;
         *index = st.index;
         W.sampleIndex[q] = st.index;   // later levels read it by sample id
@@ -494,8 +495,8 @@ __device__ __forceinline__ void camera_trace(const WfParams& W, bool active, int
 // → 17.18 (profiles/r3_fused_ab.log).  Tracing the continuations inside the later shades as well
 // (no extend launch) was slower: 17.46.
 //
-// SKY (untextured lobes, the scene's one light is a SkyBox — C2): the kernel holds only the SkyBox
-// branches, and the light sample's direction wi = UniformSampleSphere(u) is computed before the hit's
+// SKY (untextured lobes, the scene's one light is a SkyBox, a pinhole camera — C2): the kernel
+// holds only the SkyBox branches and no lens sampling, and the light sample's direction wi = UniformSampleSphere(u) is computed before the hit's
 // geometry, where few values are live across its out-of-line sin/cos call (the calls clobber every
 // caller-saved VGPR; around the late call the shade spilled its whole shading state).  The draw is
 // the light loop's own (same dimensions, same sample index), made under the same condition: a
@@ -505,6 +506,7 @@ template <int LOBES, bool MATS_LDS,
           bool CAMERA = false, bool SKY = false>
 __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     static_assert(!SKY || (LOBES & kTexturedLobes) == 0, "the SkyBox variant is untextured");
+    constexpr int kSmp = SKY ? PBR_SAMPLER_HALTON : -1;   // the SkyBox variants run Halton frames only
     const KParams& P = W.P;
     const DeviceScene& S = P.S;
     stage_halton_lds(P.smp);
@@ -536,7 +538,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
         f3 skyWi = mk(0, 0, 0);
         float4 o = make_float4(0.f, 0.f, 0.f, 0.f), d = o, hr = o;
         uint32_t camIndex = 0;
-        if constexpr (CAMERA) camera_trace(W, active, q, &o, &d, &hr, &camIndex);   // level 0 only
+        if constexpr (CAMERA) camera_trace<SKY, kSmp>(W, active, q, &o, &d, &hr, &camIndex);   // level 0 only
         else if (active) { o = W.cur.o[q]; d = W.cur.d[q]; hr = W.cur.hit[q]; }
         if (active) {
             id = level0 ? q : W.cur.id[q];
@@ -567,7 +569,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                         t.index = CAMERA ? camIndex : W.sampleIndex[id];
                         t.sid = id; t.dim = dim; t.px = t.py = 0;
                         float a, b;
-                        get2d<true>(P.smp, t, &a, &b);
+                        get2d<true, kSmp>(P.smp, t, &a, &b);
                         skyDir = uniform_sphere(a, b);
                     }
                 }
@@ -593,7 +595,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                     st.px = st.py = 0;   // dims >= 2 only past the camera
                     {   // the single light (WhittedIntegrator.cpp:39-54)
                         float a, b;
-                        get2d<true>(P.smp, st, &a, &b);
+                        get2d<true, kSmp>(P.smp, st, &a, &b);
                         // Reordered but equivalent: f(wo, wi) does not depend on Li, and nothing is
                         // added when f is black — so the light's radiance (for the SkyBox: atan2,
                         // asin and an env gather) is only evaluated when f is not black, and a
@@ -646,7 +648,7 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
                         float pdf = 0;
                         int stype = 0;
                         float a, b;
-                        get2d<true>(P.smp, st, &a, &b);
+                        get2d<true, kSmp>(P.smp, st, &a, &b);
                         // only L_SPEC_R lobes match BSDF_REFLECTION | BSDF_SPECULAR
                         rgb f = bsdf_sample<(1 << L_SPEC_R)>(bsdf, wo, &wi, a, b, &pdf, BSDF_REFLECTION | BSDF_SPECULAR, &stype);
                         if (!black(f) && pdf > 0.f && absdot(wi, isect.sn) != 0.f && depth + 1 < kWfMaxDepth) {
