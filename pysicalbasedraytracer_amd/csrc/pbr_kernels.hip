@@ -1366,6 +1366,8 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
     const bool micro = (lobes & ~kMicroLobes) == 0;   // Lambert + microfacet reflection/transmission (C4, C5)
+    // the frame's sampler, for the shade variants specialised on it (C3 Sobol, C4 / C5 Halton)
+    const bool halton = P.smp.type == PBR_SAMPLER_HALTON, sobol = P.smp.type == PBR_SAMPLER_SOBOL;
     const bool mm = (lobes & ~kMatteMirrorLobes) == 0;   // Lambert + mirror only (C3)
     const bool textured = (lobes & kTexturedLobes) != 0;
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats;   // templates staged in LDS
@@ -1467,15 +1469,18 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
                     if (textured) hipLaunchKernelGGL((k_wfv_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, V, l0);
                     else if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0);
                     else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, st, V, l0);
+                    else if (micro && matsLds && halton) hipLaunchKernelGGL((k_wfv_shade<kMicroLobes, true, PBR_WFV_OCC, PBR_SAMPLER_HALTON>), gshade, blk, 0, st, V, l0);
                     else if (micro && matsLds) hipLaunchKernelGGL((k_wfv_shade<kMicroLobes, true>), gshade, blk, 0, st, V, l0);
                     else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0);
                     else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0));
             } else {
                 PROF_LAUNCH(KP_WFP_SHADE, st,
                     if (textured) hipLaunchKernelGGL((k_wfp_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, X, l0);
+                    else if (mm && matsLds && sobol) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true, PBR_WFP_OCC, PBR_SAMPLER_SOBOL>), gshade, blk, 0, st, X, l0);
                     else if (mm && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true>), gshade, blk, 0, st, X, l0);
                     else if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
                     else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0);
+                    else if (micro && matsLds && halton) hipLaunchKernelGGL((k_wfp_shade<kMicroLobes, true, PBR_WFP_OCC, PBR_SAMPLER_HALTON>), gshade, blk, 0, st, X, l0);
                     else if (micro && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMicroLobes, true>), gshade, blk, 0, st, X, l0);
                     else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, st, X, l0);
                     else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, st, X, l0));

@@ -89,7 +89,9 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
 #ifndef PBR_WFP_OCC
 #define PBR_WFP_OCC 3
 #endif
-template <int LOBES, bool MATS_LDS, int OCC = PBR_WFP_OCC>
+// SMP: the frame's sampler type when the launch knows it (the other samplers' code — and the kernel
+// parameters it reads, which otherwise spill from SGPRs into VGPR lanes — is compiled out), else -1
+template <int LOBES, bool MATS_LDS, int OCC = PBR_WFP_OCC, int SMP = -1>
 __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0) {
     WfParams& W = X.W;
     const KParams& P = W.P;
@@ -181,11 +183,11 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                     if (num_components(bsdf, BSDF_ALL & ~BSDF_SPECULAR) > 0 && S.nLights > 0) {
                         // UniformSampleOneLight: light choice, then EstimateDirect's two strategies
                         float pmf;
-                        const int li = sample_light(S, get1d<true>(P.smp, st), &pmf);
+                        const int li = sample_light(S, get1d<true, SMP>(P.smp, st), &pmf);
                         if (pmf != 0) {
                             float uL0, uL1, uS0, uS1;
-                            get2d<true>(P.smp, st, &uL0, &uL1);
-                            get2d<true>(P.smp, st, &uS0, &uS1);
+                            get2d<true, SMP>(P.smp, st, &uL0, &uL1);
+                            get2d<true, SMP>(P.smp, st, &uS0, &uS1);
                             const DLight& light = S.lights[li];
                             const bool delta = light.type == LT_POINT;
                             const int flagsNS = BSDF_ALL & ~BSDF_SPECULAR;
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
             float pdf = 0;
             int flags = 0;
             float u0, u1;
-            get2d<true>(P.smp, st, &u0, &u1);
+            get2d<true, SMP>(P.smp, st, &u0, &u1);
             rgb f = bsdf_sample<LOBES>(bsdf, woPath, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
             if (!(black(f) || pdf == 0.f)) {
                 beta = beta * (f * absdot(wi, isect.sn) / pdf);
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                 rgb rrBeta = beta * etaScale;
                 if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
                     float qq = mx((float).05, 1 - maxval(rrBeta));
-                    if (get1d<true>(P.smp, st) < qq) stop = true;
+                    if (get1d<true, SMP>(P.smp, st) < qq) stop = true;
                     else beta = beta / (1 - qq);
                 }
                 if (!stop) {

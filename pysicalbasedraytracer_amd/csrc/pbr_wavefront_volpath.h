@@ -40,7 +40,7 @@ __device__ __forceinline__ void set_interface(const DeviceScene& S, Isect* it, i
 #ifndef PBR_WFV_OCC
 #define PBR_WFV_OCC 3
 #endif
-template <int LOBES, bool MATS_LDS, int OCC = PBR_WFV_OCC>
+template <int LOBES, bool MATS_LDS, int OCC = PBR_WFV_OCC, int SMP = -1>   // SMP: as k_wfp_shade's
 __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0) {
     WfpParams& X = V.X;
     WfParams& W = X.W;
@@ -123,9 +123,9 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             // HomogeneousMedium::Sample (HomogeneousMedium.cpp:15-45)
             if (ray.medium >= 0) {
                 const float* md = S.media + 10 * ray.medium;
-                int channel = (int)(get1d<true>(P.smp, st) * 3);
+                int channel = (int)(get1d<true, SMP>(P.smp, st) * 3);
                 if (channel > 2) channel = 2;
-                float dist = -t_log(1 - get1d<true>(P.smp, st)) / md[6 + channel];
+                float dist = -t_log(1 - get1d<true, SMP>(P.smp, st)) / md[6 + channel];
                 float t = mn(dist / len(ray.d), ray.tMax);
                 bool sampled = t < ray.tMax;
                 if (sampled) {
@@ -167,11 +167,11 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 // UniformSampleOneLight(handleMedia = true) / EstimateDirect
                 const Isect& ref = isect;
                 float pmf;
-                const int li = sample_light(S, get1d<true>(P.smp, st), &pmf);
+                const int li = sample_light(S, get1d<true, SMP>(P.smp, st), &pmf);
                 if (pmf != 0) {
                     float uL0, uL1, uS0, uS1;
-                    get2d<true>(P.smp, st, &uL0, &uL1);
-                    get2d<true>(P.smp, st, &uS0, &uS1);
+                    get2d<true, SMP>(P.smp, st, &uL0, &uL1);
+                    get2d<true, SMP>(P.smp, st, &uS0, &uS1);
                     const DLight& light = S.lights[li];
                     const bool delta = light.type == LT_POINT;
                     const int flagsNS = BSDF_ALL & ~BSDF_SPECULAR;
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 if (mediumEvent) {   // HenyeyGreenstein::Sample_p, then the ray leaves the interaction
                     f3 wo = -ray.d, wi;
                     float u0, u1;
-                    get2d<true>(P.smp, st, &u0, &u1);
+                    get2d<true, SMP>(P.smp, st, &u0, &u1);
                     hg_sample(g, wo, &wi, u0, u1);
                     cont = spawn_ray(isect, wi);
                     specularBounce = false;
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                     float pdf = 0;
                     int flags = 0;
                     float u0, u1;
-                    get2d<true>(P.smp, st, &u0, &u1);
+                    get2d<true, SMP>(P.smp, st, &u0, &u1);
                     rgb f = bsdf_sample<LOBES>(bsdf, wo, &wi, u0, u1, &pdf, BSDF_ALL, &flags);
                     if (!(black(f) || pdf == 0.f)) {
                         beta = beta * (f * absdot(wi, isect.sn) / pdf);
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                 rgb rrBeta = beta * etaScale;
                 if (maxval(rrBeta) < P.rrThreshold && bounces > 3) {
                     float qq = mx((float).05, 1 - maxval(rrBeta));
-                    if (get1d<true>(P.smp, st) < qq) stop = true;
+                    if (get1d<true, SMP>(P.smp, st) < qq) stop = true;
                     else beta = beta / (1 - qq);
                 }
                 if (!stop) {
