@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_ANY) void k_wfp_shadow(WfpParam
                 return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
             },
             [&](int q, bool hit, const Ray&, const HitRec&) {
-                if (W.prof) atomicAdd(W.prof + KP_WFP_SHADOW * kProfFields + 1, (unsigned long long)(hit ? 0 : 1));
+                if (W.prof) prof_count(W.prof + KP_WFP_SHADOW * kProfFields + 1, !hit);   // one atomic per wave
                 if (!hit) X.dFlags[W.sid[q]] |= kWfpVisible;   // the only writer of this record in this launch
             },
             W.prof, KP_WFP_SHADOW);
