@@ -11,6 +11,10 @@ ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
+# a line a minute under gpurun_out/: a C4 bench runs for minutes before it prints its one line
+( while true; do date >> "$OUT/heartbeat.log"; sleep 60; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 for cfg in ${CONFIGS:-C2}; do
   lc=$(echo "$cfg" | tr 'A-Z' 'a-z')
   S=${STEPS:-5}; [ "$cfg" = C4 ] && S=${STEPS_C4:-2}
