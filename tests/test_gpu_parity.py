@@ -250,6 +250,19 @@ def test_errors_fail_loudly(hip):
     fresh.close()
 
 
+def test_whitted_serial_schedule_is_the_same_frame(hip):
+    """bench.py times every kernel alone in a serial window (one lane, shadow rays on the render
+    stream); that schedule renders the benchmarked frame's bits (multi-chunk, fused level 0)."""
+    s, rd = scenes.config_c2(160, 90, 32, mesh=small_dragon(64))
+    hip.upload(s)
+    hip.set_schedule(chunk_log2=16)
+    a, a8, _ = hip.render(rd)
+    hip.set_schedule(chunk_log2=16, serial=1)
+    b, b8, _ = hip.render(rd)
+    hip.set_schedule()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(a8, b8)
+
+
 def test_wavefront_equals_megakernel(hip):
     """The wavefront Whitted schedule and the megakernel produce identical bits."""
     s, rd = scenes.config_c2(160, 90, 8, mesh=small_dragon(64))
@@ -374,7 +387,8 @@ def test_sobol_caller_matrices_and_pow2_spp(hip):
 # direct records carried over chunks), and 2^10-sample chunks (33-41 chunks: the balanced chunk size
 # that frames of 24 or more chunks get, as C4's 254 chunks do).
 SCHEDULES = {"one_chunk": {}, "c12_3lanes": {"chunk_log2": 12, "lanes": 3},
-             "c10_balanced": {"chunk_log2": 10, "lanes": 3}, "c12_2lanes": {"chunk_log2": 12, "lanes": 2}}
+             "c10_balanced": {"chunk_log2": 10, "lanes": 3}, "c12_2lanes": {"chunk_log2": 12, "lanes": 2},
+             "c12_serial": {"chunk_log2": 12, "serial": 1}}   # serial: bench.py's standalone per-kernel window
 
 
 @pytest.mark.parametrize("sched", sorted(SCHEDULES))

@@ -47,6 +47,15 @@ def test_whitted_profile_counts_are_consistent(hip, fused):
     assert extend["units"] == shade["counts"][4] == shade["counts"][5]
     for v in prof.values():
         assert v["ms"] > 0 and v["bytes"] > 0
+    # round 4 fields: f[6] = level-0 samples of fused launches (they read no queue entry), f[7] =
+    # shadow pushes that carry a SkyBox direction (C2: every one), shadow f[2] = those that got
+    # through (the sky lookup reads the direction); the byte formulas of pbr_kernels.hip
+    f = shade["counts"]
+    assert f[6] == (n if fused == "1" else 0)
+    assert f[7] == f[1] and shadow["counts"][2] == shadow["counts"][1]
+    assert shade["bytes"] == 72 * f[0] - 48 * f[6] + 4 * f[5] + 52 * f[1] + 52 * f[4] + 16 * f[7]
+    g2 = shadow["counts"]
+    assert shadow["bytes"] == 52 * g2[0] + 32 * g2[1] + 16 * g2[2]
 
 
 @pytest.mark.gpu
