@@ -53,9 +53,13 @@ def main():
     if a.ref_file and os.path.exists(a.ref_file):
         ref = np.load(a.ref_file)
     for v in a.variants:
-        env = dict(kv.split("=") for kv in v.split(",") if kv)
-        saved = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
+        # a variant is a schedule (pbr_hip_set_schedule; the library reads no environment variables):
+        # comma-separated kernels=mega, chunk_log2=N, lanes=N, fuse=on|off, serial=1
+        kw = dict(kv.split("=") for kv in v.split(",") if kv)
+        r.set_schedule(kernels=capi.KERNELS_MEGAKERNEL if kw.get("kernels") == "mega" else capi.KERNELS_AUTO,
+                       chunk_log2=int(kw.get("chunk_log2", 0)), lanes=int(kw.get("lanes", 0)),
+                       fuse_camera={"on": capi.FUSE_ON, "off": capi.FUSE_OFF}.get(kw.get("fuse"), capi.FUSE_AUTO),
+                       serial=kw.get("serial") == "1")
         r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
         torch.cuda.synchronize(dev)
         ms = []
@@ -84,11 +88,7 @@ def main():
         tag = f" shard {a.shard} tile {a.tile} ({npx} px)" if a.shard else ""
         print(f"{a.config}{tag} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  "
               f"{npx * spp / m / 1e3:8.1f} Msamples/s  {same}{kern}", flush=True)
-        for k, old in saved.items():
-            if old is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = old
+        r.set_schedule()
 
 
 if __name__ == "__main__":
