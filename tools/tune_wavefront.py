@@ -1,9 +1,9 @@
-"""A/B the wavefront tuning switches on one GPU (results must stay bit-identical across them).
+"""Time one config under several schedules on one GPU (frames must stay bit-identical across them).
 
-    python tools/tune_wavefront.py [--config C2] [--steps 3] VAR=VAL[,VAR=VAL] ...
+    python tools/tune_wavefront.py [--config C2] [--steps 3] [--profile] "" "fuse=off" "serial=1" ...
 
-Each positional argument is one variant: a comma-separated list of environment settings read by
-libpbr_hip at render time (PBR_SHORT_STACK, PBR_SHADE_OCC, PBR_WAVEFRONT, PBR_OCC).
+Each positional argument is one schedule (pbr_hip_set_schedule): a comma-separated list of
+kernels=mega, chunk_log2=N, lanes=N, fuse=on|off, serial=1; "" is the default schedule.
 """
 import argparse
 import os
