@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PBR_HIP_ABI_VERSION 4
+#define PBR_HIP_ABI_VERSION 5
 
 /* ---- status codes ---- */
 enum {
@@ -74,7 +74,12 @@ enum pbr_light_type {
     PBR_LIGHT_SKYBOX = 2,       /* Light/SkyBoxLight.cpp */
     PBR_LIGHT_INFINITE_AREA = 3 /* Light/InfiniteAreaLight.cpp: light_to_world, Le = the `power`
                                  * scale, n_samples, env_* = the image as stbi_loadf returned it
-                                 * (NULL → a 1x1 map of Le); worldRadius from the scene bounds */
+                                 * (NULL → a 1x1 map of Le); worldRadius from the scene bounds.
+                                 * A caller holding only a built light's map — Lmap's level 0
+                                 * (InfiniteAreaLight.h:33: powers of two, L already applied) —
+                                 * passes those texels with Le = (1, 1, 1): 1·x is x, a power-of-two
+                                 * image is not resampled (MIPMap.h:96), so the upload rebuilds the
+                                 * same pyramid, Distribution2D and Power() */
 };
 enum pbr_integrator_type {
     PBR_INTEGRATOR_WHITTED = 0, /* Integrator/WhittedIntegrator.cpp:11-65 */
@@ -135,6 +140,10 @@ typedef struct pbr_texture_desc {
     int trilinear;              /* doTrilinear (no effect, see above) */
     float max_aniso;            /* maxAniso (no effect, see above) */
     float su, sv, du, dv;       /* UVMapping2D(su, sv, du, dv): st = (su·u + du, sv·v + dv) */
+    int level0;                 /* 1: `data` is already the MIPMap's level 0 — what a built ImageTexture
+                                 * holds (ImageTexture.h:88, MIPMap.h:150-153): width and height powers
+                                 * of two, convertIn applied, `components` = 3 (RGB) or 1 (float
+                                 * textures); used as is (scale and gamma ignored) */
 } pbr_texture_desc;
 
 /* Material parameter slots that may hold an image texture instead of the constant below
@@ -227,6 +236,12 @@ typedef struct pbr_camera_desc {
     float lens_radius;          /* the reference fixes 0 */
     float focal_distance;
     int medium;                 /* camera medium (dropped by CameraToWorld, F12) */
+    /* 1: raster_to_camera is the camera's own ProjectiveCamera::RasterToCamera (Camera.h:36-53:
+     * Inverse(CameraToScreen) · RasterToScreen of its screen window and fov), used instead of
+     * CreatePerspectiveCamera's (fov above, the raster's aspect-ratio screen window): a reference
+     * PerspectiveCamera built with any fov or screen window (Perspective.cpp:6-9) hands over exactly */
+    int use_raster_to_camera;
+    pbr_transform raster_to_camera;
 } pbr_camera_desc;
 
 typedef struct pbr_tile {

@@ -15,6 +15,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -40,6 +41,8 @@
 #include "Sampler\Halton.h"
 #include "Shape\Triangle.h"
 #include "Texture\ConstantTexture.h"
+#include "Texture\ImageTexture.h"
+#include "Texture\MIPMap.h"
 #undef protected
 #undef private
 
@@ -67,54 +70,96 @@ pbr_transform identity() {
     for (int i = 0; i < 4; ++i) t.m[5 * i] = t.m_inv[5 * i] = 1.f;
     return t;
 }
-// ConstantTexture values (Texture/ConstantTexture.h); the device path has image textures, but
-// an ImageTexture keeps only its resampled MIPMap, not the image it was loaded from, so a
-// reference scene with one cannot be handed over losslessly and is refused.
-Spectrum constS(const std::shared_ptr<Texture<Spectrum>>& t, const char* what) {
-    auto* c = dynamic_cast<const ConstantTexture<Spectrum>*>(t.get());
-    need(c != nullptr, what);
-    return c->value;
+// A material parameter: a ConstantTexture's value (Texture/ConstantTexture.h), or an ImageTexture
+// (Texture/ImageTexture.h:43-91) handed over as what the built texture holds — its MIPMap's level 0
+// (MIPMap.h:150-153: the image after convertIn and the power-of-two resample) and its UVMapping2D
+// (Texture.h:16-27) — with pbr_texture_desc::level0.  The reference's ray differentials are zero
+// (F5), so level 0 is all its lookups ever read (pbr_hip.h, pbr_texture_desc).
+template <class Tm, class Tr>
+int image_texture(FlatScene* F, const ImageTexture<Tm, Tr>* it) {
+    auto found = F->textureOf.find(it);
+    if (found != F->textureOf.end()) return found->second;
+    auto* uv = dynamic_cast<const UVMapping2D*>(it->mapping.get());
+    need(uv != nullptr, "an ImageTexture's mapping must be a UVMapping2D");
+    const MIPMap<Tm>& mm = *it->mipmap;
+    constexpr bool isFloat = std::is_same<Tm, float>::value;
+    const int W = mm.Width(), H = mm.Height(), nc = isFloat ? 1 : 3;
+    std::vector<float> t0((size_t)W * H * nc);
+    for (int t = 0; t < H; ++t)
+        for (int s = 0; s < W; ++s) {
+            const Tm& v = (*mm.pyramid[0])(s, t);
+            float* o = &t0[((size_t)t * W + s) * nc];
+            if constexpr (isFloat) o[0] = v;
+            else { o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; }
+        }
+    pbr_texture_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.is_float = isFloat ? 1 : 0;
+    d.width = W;
+    d.height = H;
+    d.components = nc;
+    d.level0 = 1;
+    d.scale = 1.f;
+    d.wrap = mm.wrapMode == ImageWrap::Repeat ? PBR_WRAP_REPEAT : (mm.wrapMode == ImageWrap::Black ? PBR_WRAP_BLACK : PBR_WRAP_CLAMP);
+    d.trilinear = mm.doTrilinear;
+    d.max_aniso = mm.maxAnisotropy;
+    d.su = uv->su; d.sv = uv->sv; d.du = uv->du; d.dv = uv->dv;
+    F->texels.push_back(std::move(t0));
+    d.data = F->texels.back().data();   // a moved vector keeps its buffer: stable as texels grows
+    F->textures.push_back(d);
+    const int k = (int)F->textures.size() - 1;
+    F->textureOf[it] = k;
+    return k;
 }
-float constF(const std::shared_ptr<Texture<float>>& t, const char* what) {
-    auto* c = dynamic_cast<const ConstantTexture<float>*>(t.get());
-    need(c != nullptr, what);
-    return c->value;
+// slot: pbr_texture_slot, or -1 where the device takes constants only
+void slotS(FlatScene* F, pbr_material_desc* d, int slot, const std::shared_ptr<Texture<Spectrum>>& t, float* out, const char* what) {
+    if (auto* c = dynamic_cast<const ConstantTexture<Spectrum>*>(t.get())) { put3(out, c->value); return; }
+    auto* it = dynamic_cast<const ImageTexture<RGBSpectrum, Spectrum>*>(t.get());
+    need(it != nullptr && slot >= 0, what);
+    d->tex[slot] = image_texture(F, it) + 1;
+}
+float slotF(FlatScene* F, pbr_material_desc* d, int slot, const std::shared_ptr<Texture<float>>& t, const char* what) {
+    if (auto* c = dynamic_cast<const ConstantTexture<float>*>(t.get())) return c->value;
+    auto* it = dynamic_cast<const ImageTexture<float, float>*>(t.get());
+    need(it != nullptr && slot >= 0, what);
+    d->tex[slot] = image_texture(F, it) + 1;
+    return 0.f;
 }
 
 // Material/*.h → pbr_material_desc (the fields pbr_hip.h documents per type).  Bump maps are not
 // read: the reference's ComputeScatteringFunctions never applies them.
-pbr_material_desc material_desc(const Material* m) {
+pbr_material_desc material_desc(FlatScene* F, const Material* m) {
     pbr_material_desc d;
     std::memset(&d, 0, sizeof(d));
     if (auto* x = dynamic_cast<const MatteMaterial*>(m)) {
         d.type = PBR_MAT_MATTE;
-        put3(d.Kd, constS(x->Kd, "MatteMaterial Kd must be a ConstantTexture"));
-        d.sigma = constF(x->sigma, "MatteMaterial sigma must be a ConstantTexture");
+        slotS(F, &d, PBR_TEX_KD, x->Kd, d.Kd, "MatteMaterial Kd must be a Constant or ImageTexture");
+        d.sigma = slotF(F, &d, PBR_TEX_SIGMA, x->sigma, "MatteMaterial sigma must be a Constant or ImageTexture");
     } else if (auto* x = dynamic_cast<const MirrorMaterial*>(m)) {
         d.type = PBR_MAT_MIRROR;
-        put3(d.Kr, constS(x->Kr, "MirrorMaterial Kr must be a ConstantTexture"));
+        slotS(F, &d, PBR_TEX_KR, x->Kr, d.Kr, "MirrorMaterial Kr must be a Constant or ImageTexture");
     } else if (auto* x = dynamic_cast<const GlassMaterial*>(m)) {
         d.type = PBR_MAT_GLASS;
-        put3(d.Kr, constS(x->Kr, "GlassMaterial Kr must be a ConstantTexture"));
-        put3(d.Kt, constS(x->Kt, "GlassMaterial Kt must be a ConstantTexture"));
-        d.uroughness = constF(x->uRoughness, "GlassMaterial uRoughness must be a ConstantTexture");
-        d.vroughness = constF(x->vRoughness, "GlassMaterial vRoughness must be a ConstantTexture");
-        d.eta = constF(x->index, "GlassMaterial index must be a ConstantTexture");
+        slotS(F, &d, PBR_TEX_KR, x->Kr, d.Kr, "GlassMaterial Kr must be a Constant or ImageTexture");
+        slotS(F, &d, PBR_TEX_KT, x->Kt, d.Kt, "GlassMaterial Kt must be a Constant or ImageTexture");
+        d.uroughness = slotF(F, &d, -1, x->uRoughness, "GlassMaterial uRoughness must be a ConstantTexture");
+        d.vroughness = slotF(F, &d, -1, x->vRoughness, "GlassMaterial vRoughness must be a ConstantTexture");
+        d.eta = slotF(F, &d, -1, x->index, "GlassMaterial index must be a ConstantTexture");
         d.remap_roughness = x->remapRoughness;
     } else if (auto* x = dynamic_cast<const MetalMaterial*>(m)) {
         d.type = PBR_MAT_METAL;
-        put3(d.metal_eta, constS(x->eta, "MetalMaterial eta must be a ConstantTexture"));
-        put3(d.metal_k, constS(x->k, "MetalMaterial k must be a ConstantTexture"));
-        d.roughness = constF(x->roughness, "MetalMaterial roughness must be a ConstantTexture");
+        slotS(F, &d, -1, x->eta, d.metal_eta, "MetalMaterial eta must be a ConstantTexture");
+        slotS(F, &d, -1, x->k, d.metal_k, "MetalMaterial k must be a ConstantTexture");
+        d.roughness = slotF(F, &d, -1, x->roughness, "MetalMaterial roughness must be a ConstantTexture");
         d.has_uv_roughness = x->uRoughness != nullptr;   // MetalMaterial.cpp: u/v textures when present
-        if (x->uRoughness) d.uroughness = constF(x->uRoughness, "MetalMaterial uRoughness must be a ConstantTexture");
-        if (x->vRoughness) d.vroughness = constF(x->vRoughness, "MetalMaterial vRoughness must be a ConstantTexture");
+        if (x->uRoughness) d.uroughness = slotF(F, &d, -1, x->uRoughness, "MetalMaterial uRoughness must be a ConstantTexture");
+        if (x->vRoughness) d.vroughness = slotF(F, &d, -1, x->vRoughness, "MetalMaterial vRoughness must be a ConstantTexture");
         d.remap_roughness = x->remapRoughness;
     } else if (auto* x = dynamic_cast<const PlasticMaterial*>(m)) {
         d.type = PBR_MAT_PLASTIC;
-        put3(d.Kd, constS(x->Kd, "PlasticMaterial Kd must be a ConstantTexture"));
-        put3(d.Ks, constS(x->Ks, "PlasticMaterial Ks must be a ConstantTexture"));
-        d.roughness = constF(x->roughness, "PlasticMaterial roughness must be a ConstantTexture");
+        slotS(F, &d, PBR_TEX_KD, x->Kd, d.Kd, "PlasticMaterial Kd must be a Constant or ImageTexture");
+        slotS(F, &d, PBR_TEX_KS, x->Ks, d.Ks, "PlasticMaterial Ks must be a Constant or ImageTexture");
+        d.roughness = slotF(F, &d, PBR_TEX_ROUGHNESS, x->roughness, "PlasticMaterial roughness must be a Constant or ImageTexture");
         d.remap_roughness = x->remapRoughness;
     } else {
         need(false, "material type not on the GPU path");
@@ -167,7 +212,7 @@ std::shared_ptr<FlatScene> SceneFlattener::Flatten(const Scene& scene) {
         const Material* m = gp->material.get();
         if (!m || matIndex.count(m)) continue;
         matIndex[m] = (int)F->materials.size();
-        F->materials.push_back(material_desc(m));
+        F->materials.push_back(material_desc(F.get(), m));
     }
     std::unordered_map<const Light*, int> lightIndex;
     for (size_t i = 0; i < scene.lights.size(); ++i) lightIndex[scene.lights[i].get()] = (int)i;
@@ -287,9 +332,31 @@ std::shared_ptr<FlatScene> SceneFlattener::Flatten(const Scene& scene) {
             L.medium_inside = L.medium_outside = -1;
         } else if (dynamic_cast<const DiffuseAreaLight*>(l)) {
             need(boundArea[li], "a DiffuseAreaLight whose shape is not a scene triangle");
+        } else if (auto* il = dynamic_cast<const InfiniteAreaLight*>(l)) {
+            // InfiniteAreaLight keeps its map as the MIPMap Lmap (InfiniteAreaLight.h:33): level 0 is
+            // the image times L after the power-of-two resample.  It goes over with Le = 1 (pbr_hip.h):
+            // the upload rebuilds the same pyramid, Distribution2D and Power() from it.
+            const MIPMap<RGBSpectrum>& mm = *il->Lmap;
+            const int W = mm.Width(), H = mm.Height();
+            std::vector<float> t0((size_t)W * H * 3);
+            for (int t = 0; t < H; ++t)
+                for (int s = 0; s < W; ++s) {
+                    const RGBSpectrum& v = (*mm.pyramid[0])(s, t);
+                    float* o = &t0[((size_t)t * W + s) * 3];
+                    o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+                }
+            F->texels.push_back(std::move(t0));
+            std::memset(&L, 0, sizeof(L));
+            L.type = PBR_LIGHT_INFINITE_AREA;
+            put_transform(il->LightToWorld, &L.light_to_world);
+            L.Le[0] = L.Le[1] = L.Le[2] = 1.f;
+            L.n_samples = il->nSamples;
+            L.env_width = W;
+            L.env_height = H;
+            L.env_components = 3;
+            L.env_data = F->texels.back().data();
+            L.medium_inside = L.medium_outside = -1;
         } else {
-            // InfiniteAreaLight keeps only its resampled MIPMap (the image it was built from is
-            // gone), and the descriptor takes the image: not handed over
             need(false, "light type not on the GPU path of the binding");
         }
     }
@@ -322,6 +389,8 @@ std::shared_ptr<FlatScene> SceneFlattener::Flatten(const Scene& scene) {
     d.split_method = (int)bvh->splitMethod;
     d.bvh_nodes = F->nodes.empty() ? nullptr : F->nodes.data();
     d.n_bvh_nodes = total;
+    d.n_textures = (int)F->textures.size();
+    d.textures = F->textures.empty() ? nullptr : F->textures.data();
     return F;
 }
 
@@ -353,14 +422,23 @@ void HipSamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
         check(pbr_hip_upload_scene(ctx_, &flat_->desc), "upload_scene");
         uploaded_ = &scene;
     }
-    // the camera: CreatePerspectiveCamera's (Perspective.cpp:84-104), fov 90 and the screen window of
-    // the raster's aspect ratio; its CameraToWorld and lens go over as they are
+    // the camera: its CameraToWorld, lens and its own RasterToCamera (ProjectiveCamera, Camera.h:36-53)
+    // — whatever fov and screen window it was constructed with (Perspective.cpp:6-9) — go over as they
+    // are (pbr_camera_desc::use_raster_to_camera)
     auto* pc = dynamic_cast<const PerspectiveCamera*>(camera.get());
     need(pc != nullptr, "the camera must be a PerspectiveCamera");
     auto* halton = dynamic_cast<const HaltonSampler*>(sampler_.get());
     need(halton != nullptr, "the sampler must be a HaltonSampler");
     const int W = bounds_.pMax.x, H = bounds_.pMax.y;
     need(bounds_.pMin.x == 0 && bounds_.pMin.y == 0 && W > 0 && H > 0, "pixel bounds must start at (0, 0)");
+    // the device derives the Halton base scales from the raster (Halton.cpp:39-51): the sampler's
+    // sampleBounds must be these pixel bounds
+    for (int i = 0; i < 2; ++i) {
+        const int base = i == 0 ? 2 : 3, res = i == 0 ? W : H;
+        int scale = 1;
+        while (scale < std::min(res, 128)) scale *= base;
+        need(halton->baseScales[i] == scale, "the HaltonSampler's sample bounds must be the integrator's pixel bounds");
+    }
     pbr_render_desc rd;
     std::memset(&rd, 0, sizeof(rd));
     rd.integrator = integrator_;
@@ -374,17 +452,25 @@ void HipSamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     rd.camera.height = H;
     put_transform(pc->CameraToWorld, &rd.camera.camera_to_world);
     rd.camera.fov = 90.f;
+    rd.camera.use_raster_to_camera = 1;
+    put_transform(pc->RasterToCamera, &rd.camera.raster_to_camera);
     rd.camera.lens_radius = pc->lensRadius;
     rd.camera.focal_distance = pc->focalDistance;
     rd.camera.medium = SceneFlattener::MediumIndex(*flat_, pc->medium);
     std::vector<uint8_t> rgba((size_t)W * H * 4);
-    check(pbr_hip_render(ctx_, &rd, nullptr, rgba.data(), nullptr), "render");
+    std::vector<float> rgb((size_t)W * H * 3);
+    check(pbr_hip_render(ctx_, &rd, rgb.data(), rgba.data(), nullptr), "render");
     // Integrator.cpp:327-344: pixel (x, y) → set_uc(x, height - 1 - y); the device produced the same
-    // bytes (ToXYZ, XYZToRGB, GammaCorrect, +0.5, clamp) with alpha 255
+    // bytes (ToXYZ, XYZToRGB, GammaCorrect, +0.5, clamp) with alpha 255.  The FrameBuffer's float
+    // buffer, which the reference allocates but never writes, gets colObj / spp (linear
+    // RGB, alpha 1) at the same place through its own set_fc.
     if (fb_) {
         for (int y = 0; y < H; ++y)
-            for (int x = 0; x < W; ++x)
+            for (int x = 0; x < W; ++x) {
                 for (int c = 0; c < 4; ++c) fb_->set_uc(x, H - y - 1, c, rgba[((size_t)y * W + x) * 4 + c]);
+                for (int c = 0; c < 3; ++c) fb_->set_fc(x, H - y - 1, c, rgb[((size_t)y * W + x) * 3 + c]);
+                fb_->set_fc(x, H - y - 1, 3, 1.f);
+            }
     }
     timeConsume = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }

@@ -28,6 +28,7 @@
 // implementation file opens them with `#define private public` instead.
 #pragma once
 
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -52,13 +53,18 @@ struct FlatScene {
     std::vector<std::vector<float>> uvs;           // per mesh: TriangleMesh::uv, if any
     std::vector<unsigned char> nodes;              // the BVHAccel's LinearBVHNode array (32 B each)
     std::vector<const void*> mediumOf;             // media in index order (PBR::Medium*)
+    std::vector<pbr_texture_desc> textures;        // ImageTextures (their MIPMap level 0), in index order
+    std::map<const void*, int> textureOf;          // ImageTexture object → its index
+    std::vector<std::vector<float>> texels;        // level-0 texels of the textures and InfiniteAreaLights
 };
 
 class SceneFlattener {
   public:
     // Throws std::invalid_argument for what the device path does not hold: an aggregate that is not
-    // a BVHAccel, non-triangle shapes (the reference's Sphere is a stub), image textures, bump maps,
-    // per-vertex shading normals, InfiniteAreaLight, media other than HomogeneousMedium.
+    // a BVHAccel, non-triangle shapes (the reference's Sphere is a stub), image textures on metal or
+    // on glass roughness / index, texture mappings other than UVMapping2D, bump maps, per-vertex
+    // shading normals, media other than HomogeneousMedium.  ImageTextures and InfiniteAreaLights go
+    // over as the MIPMap level 0 they hold (pbr_texture_desc::level0, pbr_hip.h).
     static std::shared_ptr<FlatScene> Flatten(const PBR::Scene& scene);
     // index of a medium of the flattened scene (-1 for nullptr)
     static int MediumIndex(const FlatScene& f, const void* medium);

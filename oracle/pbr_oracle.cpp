@@ -1461,6 +1461,9 @@ struct Camera {
                                Translate(V3(-sMinX, -sMaxY, 0));
         Xform rasterToScreen = InverseX(screenToRaster);
         rasterToCamera = InverseX(cameraToScreen) * rasterToScreen;
+        // pbr_camera_desc::use_raster_to_camera: the camera's own RasterToCamera, any fov / screen window
+        if (d.use_raster_to_camera)
+            rasterToCamera = Xform(M4::rows(d.raster_to_camera.m), M4::rows(d.raster_to_camera.m_inv));
         lensRadius = d.lens_radius;
         focalDistance = d.focal_distance;
         medium = d.medium;
@@ -1595,6 +1598,22 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
         t.su = td.su; t.sv = td.sv; t.du = td.du; t.dv = td.dv;
         int w = 1, h = 1;
         std::vector<Spec> texels;
+        const ImageWrapO wrap0 = (ImageWrapO)td.wrap;
+        if (td.level0) {   // pbr_texture_desc::level0: a built texture's MIPMap level 0, used as is
+            if (!td.data || td.width <= 0 || td.height <= 0 || (td.width & (td.width - 1)) || (td.height & (td.height - 1)) ||
+                td.components != (t.isFloat ? 1 : 3))
+                throw std::invalid_argument("bad level-0 texture");
+            const size_t n = (size_t)td.width * td.height;
+            if (t.isFloat) {
+                t.mf = std::make_shared<MIPMapT<float>>(td.width, td.height, td.data, wrap0);
+            } else {
+                std::vector<Spec> l0(n);
+                for (size_t j = 0; j < n; ++j) l0[j] = Spec(td.data[3 * j], td.data[3 * j + 1], td.data[3 * j + 2]);
+                t.ms = std::make_shared<MIPMapT<Spec>>(td.width, td.height, l0.data(), wrap0);
+            }
+            s->textures.push_back(t);
+            continue;
+        }
         if (td.data && td.width > 0 && td.height > 0) {
             w = td.width; h = td.height;
             for (int j = 0; j < w * h; ++j)

@@ -196,6 +196,7 @@ std::unique_ptr<RefScene> build(const pbr_scene_desc* d) {
     // image goes through a file that the texture's own loadImage (stbi_loadf, flip-on-load set,
     // ImageTexture.cpp:13-37) reads back as exactly the descriptor's floats
     auto image = [&](const pbr_texture_desc& td) {
+        if (td.level0) throw std::runtime_error("a level-0 texture: build the reference ImageTexture itself");
         std::string path;
         if (td.data && td.width > 0 && td.height > 0) {
             path = write_env(td.data, td.width, td.height, td.components, true);
@@ -326,6 +327,7 @@ struct RefCamera {
 // distance, and fov 90.
 std::shared_ptr<Camera> make_camera(const pbr_camera_desc& c) {
     if (c.fov != 90.f || c.lens_radius < 0.f) throw std::runtime_error("the reference camera is fov 90");
+    if (c.use_raster_to_camera) throw std::runtime_error("a given RasterToCamera: build the reference camera itself");
     Transform c2w;
     if (c.use_look_at)
         c2w = Inverse(LookAt(Point3f(c.eye[0], c.eye[1], c.eye[2]), Point3f(c.look[0], c.look[1], c.look[2]),

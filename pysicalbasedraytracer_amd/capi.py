@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 PBR_OK = 0
 PBR_E_INVALID = -1
@@ -91,6 +91,7 @@ class TextureDesc(C.Structure):
         ("sv", C.c_float),
         ("du", C.c_float),
         ("dv", C.c_float),
+        ("level0", C.c_int),
     ]
 
 
@@ -152,6 +153,8 @@ class CameraDesc(C.Structure):
         ("lens_radius", C.c_float),
         ("focal_distance", C.c_float),
         ("medium", C.c_int),
+        ("use_raster_to_camera", C.c_int),
+        ("raster_to_camera", Transform),
     ]
 
 

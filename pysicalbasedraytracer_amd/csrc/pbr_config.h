@@ -15,7 +15,17 @@
     defined(PBR_REFILL_OCC) || defined(PBR_REFILL_OCC_ANY) || defined(PBR_REFILL_OCC_TR) ||                          \
     defined(PBR_CAMERA_SHORT) || defined(PBR_WF_SHADE_OCC) || defined(PBR_WF_SHADE_OCC_MM) ||                        \
     defined(PBR_WF_FUSED_OCC) || defined(PBR_WFP_OCC) || defined(PBR_WFV_OCC) || defined(PBR_LANES_DEFAULT) ||       \
-    defined(PBR_INLINE_TRANS)
+    defined(PBR_INLINE_TRANS) || defined(PBR_DIAG_SHADE) || defined(PBR_STACK_DIAG)
 #error "tuning switches are development builds only: add -DPBR_DEV_KNOBS=1"
 #endif
+#endif
+// PBR_DIAG_SHADE (diagnostic builds only, results NOT the reference's): bits that stub parts of the
+// Path shade to price them (tools/r5_shade_probe.py).
+#ifndef PBR_DIAG_SHADE
+#define PBR_DIAG_SHADE 0
+#endif
+// PBR_STACK_DIAG (diagnostic builds): the lane-refill traversals count the rays whose stack went
+// deeper than 6 / 10 / 16 / 24 entries into profile fields 2-5 of their family.
+#ifndef PBR_STACK_DIAG
+#define PBR_STACK_DIAG 0
 #endif

@@ -917,6 +917,10 @@ PBR_HD f3 cosine_hemisphere(float u0, float u1) {
     float z = sqrtf(mx((float)0, 1 - dx * dx - dy * dy));
     return mk(dx, dy, z);
 }
+// BxDF::Sample_f.  The value it returns is only used for specular lobes: BSDF::Sample_f replaces a
+// non-specular lobe's f by the sum of f over the matching lobes (Reflection.cpp:150-160), so for
+// the diffuse and microfacet kinds the lobe's own f(wo, wi) — which the reference evaluates and
+// then drops — is not computed here (black is returned; wi and pdf are the reference's).
 template <int K = kAllLobes>
 PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* pdf, int* st) {
     switch (l.kind) {
@@ -924,7 +928,7 @@ PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* 
         *wi = cosine_hemisphere(u0, u1);
         if (wo.z < 0) wi->z *= -1;
         *pdf = lobe_pdf<K>(l, wo, *wi);
-        return lobe_f<K>(l, wo, *wi);
+        return sp(0.f);   // (f: dropped by bsdf_sample)
     } break;
     case L_SPEC_R: if constexpr (PBR_HAS(K, L_SPEC_R)) {
         *wi = mk(-wo.x, -wo.y, wo.z);
@@ -964,7 +968,7 @@ PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* 
         *wi = reflect_(wo, wh);
         if (!same_hemi(wo, *wi)) return sp(0.f);
         *pdf = tr_pdf(l, wo, wh) / (4 * dot(wo, wh));
-        return lobe_f<K>(l, wo, *wi);
+        return sp(0.f);   // (f: dropped by bsdf_sample)
     } break;
     case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
         if (wo.z == 0) return sp(0.f);
@@ -973,7 +977,7 @@ PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* 
         float eta = cos_t(wo) > 0 ? (l.etaA / l.etaB) : (l.etaB / l.etaA);
         if (!refract_(wo, wh, eta, wi)) return sp(0.f);
         *pdf = lobe_pdf<K>(l, wo, *wi);
-        return lobe_f<K>(l, wo, *wi);
+        return sp(0.f);   // (f: dropped by bsdf_sample)
     } break;
     default: break;
     }
@@ -1039,6 +1043,7 @@ PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float
     *sampledType = st;
     if (*pdf == 0) { *sampledType = 0; return sp(0.f); }
     *wiW = b.to_world(wi);
+    // (a non-specular lobe's f is the sum below: lobe_sample does not evaluate it)
     if (!(bx.type & BSDF_SPECULAR) && m > 1)
         for (int i = 0; i < b.mt->nLobes; ++i)
             if (i != chosen && matches(b.mt->lobes[i], type)) *pdf += lobe_pdf<K>(b.mt->lobes[i], wo, wi);

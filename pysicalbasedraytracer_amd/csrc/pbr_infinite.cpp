@@ -210,6 +210,23 @@ void build_image_texture(const pbr_texture_desc& td, TexDev* out, std::vector<fl
     // convertIn per texel (ImageTexture.h:69-78) → MIPMap level 0 (MIPMap.h:86-150)
     int w = 1, h = 1;
     std::vector<RGB> rgb;
+    if (td.wrap < PBR_WRAP_REPEAT || td.wrap > PBR_WRAP_CLAMP) throw std::invalid_argument("bad texture wrap mode");
+    if (td.level0) {   // a built ImageTexture's MIPMap level 0 (MIPMap.h:150-153): used as is
+        const int nc = td.is_float ? 1 : 3;
+        if (!td.data || td.width <= 0 || td.height <= 0 || !is_pow2(td.width) || !is_pow2(td.height))
+            throw std::invalid_argument("a level-0 texture needs data with power-of-two width and height");
+        if (td.components != nc) throw std::invalid_argument("a level-0 texture has 3 (RGB) or 1 (float) components");
+        std::memset(out, 0, sizeof(*out));
+        out->offset = (int)(texels->size() / 4);
+        out->w = td.width;
+        out->h = td.height;
+        out->wrap = td.wrap;
+        out->isFloat = td.is_float ? 1 : 0;
+        out->su = td.su; out->sv = td.sv; out->du = td.du; out->dv = td.dv;
+        for (size_t i = 0; i < (size_t)td.width * td.height; ++i)
+            for (int k = 0; k < 4; ++k) texels->push_back(k < nc ? td.data[i * nc + k] : 0.f);
+        return;
+    }
     if (td.data && td.width > 0 && td.height > 0) {
         if (td.components < 3) throw std::invalid_argument("ImageTexture image needs >= 3 components");
         w = td.width;
@@ -220,7 +237,6 @@ void build_image_texture(const pbr_texture_desc& td, TexDev* out, std::vector<fl
     } else {
         rgb.assign(1, RGB{{0.5f, 0.5f, 0.5f}});
     }
-    if (td.wrap < PBR_WRAP_REPEAT || td.wrap > PBR_WRAP_CLAMP) throw std::invalid_argument("bad texture wrap mode");
     const int nc = td.is_float ? 1 : 3;
     std::vector<float> img((size_t)w * h * nc);
     for (size_t i = 0; i < rgb.size(); ++i) {

@@ -167,11 +167,17 @@ __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32
 // arrayStartDim == arrayEndDim == 5, so only a Get2D that would straddle dimension 5 is moved.
 template <bool LDS = false, int KIND = -1>
 __device__ __forceinline__ float get1d(const DeviceSampler& s, SState& st) {
+    if constexpr (PBR_DIAG_SHADE & 8) {   // diagnostic: a hash instead of the sampler
+        uint32_t h = st.index * 0x9E3779B1u ^ (uint32_t)(st.dim++) * 0x85EBCA77u ^ (uint32_t)st.sid * 0xC2B2AE3Du;
+        h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
+        return (float)(h >> 8) * (1.f / 16777216.f);
+    }
     return sample_dimension<LDS, KIND>(s, st.index, st.sid, st.dim++, st.px, st.py);
 }
 template <bool LDS = false, int KIND = -1>
 __device__ __forceinline__ void get2d(const DeviceSampler& s, SState& st, float* a, float* b) {
     if (st.dim == 4) st.dim = 5;
+    if constexpr (PBR_DIAG_SHADE & 8) { *a = get1d<LDS, KIND>(s, st); *b = get1d<LDS, KIND>(s, st); return; }
     *a = sample_dimension<LDS, KIND>(s, st.index, st.sid, st.dim, st.px, st.py);
     *b = sample_dimension<LDS, KIND>(s, st.index, st.sid, st.dim + 1, st.px, st.py);
     st.dim += 2;
@@ -1992,7 +1998,10 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     }
     unsigned long long hs[4] = {0, 0, 0, 0};
     if (d->collect_stats) HIP_TRY(hipMemcpyAsync(hs, ctx->dStats.p, sizeof(hs), hipMemcpyDeviceToHost, s));
-    if (guardFrame) HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    // every frame copies the guard word out (4 B, asynchronous): a bound or a full traversal stack
+    // fails this call (synchronous frames) or the next one / pbr_hip_sync (asynchronous ones), and a
+    // bit is never left behind to fail an unrelated later frame
+    HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, s));
     if (!d->outputs_on_device || d->collect_stats || stats || d->sampler == PBR_SAMPLER_TABLE) {
         HIP_TRY(hipStreamSynchronize(s));
         if (int rc = check_guard(ctx)) return rc;

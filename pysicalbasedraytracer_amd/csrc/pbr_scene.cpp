@@ -733,6 +733,8 @@ void build_camera(const pbr_camera_desc* c, DeviceCamera* out) {
     Xf screenToRaster = compose(compose(scale((float)c->width, (float)c->height, 1), scale(1 / (x1 - x0), 1 / (y0 - y1), 1)),
                                 translate(mk(-x0, -y1, 0)));
     Xf rasterToCamera = compose(inverse(camToScreen), inverse(screenToRaster));
+    // a camera's own RasterToCamera (any fov / screen window): used as given
+    if (c->use_raster_to_camera) rasterToCamera = Xf{from_rows(c->raster_to_camera.m), from_rows(c->raster_to_camera.m_inv)};
     std::memcpy(out->rasterToCamera, &rasterToCamera.m.a[0][0], 64);
     std::memcpy(out->cameraToWorld, &camToWorld.m.a[0][0], 64);
     out->lensRadius = c->lens_radius;

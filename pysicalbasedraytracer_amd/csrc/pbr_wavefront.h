@@ -232,6 +232,8 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
     h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
     unsigned long long laneSteps = 0, waveSteps = 0;
     (void)laneSteps; (void)waveSteps;
+    int maxSp = 0;   // PBR_STACK_DIAG: the ray's deepest stack
+    (void)maxSp;
     while (true) {
         const unsigned long long idle = __ballot(!have);
         const int nIdle = __popcll(idle);
@@ -252,6 +254,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
                     if (ok) {
                         cur = S.quadRootRef;
                         sp = 0;
+                        maxSp = 0;
                         have = true;
                     } else {
                         store(key, false, r, h);
@@ -313,6 +316,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
                 if (p3 && first < 3) push(q.ref[3], q.t[3]);
                 if (p2 && first < 2) push(q.ref[2], q.t[2]);
                 if (p1 && first < 1) push(q.ref[1], q.t[1]);
+                if constexpr (PBR_STACK_DIAG) maxSp = max(maxSp, sp);
                 cur = first == 0 ? q.ref[0] : (first == 1 ? q.ref[1] : (first == 2 ? q.ref[2] : q.ref[3]));
                 descend = true;
             }
@@ -331,6 +335,14 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             done = !more;
         }
         if (done) {
+            if constexpr (PBR_STACK_DIAG) {   // rays whose stack went past 6 / 10 / 16 / 24 entries
+                if (diag) {
+                    prof_count(diag + diagKind * kProfFields + 2, maxSp > 6);
+                    prof_count(diag + diagKind * kProfFields + 3, maxSp > 10);
+                    prof_count(diag + diagKind * kProfFields + 4, maxSp > 16);
+                    prof_count(diag + diagKind * kProfFields + 5, maxSp > 24);
+                }
+            }
             store(key, found, r, h);
             have = false;
         }

@@ -198,8 +198,12 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                             rgb Li = sample_li(S, light, isect, uL0, uL1, &wi, &lightPdf, &vis);
                             A = sp(0.f);
                             if (lightPdf > 0 && !black(Li)) {
-                                rgb f = bsdf_f<LOBES>(bsdf, wo, wi, flagsNS) * absdot(wi, isect.sn);
+                                rgb f;
+                                if constexpr (PBR_DIAG_SHADE & 1) { f = sp(0.25f); scatteringPdf = 0.5f; }
+                                else {
+                                f = bsdf_f<LOBES>(bsdf, wo, wi, flagsNS) * absdot(wi, isect.sn);
                                 scatteringPdf = bsdf_pdf<LOBES>(bsdf, wo, wi, flagsNS);
+                                }
                                 if (!black(f)) {
                                     if (delta) A = f * Li / lightPdf;
                                     else {
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                             }
                             fB = sp(0.f);
                             weightB = 1.f;
-                            if (!delta) {
+                            if (!delta && !(PBR_DIAG_SHADE & 2)) {
                                 int stype = 0;
                                 fB = bsdf_sample<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
                                 fB = fB * absdot(wi, isect.sn);
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                                 if (!black(fB) && scatteringPdf > 0) {
                                     bool probeIt = true;
                                     if (!sampledSpecular) {
-                                        float lp = pdf_li(S, light, isect, wi);
+                                        float lp = (PBR_DIAG_SHADE & 4) ? 0.5f : pdf_li(S, light, isect, wi);
                                         if (lp == 0) probeIt = false;
                                         else {
                                             float fp = 1 * scatteringPdf, gp = 1 * lp;

@@ -1077,6 +1077,9 @@ void check(pbr_hip_ctx* ctx, int rc, const char* what) {
     if (ctx) msg += ": " + std::string(pbr_hip_last_error(ctx));
     throw std::runtime_error(msg);
 }
+// The sample-table path (a GlobalSampler subclass the device cannot compute) holds the whole frame's
+// values in host and device memory: up to this many bytes.
+constexpr double kMaxSampleTableBytes = 16e9;
 void camera_desc(const PerspectiveCamera& cam, pbr_camera_desc* c) {
     std::memset(c, 0, sizeof(*c));
     c->width = cam.RasterWidth;
@@ -1086,6 +1089,22 @@ void camera_desc(const PerspectiveCamera& cam, pbr_camera_desc* c) {
     c->lens_radius = cam.lensRadius;
     c->focal_distance = cam.focalDistance;
     c->medium = -1;
+    // A screen window other than CreatePerspectiveCamera's (Perspective.cpp:84-104): the camera's own
+    // RasterToCamera, as ProjectiveCamera's constructor forms it (Camera.h:36-53), goes over instead.
+    const float frame = (float)cam.RasterWidth / (float)cam.RasterHeight;
+    const float sx = frame > 1.f ? frame : 1.f, sy = frame > 1.f ? 1.f : 1.f / frame;
+    const Bounds2f& w = cam.screenWindow;
+    if (w.pMin.x != -sx || w.pMax.x != sx || w.pMin.y != -sy || w.pMax.y != sy) {
+        using namespace pbr::xform;
+        const Xf camToScreen = perspective(cam.fov, 1e-2f, 1000.f);
+        const Xf screenToRaster = compose(compose(scale((float)cam.RasterWidth, (float)cam.RasterHeight, 1),
+                                                  scale(1 / (w.pMax.x - w.pMin.x), 1 / (w.pMin.y - w.pMax.y), 1)),
+                                          translate(pbr::mk(-w.pMin.x, -w.pMax.y, 0)));
+        const Xf r2c = compose(inverse(camToScreen), inverse(screenToRaster));
+        c->use_raster_to_camera = 1;
+        std::memcpy(c->raster_to_camera.m, &r2c.m.a[0][0], 64);
+        std::memcpy(c->raster_to_camera.m_inv, &r2c.mi.a[0][0], 64);
+    }
 }
 // The samplers the device runs: HaltonSampler (any raster: its values depend on the pixel only) and
 // SobolSampler, whose resolution must be the camera's raster (the device derives it from there).
@@ -1115,12 +1134,6 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     const int W = pixelBounds.pMax.x, H = pixelBounds.pMax.y;   // the reference reads pMax only
     if (W <= 0 || H <= 0 || W > cam->RasterWidth || H > cam->RasterHeight)
         throw std::invalid_argument("Render: pixelBounds outside the camera raster");
-    // the device derives the screen window as CreatePerspectiveCamera does
-    float frame = (float)cam->RasterWidth / (float)cam->RasterHeight;
-    float sx = frame > 1.f ? frame : 1.f, sy = frame > 1.f ? 1.f : 1.f / frame;
-    if (cam->screenWindow.pMin.x != -sx || cam->screenWindow.pMax.x != sx || cam->screenWindow.pMin.y != -sy ||
-        cam->screenWindow.pMax.y != sy)
-        throw std::invalid_argument("Render: custom screen windows are not on the GPU path");
     ensure_scene(scene);
     auto flat = FlattenScene(scene, cam->medium);   // for the camera medium's index
     pbr_render_desc rd;
@@ -1140,18 +1153,16 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
         tl.push_back({0, 0, W, H});
     }
     std::vector<float> table;
-    if (rd.sampler == PBR_SAMPLER_TABLE) {
-        // A GlobalSampler the device cannot compute: its values for every pixel and sample of the
-        // frame, taken the way Render's loop takes them (Integrator.cpp:290-300: Clone(offset),
-        // StartPixel, then sample after sample), for the dimensions the integrator can reach — 5
-        // camera dimensions, then per bounce at most 2 per light + 2 (Whitted), 8 (Path: light choice,
-        // light and BSDF samples, its own BSDF sample, roulette) or 10 (VolPath: + medium sampling).
-        // The device fails the frame if a path asks for more (kGuardSampleTable).
-        const int depth = std::max(1, MaxDepth()), nl = (int)scene.lights.size();
-        const int dims = IntegratorType() == PBR_INTEGRATOR_WHITTED ? 5 + depth * (2 * std::max(1, nl) + 2) + 2
-                         : IntegratorType() == PBR_INTEGRATOR_PATH ? 5 + (depth + 1) * 8 + 2
-                                                                   : 5 + (depth + 1) * 10 + 2;
+    // A GlobalSampler the device cannot compute: its values for every pixel and sample of the frame,
+    // taken the way Render's loop takes them (Integrator.cpp:290-300: Clone(offset), StartPixel, then
+    // sample after sample), for `dims` dimensions.
+    auto tabulate = [&](int dims) {
         const int Wr = cam->RasterWidth, Hr = cam->RasterHeight, spp = rd.spp;
+        const double bytes = (double)Wr * Hr * spp * dims * sizeof(float);
+        if (bytes > kMaxSampleTableBytes)
+            throw std::invalid_argument("Render: a " + std::to_string((int)(bytes / 1e9)) + " GB sample table for this " +
+                                        "GlobalSampler is beyond the " + std::to_string((int)(kMaxSampleTableBytes / 1e9)) +
+                                        " GB the sample-table path takes (fewer samples per pixel or a smaller frame)");
         table.assign((size_t)Wr * Hr * spp * dims, 0.f);
         for (const pbr_tile& t : tl)
             for (int y = t.y0; y < t.y1; ++y)
@@ -1167,6 +1178,21 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
                 }
         rd.sample_table = table.data();
         rd.table_dims = dims;
+    };
+    int dims = 0;
+    if (rd.sampler == PBR_SAMPLER_TABLE) {
+        // The dimensions the integrator reaches: 5 camera dimensions, then per bounce at most 2 per
+        // light + 2 (Whitted), 8 (Path: light choice, light and BSDF samples, its own BSDF sample,
+        // roulette) or 10 (VolPath: + medium sampling).  A VolPath path also draws HomogeneousMedium::
+        // Sample's 2 dimensions at each material-less boundary it crosses inside a medium, which does
+        // not count as a bounce (VolPathIntegrator.cpp:68-71): when a path asks the table for more
+        // than it holds (the device's kGuardSampleTable), the frame is tabulated again with twice the
+        // dimensions and rendered again, below.
+        const int depth = std::max(1, MaxDepth()), nl = (int)scene.lights.size();
+        dims = IntegratorType() == PBR_INTEGRATOR_WHITTED ? 5 + depth * (2 * std::max(1, nl) + 2) + 2
+               : IntegratorType() == PBR_INTEGRATOR_PATH ? 5 + (depth + 1) * 8 + 2
+                                                         : 5 + (depth + 1) * 10 + 2;
+        tabulate(dims);
     }
     rd.n_tiles = (int)tl.size();
     rd.tiles = tl.data();
@@ -1175,7 +1201,17 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     std::vector<float> rgb(npx * 3);
     std::vector<uint8_t> rgba(npx * 4);
     pbr_render_stats st;
-    check(ctx, pbr_hip_render(ctx, &rd, rgb.data(), rgba.data(), &st), "pbr_hip_render");
+    for (;;) {
+        const int rc = pbr_hip_render(ctx, &rd, rgb.data(), rgba.data(), &st);
+        if (rc == PBR_E_UNSUPPORTED && rd.sampler == PBR_SAMPLER_TABLE &&
+            std::strstr(pbr_hip_last_error(ctx), "sample table") != nullptr) {
+            dims *= 2;   // a path went past the table (medium boundaries): more dimensions, same frame
+            tabulate(dims);
+            continue;
+        }
+        check(ctx, rc, "pbr_hip_render");
+        break;
+    }
     if (m_FrameBuffer) {
         if (m_FrameBuffer->width != W || m_FrameBuffer->height != H || m_FrameBuffer->channals < 3)
             throw std::invalid_argument("Render: FrameBuffer not initialised to the pixel bounds");

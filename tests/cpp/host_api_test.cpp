@@ -103,6 +103,50 @@ void build_area(Built& b, int W, int H, bool medium) {
     b.cam = std::shared_ptr<Camera>(CreatePerspectiveCamera(W, H, Inverse(lookat), nullptr));
 }
 
+// Nested closed boxes with no material (pbrt's medium-interface idiom): the outer one bounds a thin
+// medium, the inner one a denser one, around a matte tetrahedron; matte floor, area light above.
+void build_boxes(Built& b, int W, int H) {
+    std::vector<std::shared_ptr<Primitive>> prims;
+    b.media.push_back(std::make_unique<HomogeneousMedium>(Spectrum(0.05f), Spectrum(0.3f), 0.2f));
+    b.media.push_back(std::make_unique<HomogeneousMedium>(Spectrum(0.1f), Spectrum(0.9f), -0.3f));
+    const Medium* m1 = b.media[0].get();
+    const Medium* m2 = b.media[1].get();
+    const Transform* id = keep(b, Transform());
+    auto box = [&](float h, const Medium* in, const Medium* out) {
+        const Point3f p[8] = {Point3f(-h, -h, -h), Point3f(h, -h, -h), Point3f(h, h, -h), Point3f(-h, h, -h),
+                              Point3f(-h, -h, h),  Point3f(h, -h, h),  Point3f(h, h, h),  Point3f(-h, h, h)};
+        const int idx[36] = {0, 2, 1, 0, 3, 2, 4, 5, 6, 4, 6, 7, 0, 1, 5, 0, 5, 4, 3, 6, 2, 3, 7, 6, 0, 4, 7, 0, 7, 3, 1, 2, 6, 1, 6, 5};
+        for (auto& s : CreateTriangleMesh(id, id, false, 12, idx, 8, p, nullptr, nullptr, nullptr))
+            prims.push_back(std::make_shared<GeometricPrimitive>(s, nullptr, nullptr, MediumInterface(in, out)));
+    };
+    box(0.95f, m1, nullptr);
+    box(0.6f, m2, m1);
+    auto matte = std::make_shared<MatteMaterial>(rgbTex(0.7f, 0.5f, 0.3f), fTex(0.f), nullptr);
+    const Point3f tp[4] = {Point3f(-0.3f, -0.3f, -0.2f), Point3f(0.3f, -0.3f, -0.2f), Point3f(0.f, -0.3f, 0.3f), Point3f(0.f, 0.3f, 0.f)};
+    const int ti[12] = {0, 2, 1, 0, 1, 3, 1, 2, 3, 2, 0, 3};
+    for (auto& s : CreateTriangleMesh(id, id, false, 4, ti, 4, tp, nullptr, nullptr, nullptr))
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, matte, nullptr, MediumInterface(m2, m2)));
+    auto floorMat = std::make_shared<MatteMaterial>(rgbTex(0.6f, 0.6f, 0.6f), fTex(0.f), nullptr);
+    const Point3f fp[4] = {Point3f(-5, -1, -5), Point3f(5, -1, -5), Point3f(5, -1, 5), Point3f(-5, -1, 5)};
+    const int fi[6] = {0, 2, 1, 0, 3, 2};
+    for (auto& s : CreateTriangleMesh(id, id, false, 2, fi, 4, fp, nullptr, nullptr, nullptr))
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, floorMat, nullptr, MediumInterface()));
+    const Transform* lx = keep(b, Translate(Vector3f(0.f, 2.45f, 0.f)));
+    const Transform* lxi = keep(b, Inverse(*lx));
+    const Point3f lp[4] = {Point3f(-0.6f, 0, -0.6f), Point3f(0.6f, 0, -0.6f), Point3f(0.6f, 0, 0.6f), Point3f(-0.6f, 0, 0.6f)};
+    const int li[6] = {0, 1, 2, 0, 2, 3};
+    std::vector<std::shared_ptr<Light>> lights;
+    auto lightMat = std::make_shared<MatteMaterial>(rgbTex(0, 0, 0), fTex(0.f), nullptr);
+    for (auto& s : CreateTriangleMesh(lx, lxi, true, 2, li, 4, lp, nullptr, nullptr, nullptr)) {
+        auto area = std::make_shared<DiffuseAreaLight>(*lx, MediumInterface(), Spectrum(5.f), 5, s, false);
+        lights.push_back(area);
+        prims.push_back(std::make_shared<GeometricPrimitive>(s, lightMat, area, MediumInterface()));
+    }
+    b.scene = std::make_unique<Scene>(std::make_shared<BVHAccel>(prims, 1), lights);
+    Transform lookat = LookAt(Point3f(0.f, 0.3f, 3.2f), Point3f(0.f, -0.3f, 0.f), Vector3f(0.f, 1.f, 0.f));
+    b.cam = std::shared_ptr<Camera>(CreatePerspectiveCamera(W, H, Inverse(lookat), nullptr));
+}
+
 // The reference's main.cpp light (main.cpp:377-381): InfiniteAreaLight(RotateX(-90) * RotateY(-0) *
 // RotateZ(-50), power 1, nSamples 10, texmap) — here an in-memory 60x30 sky (not a power of two,
 // so the MIPMap resamples it) added to a built scene.
@@ -515,6 +559,26 @@ void custom_samplers() {
         expect(finite && sum > 0 && std::memcmp(h1.getFCbuffer(), h2.getFCbuffer(), nb * sizeof(float)) == 0,
                itype ? "Path: a ClockRandSampler-shaped GlobalSampler renders a finite, deterministic frame"
                      : "Whitted: a ClockRandSampler-shaped GlobalSampler renders a finite, deterministic frame");
+    }
+    {   // VolPath through media bounded by material-less surfaces: each crossing inside a
+        // medium draws HomogeneousMedium::Sample's 2 dimensions without counting as a bounce
+        // (VolPathIntegrator.cpp:68-71), so a path can ask for more dimensions than the first table
+        // holds; Render tabulates again with more and the frame equals the HaltonSampler's.
+        Built b;
+        build_boxes(b, W, H);
+        auto render = [&](std::shared_ptr<Sampler> smp, FrameBuffer& fb) {
+            auto integ = std::make_shared<VolPathIntegrator>(1, b.cam, smp, bounds, 1.f, "uniform", &fb);
+            double t = 0;
+            integ->Render(*b.scene, t);
+        };
+        FrameBuffer ref, fwd;
+        for (FrameBuffer* f : {&ref, &fwd}) f->InitBuffer(W, H, 4);
+        render(std::make_shared<HaltonSampler>(spp, bounds), ref);
+        render(std::make_shared<ForwardingHalton>(spp, bounds), fwd);
+        const size_t nb = (size_t)W * H * 4;
+        expect(std::memcmp(ref.getUCbuffer(), fwd.getUCbuffer(), nb) == 0 &&
+                   std::memcmp(ref.getFCbuffer(), fwd.getFCbuffer(), nb * sizeof(float)) == 0,
+               "VolPath: a GlobalSampler subclass through nested material-less medium boxes renders = HaltonSampler, bit for bit");
     }
     // PixelSampler: the reference's streams (Sampler.cpp:67-95), refused by Render
     FilledPixelSampler ps(4, 2);

@@ -339,11 +339,14 @@ def _fields(h, st):
         v = getattr(st, name)
         if isinstance(typ, type) and issubclass(typ, (C._Pointer, C.c_void_p, C.c_char_p)) or typ is C.c_void_p:
             continue
-        if name == "n_bvh_nodes" and v == 0:
-            continue   # added after the fixtures were digested; hashed only when a tree is supplied
+        if name in ("n_bvh_nodes", "level0", "use_raster_to_camera") and v == 0:
+            continue   # added after the fixtures were digested; hashed only when set
+        if name == "raster_to_camera" and not st.use_raster_to_camera:
+            continue
         if name == "abi_version":
             # the descriptor layout the fixtures were digested with: ABI v4 added an entry point
-            # (pbr_hip_set_schedule), no descriptor field, so scene digests stay comparable
+            # (pbr_hip_set_schedule), v5 fields that are hashed only when set, so scene digests
+            # stay comparable
             v = 3
         if isinstance(v, C.Structure):
             _fields(h, v)

@@ -1,20 +1,22 @@
-"""The reference-side drop-in (integration/reference_binding, VERDICT r3 missing 1), compiled against
-the reference's own headers and exercised the way a user of the reference would use it.
+"""The reference-side drop-in (integration/reference_binding, VERDICT r3 missing 1, r4 missing 1-3),
+compiled against the reference's own headers and exercised the way a user of the reference would.
 
-oracle/ref/refbind_scenes.cpp assembles C2/C3/C5-shaped scenes from the reference's OWN classes as
-Main/main.cpp:186-413 does, then renders each twice into the reference's FrameBuffer: once with the
-reference's own SamplerIntegrator::Render (Integrator.cpp:280-356, Whitted/Path/VolPath) and once with
-pbrhip::Hip{Whitted,Path,VolPath}Integrator — the same constructor arguments — which flattens the
-reference Scene (its BVHAccel's tree included) into pbr_scene_desc and renders through the C-ABI.
+oracle/ref/refbind_scenes.cpp assembles scenes from the reference's OWN classes as
+Main/main.cpp:186-413 does — the C2/C3/C4/C5 shapes, the scene main.cpp ships (VolPath, mirror floor,
+InfiniteAreaLight, an ImageTexture plastic), and cameras of another fov / screen window — then renders
+each twice into the reference's FrameBuffer: once with the reference's own SamplerIntegrator::Render
+(Integrator.cpp:280-356, Whitted/Path/VolPath) and once with pbrhip::Hip{Whitted,Path,VolPath}Integrator
+— the same constructor arguments — which flattens the reference Scene (its BVHAccel's tree, its
+textures' and InfiniteAreaLight's MIPMap level 0, its camera's RasterToCamera) into pbr_scene_desc and
+renders through the C-ABI.  Besides the 8-bit FrameBuffers, the reference's float colObj / spp comes
+from its per-pixel body on the same objects and the drop-in's from the FrameBuffer's float buffer.
 
-Bar: the device walks the reference's own tree (its LinearBVHNode array, uploaded byte for byte);
-the FrameBuffers are identical except where a last-bit libm difference (glibc's float sinf/expf/logf
-in the reference, correctly rounded transcendentals on the device) moves a byte by one —
-or, rarely, flips one sample's discrete decision (Russian roulette, a lobe or medium-event choice) and
-moves its pixel further.  The oracle, which follows the device's rounding policy, shows the same
-against the reference on its own scenes: C3 at 96×96×16 on Halton, 68 of 9216 float pixels differ,
-one u8 byte by 4; C3 64×64×16 and C5 48×48×8, u8 identical (tests/ref_lib vs tests/oracle_lib, CPU).
-So at most 0.1% of the pixels may differ by more than one."""
+Bar (tests/parity.py's, against the reference itself): the device walks the reference's own tree;
+wherever a float pixel is bit-identical its FrameBuffer bytes are identical; the float pixels that
+are not differ by a last-bit libm difference (glibc's float sinf/expf/logf/powf in the reference,
+correctly rounded transcendentals on the device) or — rarely — by one sample's flipped
+discrete decision (Russian roulette, a lobe or medium-event choice), so at most 2% of the pixels may
+differ by one 8-bit step and at most 0.1% by more."""
 import ctypes as C
 import os
 
@@ -31,48 +33,94 @@ def lib():
     capi.load_library()   # torch first, then the product's HIP runtime (see capi.load_library)
     L = C.CDLL(LIB)
     L.refbind_render.restype = C.c_int
-    L.refbind_render.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_double),
-                                 C.POINTER(C.c_int), C.c_char_p, C.c_int]
+    L.refbind_render.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_char_p, C.c_int]
     L.refbind_flatten.restype = C.c_int
-    L.refbind_flatten.argtypes = [C.c_int, C.POINTER(C.c_int), C.c_char_p, C.c_int]
+    L.refbind_flatten.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p,
+                                  C.c_int]
     return L
 
 
-@pytest.mark.parametrize("config", [2, 3, 5])
+def flatten(config):
+    L = lib()
+    counts, tex0, light0 = (C.c_int * 9)(), (C.c_int * 4)(), (C.c_int * 4)()
+    err = C.create_string_buffer(512)
+    rc = L.refbind_flatten(config, counts, tex0, light0, err, 512)
+    return rc, list(counts), list(tex0), list(light0), err.value.decode()
+
+
+@pytest.mark.parametrize("config", [2, 3, 4, 5, 6, 7])
 def test_flattener_hands_over_the_reference_scene(config):
     """SceneFlattener over the reference's own objects: every primitive of the BVHAccel and every
     light reaches the descriptor, with the reference's whole node array (at most 2n - 1 nodes:
     leaves of one primitive, main.cpp's maxPrimsInNode 1, except where SAH keeps primitives with
     coincident centroids together — the stand-in's pole triangles)."""
-    L = lib()
-    counts = (C.c_int * 8)()
-    err = C.create_string_buffer(512)
-    assert L.refbind_flatten(config, counts, err, 512) == 0, err.value.decode()
-    shapes, tris, mats, lights, media, nodes, ref_prims, ref_lights = list(counts)
+    rc, counts, tex0, light0, err = flatten(config)
+    assert rc == 0, err
+    shapes, tris, mats, lights, media, nodes, ref_prims, ref_lights, textures = counts
     assert tris == ref_prims and lights == ref_lights and ref_prims < nodes <= 2 * ref_prims - 1
     assert media == (1 if config == 5 else 0)
     assert shapes >= 2 and mats >= 1
+    assert mats == {4: 4, 6: 2}.get(config, mats)   # C4: glass, metal, plastic, matte; main.cpp: plastic, mirror
+    if config == 6:
+        # the ImageTexture (40 x 24 image) as its MIPMap's level 0: resampled to 64 x 32, RGB
+        assert textures == 1 and tex0 == [64, 32, 3, 1]
+        # the InfiniteAreaLight (96 x 48 image) as Lmap's level 0 (128 x 64) with Le = 1
+        assert light0 == [3, 128, 64, 1]
+    else:
+        assert textures == 0
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("config,res,spp", [(2, 96, 8), (3, 64, 16), (5, 48, 8)])
-def test_reference_render_equals_binding_render(config, res, spp):
+def test_orthographic_camera_is_refused_on_cpu():
+    """The binding renders PerspectiveCameras only; an OrthographicCamera is refused with a message
+    (scene 8), not rendered as if it were perspective.  (Flattening alone needs no camera: this
+    checks the scene of config 8 flattens, the refusal itself is on the device test below.)"""
+    rc, counts, _, _, err = flatten(8)
+    assert rc == 0, err
+
+
+def render(config, res, spp):
     L = lib()
     ref = np.zeros(res * res * 4, np.uint8)
     hip = np.zeros(res * res * 4, np.uint8)
+    ref_rgb = np.zeros(res * res * 3, np.float32)
+    hip_rgb = np.zeros(res * res * 3, np.float32)
     secs = (C.c_double * 2)()
     same_tree = C.c_int(0)
     err = C.create_string_buffer(512)
-    rc = L.refbind_render(config, res, spp, ref.ctypes.data, hip.ctypes.data, secs, C.byref(same_tree), err, 512)
-    assert rc == 0, err.value.decode()
-    assert same_tree.value == 1, "the device did not get the reference's BVHAccel node array"
-    r = ref.reshape(-1, 4).astype(int)
-    h = hip.reshape(-1, 4).astype(int)
-    diff = np.abs(r - h).max(axis=1)
-    same = float((diff == 0).mean())
-    print(f"config {config}: {same:.4f} of the pixels identical, max |Δ| {int(diff.max())}, "
-          f"reference {secs[0]:.2f} s, binding {secs[1]:.3f} s")
-    assert (r[:, 3] == 255).all() and (h[:, 3] == 255).all()
-    assert (diff <= 1).mean() >= 0.999, f"{int((diff > 1).sum())} pixels differ by more than one"
-    assert same >= 0.98, f"only {same:.4f} of the pixels identical"
-    assert r[:, :3].std() > 1.0   # a real image, not a blank frame
+    rc = L.refbind_render(config, res, spp, ref.ctypes.data, hip.ctypes.data, ref_rgb.ctypes.data, hip_rgb.ctypes.data,
+                          secs, C.byref(same_tree), err, 512)
+    return rc, err.value.decode(), ref, hip, ref_rgb, hip_rgb, same_tree.value, secs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,res,spp", [(2, 128, 8), (3, 128, 16), (4, 128, 16), (5, 128, 8), (6, 128, 16),
+                                            (7, 128, 8)])
+def test_reference_render_equals_binding_render(config, res, spp):
+    rc, err, ref, hip, ref_rgb, hip_rgb, same_tree, secs = render(config, res, spp)
+    assert rc == 0, err
+    assert same_tree == 1, "the device did not get the reference's BVHAccel node array"
+    # FrameBuffer rows are bottom-up (set_uc(x, H - 1 - y)); the float arrays are top-down
+    r8 = ref.reshape(res, res, 4)[::-1].reshape(-1, 4).astype(int)
+    h8 = hip.reshape(res, res, 4)[::-1].reshape(-1, 4).astype(int)
+    rf = ref_rgb.reshape(-1, 3)
+    hf = hip_rgb.reshape(-1, 3)
+    assert np.isfinite(hf).all()
+    same_f = np.all(rf.view(np.uint32) == hf.view(np.uint32), axis=1)
+    d8 = np.abs(r8 - h8).max(axis=1)
+    print(f"config {config}: {same_f.mean():.4f} of the float pixels bit-identical, u8: {(d8 == 0).mean():.4f} "
+          f"identical, {int((d8 == 1).sum())} one step, {int((d8 > 1).sum())} more (max {int(d8.max())}); "
+          f"float L∞ {float(np.abs(rf - hf).max()):.3g}; reference {secs[0]:.2f} s, binding {secs[1]:.3f} s")
+    assert (r8[:, 3] == 255).all() and (h8[:, 3] == 255).all()
+    assert (d8[same_f] == 0).all(), "8-bit output differs where the float pixel is bit-identical"
+    n = d8.size
+    assert (d8 == 1).sum() <= 0.02 * n, f"{int((d8 == 1).sum())} pixels differ by one step"
+    assert (d8 > 1).sum() <= 0.001 * n, f"{int((d8 > 1).sum())} pixels differ by more than one step"
+    assert same_f.mean() >= 0.5, f"only {same_f.mean():.4f} of the float pixels bit-identical"
+    assert r8[:, :3].std() > 1.0   # a real image, not a blank frame
+
+
+@pytest.mark.gpu
+def test_binding_refuses_an_orthographic_camera():
+    rc, err, *_ = render(8, 32, 1)
+    assert rc == -1 and "PerspectiveCamera" in err
