@@ -901,6 +901,63 @@ PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
     }
     return 0;
 }
+// lobe_f and lobe_pdf for one (wo, wi) in one pass (bsdf_f_pdf): the microfacet kinds evaluate the
+// half vector, D(wh) and Lambda(wo) once for both.  Every value is the separate functions' own:
+// the sums wi + wo and wo + wi are the same floats, and for transmission f's half vector is pdf's
+// turned to +z, where D — a function of wh.z², |wh.x / sinθ| and |wh.y / sinθ| — is the same and
+// the two dot products change sign together.  wantF: the caller adds f (BSDF::f's reflect /
+// transmit filter); f is then exactly what lobe_f returns, black where it returns black.
+template <int K = kAllLobes>
+PBR_HD void lobe_f_pdf(const Lobe& l, f3 wo, f3 wi, bool wantF, rgb* fOut, float* pdfOut) {
+    rgb f = sp(0.f);
+    float pdf = 0.f;
+    switch (l.kind) {
+    case L_MF_R: if constexpr (PBR_HAS(K, L_MF_R)) {
+        const float cO = abscos_t(wo), cI = abscos_t(wi);
+        const f3 whRaw = wi + wo;
+        const bool sh = same_hemi(wo, wi);
+        const bool fLive = wantF && !(cI == 0 || cO == 0) && !(whRaw.x == 0 && whRaw.y == 0 && whRaw.z == 0);
+        if (fLive || sh) {
+            const f3 wh = normalize(whRaw);
+            const float D = tr_D(l, wh), lo = tr_lambda(l, wo);
+            if (fLive) {
+                const rgb F = fresnel_eval(l, dot(wi, faceforward(wh, mk(0, 0, 1))));
+                const float G = 1 / (1 + lo + tr_lambda(l, wi));   // tr_G
+                f = ld3(l.R) * D * G * F / (4 * cI * cO);
+            }
+            if (sh) pdf = D * (1 / (1 + lo)) * absdot(wo, wh) / abscos_t(wo) / (4 * dot(wo, wh));   // tr_pdf / (4 wo·wh)
+        }
+        break;
+    } break;
+    case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
+        if (same_hemi(wo, wi)) break;
+        const float eta = cos_t(wo) > 0 ? (l.etaB / l.etaA) : (l.etaA / l.etaB);
+        const f3 whp = normalize(wo + wi * eta);   // lobe_pdf's half vector
+        if (dot(wo, whp) * dot(wi, whp) > 0) break;
+        const float D = tr_D(l, whp), lo = tr_lambda(l, wo);
+        const float cO = cos_t(wo), cI = cos_t(wi);
+        if (wantF && !(cI == 0 || cO == 0)) {
+            const f3 wh = whp.z < 0 ? -whp : whp;   // lobe_f's
+            const rgb F = sp(fr_dielectric(dot(wo, wh), l.etaA, l.etaB));
+            const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+            const float factor = 1 / eta;
+            const float G = 1 / (1 + lo + tr_lambda(l, wi));   // tr_G
+            f = (sp(1.f) - F) * ld3(l.T) *
+                fabsf(D * G * eta * eta * absdot(wi, wh) * absdot(wo, wh) * factor * factor / (cI * cO * sqrtDenom * sqrtDenom));
+        }
+        const float sqrtDenom = dot(wo, whp) + eta * dot(wi, whp);
+        const float dwh = fabsf((eta * eta * dot(wi, whp)) / (sqrtDenom * sqrtDenom));
+        pdf = D * (1 / (1 + lo)) * absdot(wo, whp) / abscos_t(wo) * dwh;   // tr_pdf · dwh
+        break;
+    } break;
+    default:
+        if (wantF) f = lobe_f<K>(l, wo, wi);
+        pdf = lobe_pdf<K>(l, wo, wi);
+        break;
+    }
+    *fOut = f;
+    *pdfOut = pdf;
+}
 // Sampling.cpp:74-92, Sampling.h:57-61
 PBR_HD void concentric_disk(float u0, float u1, float* dx, float* dy) {
     float ox = 2.f * u0 - 1, oy = 2.f * u1 - 1;
@@ -1012,6 +1069,31 @@ PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cp
     }
     return f;
 }
+// BSDF::f (Reflection.cpp:56-71) and BSDF::Pdf (:92-106) of one direction in one pass: the same
+// per-lobe values and the same sums in the same order, each lobe's shared terms evaluated once
+// (lobe_f_pdf).  Returns f; *pdf as bsdf_pdf.
+template <int K = kAllLobes>
+PBR_HD rgb bsdf_f_pdf(const BSDF& b, f3 woW, f3 wiW, int flags, float* pdfOut) {
+    const f3 wi = b.to_local(wiW), wo = b.to_local(woW);
+    if (wo.z == 0) { *pdfOut = 0.f; return sp(0.f); }   // both return 0 there (BSDF::Pdf also with no lobes)
+    const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    rgb f = sp(0.f);
+    float pdf = 0.f;
+    int m = 0;
+    for (int i = 0; i < b.mt->nLobes; ++i) {
+        const Lobe& l = b.mt->lobes[i];
+        if (!matches(l, flags)) continue;
+        ++m;
+        const bool wantF = (reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION));
+        rgb fl;
+        float pl;
+        lobe_f_pdf<K>(l, wo, wi, wantF, &fl, &pl);
+        if (wantF) f = f + fl;
+        pdf += pl;
+    }
+    *pdfOut = m > 0 ? pdf / m : 0.f;
+    return f;
+}
 template <int K = kAllLobes>
 PBR_HD float bsdf_pdf(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:92-106
     if (b.mt->nLobes == 0) return 0.f;
@@ -1023,11 +1105,23 @@ PBR_HD float bsdf_pdf(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflectio
         if (matches(b.mt->lobes[i], flags)) { ++m; pdf += lobe_pdf<K>(b.mt->lobes[i], wo, wi); }
     return m > 0 ? pdf / m : 0.f;
 }
-// Reflection.cpp:108-164. On the wo.z == 0 early-out *pdf and *sampledType are left as they were.
+// BSDF::Sample_f (Reflection.cpp:108-164) in two steps.  bsdf_sample_dir picks the lobe, samples
+// its direction and forms the pdf; bsdf_sample_sum forms the value — a specular lobe's own f, else
+// the sum of f over the matching lobes.  Both are pure, so a caller that needs the value only in some
+// cases (EstimateDirect's BSDF sample: only when the sampled direction can reach the light) asks for
+// it only then; bsdf_sample is the two in sequence.  dir returns false where the reference returns
+// black before the sum (no matching lobe, wo.z == 0 — *pdf and *sampledType left as they were —
+// or a zero pdf).
+struct BsdfDraw {
+    f3 wi;          // the sampled direction, local
+    rgb fSpec;      // a specular lobe's own value
+    bool specular;  // the chosen lobe is specular
+};
 template <int K = kAllLobes>
-PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float* pdf, int type, int* sampledType) {
+PBR_HD bool bsdf_sample_dir(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float* pdf, int type, int* sampledType,
+                            BsdfDraw* d) {
     int m = num_components(b, type);
-    if (m == 0) { *pdf = 0; *sampledType = 0; return sp(0.f); }
+    if (m == 0) { *pdf = 0; *sampledType = 0; return false; }
     int comp = (int)floorf(u0 * m);
     if (comp > m - 1) comp = m - 1;
     int chosen = -1, count = comp;
@@ -1036,28 +1130,39 @@ PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float
     const Lobe& bx = b.mt->lobes[chosen];
     float ur0 = mn(u0 * m - comp, kOneMinusEpsilon);
     f3 wi, wo = b.to_local(woW);
-    if (wo.z == 0) return sp(0.f);
+    if (wo.z == 0) return false;
     *pdf = 0;
     int st = bx.type;
-    rgb f = lobe_sample<K>(bx, wo, &wi, ur0, u1, pdf, &st);
+    d->fSpec = lobe_sample<K>(bx, wo, &wi, ur0, u1, pdf, &st);
     *sampledType = st;
-    if (*pdf == 0) { *sampledType = 0; return sp(0.f); }
+    if (*pdf == 0) { *sampledType = 0; return false; }
     *wiW = b.to_world(wi);
-    // (a non-specular lobe's f is the sum below: lobe_sample does not evaluate it)
-    if (!(bx.type & BSDF_SPECULAR) && m > 1)
+    d->wi = wi;
+    d->specular = (bx.type & BSDF_SPECULAR) != 0;
+    if (!d->specular && m > 1)
         for (int i = 0; i < b.mt->nLobes; ++i)
             if (i != chosen && matches(b.mt->lobes[i], type)) *pdf += lobe_pdf<K>(b.mt->lobes[i], wo, wi);
     if (m > 1) *pdf /= m;
-    if (!(bx.type & BSDF_SPECULAR)) {
-        bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
-        f = sp(0.f);
-        for (int i = 0; i < b.mt->nLobes; ++i) {
-            const Lobe& l = b.mt->lobes[i];
-            if (matches(l, type) && ((reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION))))
-                f = f + lobe_f<K>(l, wo, wi);
-        }
+    return true;
+}
+template <int K = kAllLobes>
+PBR_HD rgb bsdf_sample_sum(const BSDF& b, f3 woW, f3 wiW, int type, const BsdfDraw& d) {
+    if (d.specular) return d.fSpec;
+    const f3 wo = b.to_local(woW);   // the same operations as bsdf_sample_dir's: the same bits
+    bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    rgb f = sp(0.f);
+    for (int i = 0; i < b.mt->nLobes; ++i) {
+        const Lobe& l = b.mt->lobes[i];
+        if (matches(l, type) && ((reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION))))
+            f = f + lobe_f<K>(l, wo, d.wi);
     }
     return f;
+}
+template <int K = kAllLobes>
+PBR_HD rgb bsdf_sample(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float* pdf, int type, int* sampledType) {
+    BsdfDraw d;
+    if (!bsdf_sample_dir<K>(b, woW, wiW, u0, u1, pdf, type, sampledType, &d)) return sp(0.f);
+    return bsdf_sample_sum<K>(b, woW, *wiW, type, d);
 }
 // ImageTexture::Evaluate (ImageTexture.h:52-60) with zero differentials: MIPMap::triangle(0, st)
 // (MIPMap.h:240-252) on the level-0 texels, Texel's wrap modes (:166-190).

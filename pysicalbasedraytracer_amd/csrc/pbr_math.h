@@ -141,7 +141,15 @@ PBR_HD rgb operator/(rgb a, float s) { return sp3(a.r / s, a.g / s, a.b / s); }
 PBR_HD bool black(rgb a) { return a.r == 0.f && a.g == 0.f && a.b == 0.f; }
 PBR_HD float maxval(rgb a) { return mx(mx(a.r, a.g), a.b); }
 PBR_HD rgb sqrt_s(rgb a) { return sp3(sqrtf(a.r), sqrtf(a.g), sqrtf(a.b)); }
-PBR_HD rgb exp_s(rgb a) { return sp3(t_exp(a.r), t_exp(a.g), t_exp(a.b)); }
+// Spectrum Exp, per channel.  Three equal channels (a grey medium's transmittance: C5's) take one
+// evaluation — the same input gives the same bits — instead of three out-of-line fp64 calls.
+PBR_HD rgb exp_s(rgb a) {
+    if (a.r == a.g && a.g == a.b) {   // (±0 compare equal and exp(+0) == exp(-0); a NaN takes the general path)
+        const float e = t_exp(a.r);
+        return sp3(e, e, e);
+    }
+    return sp3(t_exp(a.r), t_exp(a.g), t_exp(a.b));
+}
 PBR_HD rgb clamp_s(rgb a) { return sp3(clampf(a.r, 0, PBR_INF), clampf(a.g, 0, PBR_INF), clampf(a.b, 0, PBR_INF)); }
 
 // 4x4 row-major transforms (Core/Transform.h)

@@ -39,6 +39,14 @@ __device__ __forceinline__ void prof_count(unsigned long long* ctr, bool pred) {
     const unsigned long long m = __ballot(pred), act = __ballot(1);
     if (m && (int)__lane_id() == __ffsll((long long)act) - 1) atomicAdd(ctr, (unsigned long long)__popcll(m));
 }
+// a per-lane count added once per wave (every active lane must call it): the lane-refill kernels count
+// in a register while they trace and add at the end, so a profiled launch runs the same loop as an
+// unprofiled one (a per-completion atomic had slowed the counting window's any-hit launches 2-8x)
+__device__ __forceinline__ void prof_add(unsigned long long* ctr, unsigned v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const unsigned long long act = __ballot(1);
+    if (v && (int)__lane_id() == __ffsll((long long)act) - 1) atomicAdd(ctr, (unsigned long long)v);
+}
 
 struct WfQueue {
     float4* o;      // origin.xyz, tMax (the hit distance once a closest-hit kernel has traced the ray)

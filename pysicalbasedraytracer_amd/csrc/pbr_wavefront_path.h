@@ -201,8 +201,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                                 rgb f;
                                 if constexpr (PBR_DIAG_SHADE & 1) { f = sp(0.25f); scatteringPdf = 0.5f; }
                                 else {
-                                f = bsdf_f<LOBES>(bsdf, wo, wi, flagsNS) * absdot(wi, isect.sn);
-                                scatteringPdf = bsdf_pdf<LOBES>(bsdf, wo, wi, flagsNS);
+                                f = bsdf_f_pdf<LOBES>(bsdf, wo, wi, flagsNS, &scatteringPdf) * absdot(wi, isect.sn);
                                 }
                                 if (!black(f)) {
                                     if (delta) A = f * Li / lightPdf;
@@ -219,24 +218,28 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
                             fB = sp(0.f);
                             weightB = 1.f;
                             if (!delta && !(PBR_DIAG_SHADE & 2)) {
+                                // EstimateDirect's BSDF sample (Integrator.cpp:126-174).  Its value f·|cos|
+                                // is only read when the sampled direction can reach the light — a specular
+                                // sample, or Pdf_Li != 0 — so it is formed only then (the checks are pure,
+                                // so their order does not change the outcome): most sampled directions miss
+                                // a small area light and skip the sum over the lobes.
                                 int stype = 0;
-                                fB = bsdf_sample<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
-                                fB = fB * absdot(wi, isect.sn);
-                                const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
-                                if (!black(fB) && scatteringPdf > 0) {
-                                    bool probeIt = true;
-                                    if (!sampledSpecular) {
-                                        float lp = (PBR_DIAG_SHADE & 4) ? 0.5f : pdf_li(S, light, isect, wi);
-                                        if (lp == 0) probeIt = false;
-                                        else {
-                                            float fp = 1 * scatteringPdf, gp = 1 * lp;
-                                            weightB = (fp * fp) / (fp * fp + gp * gp);
+                                BsdfDraw draw;
+                                if (bsdf_sample_dir<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype, &draw) &&
+                                    scatteringPdf > 0) {
+                                    const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
+                                    const float lp = sampledSpecular ? 0.f : ((PBR_DIAG_SHADE & 4) ? 0.5f : pdf_li(S, light, isect, wi));
+                                    if (sampledSpecular || lp != 0) {
+                                        fB = bsdf_sample_sum<LOBES>(bsdf, wo, wi, flagsNS, draw) * absdot(wi, isect.sn);
+                                        if (!black(fB)) {
+                                            if (!sampledSpecular) {
+                                                float fp = 1 * scatteringPdf, gp = 1 * lp;
+                                                weightB = (fp * fp) / (fp * fp + gp * gp);
+                                            }
+                                            probe = spawn_ray(isect, wi);
+                                            pushProbe = true;
+                                            dflags |= kWfpBPending;
                                         }
-                                    }
-                                    if (probeIt) {
-                                        probe = spawn_ray(isect, wi);
-                                        pushProbe = true;
-                                        dflags |= kWfpBPending;
                                     }
                                 }
                             }
@@ -335,6 +338,7 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_ANY) void k_wfp_shadow(WfpParam
     WfParams& W = X.W;
     const int n = seg_scan(W.shadowSeg);
     if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
+        unsigned visible = 0;   // profile field 1, added once per wave at the end
         traverse_stream<true, SHORT>(
             W.P.S, n,
             [&](int i, int* key) {
@@ -344,10 +348,13 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_ANY) void k_wfp_shadow(WfpParam
                 return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
             },
             [&](int q, bool hit, const Ray&, const HitRec&) {
-                if (W.prof) prof_count(W.prof + KP_WFP_SHADOW * kProfFields + 1, !hit);   // one atomic per wave
-                if (!hit) X.dFlags[W.sid[q]] |= kWfpVisible;   // the only writer of this record in this launch
+                if (!hit) {
+                    ++visible;
+                    X.dFlags[W.sid[q]] |= kWfpVisible;   // the only writer of this record in this launch
+                }
             },
             W.prof, KP_WFP_SHADOW);
+        if (W.prof) prof_add(W.prof + KP_WFP_SHADOW * kProfFields + 1, visible);
         return;
     }
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {

@@ -184,8 +184,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                     fA = sp(0.f);
                     if (lightPdf > 0 && !black(Li)) {
                         if (!mediumEvent) {
-                            fA = bsdf_f<LOBES>(bsdf, ref.wo, wi, flagsNS) * absdot(wi, ref.sn);
-                            scatteringPdf = bsdf_pdf<LOBES>(bsdf, ref.wo, wi, flagsNS);
+                            fA = bsdf_f_pdf<LOBES>(bsdf, ref.wo, wi, flagsNS, &scatteringPdf) * absdot(wi, ref.sn);
                         } else {
                             fA = sp(phase_hg(dot(ref.wo, wi), g));
                         }
@@ -199,18 +198,36 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
                     }
                     fB = sp(0.f);
                     weightB = 1.f;
-                    if (!delta) {
-                        bool sampledSpecular = false;
-                        if (!mediumEvent) {
-                            int stype = 0;
-                            fB = bsdf_sample<LOBES>(bsdf, ref.wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype);
-                            fB = fB * absdot(wi, ref.sn);
-                            sampledSpecular = (stype & BSDF_SPECULAR) != 0;
-                        } else {
-                            float p = hg_sample(g, ref.wo, &wi, uS0, uS1);
-                            fB = sp(p);
-                            scatteringPdf = p;
+                    if (!delta && !mediumEvent) {
+                        // EstimateDirect's BSDF sample (Integrator.cpp:126-174).  Its value f·|cos| is
+                        // only read when the sampled direction can reach the light — a specular
+                        // sample, or Pdf_Li != 0 — so it is formed only then (the checks are pure,
+                        // so their order does not change the outcome): most sampled directions miss
+                        // a small area light and skip the sum over the lobes.
+                        int stype = 0;
+                        BsdfDraw draw;
+                        if (bsdf_sample_dir<LOBES>(bsdf, ref.wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype, &draw) &&
+                            scatteringPdf > 0) {
+                            const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
+                            const float lp = sampledSpecular ? 0.f : pdf_li(S, light, ref, wi);
+                            if (sampledSpecular || lp != 0) {
+                                fB = bsdf_sample_sum<LOBES>(bsdf, ref.wo, wi, flagsNS, draw) * absdot(wi, ref.sn);
+                                if (!black(fB)) {
+                                    if (!sampledSpecular) {
+                                        float fp = 1 * scatteringPdf, gp = 1 * lp;
+                                        weightB = (fp * fp) / (fp * fp + gp * gp);
+                                    }
+                                    probe = spawn_ray(ref, wi);
+                                    pushProbe = true;
+                                    dflags |= kWfpBPending;
+                                }
+                            }
                         }
+                    } else if (!delta) {
+                        const bool sampledSpecular = false;
+                        float p = hg_sample(g, ref.wo, &wi, uS0, uS1);
+                        fB = sp(p);
+                        scatteringPdf = p;
                         if (!black(fB) && scatteringPdf > 0) {
                             bool probeIt = true;
                             if (!sampledSpecular) {

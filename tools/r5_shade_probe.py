@@ -16,6 +16,8 @@ from pysicalbasedraytracer_amd import HipRenderer, capi, scenes  # noqa: E402
 
 
 def scene(kind, w, h, spp):
+    if kind in ("c3", "c5"):   # the C3 / C5 scenes at a quarter of their raster
+        return scenes.CONFIGS[kind.upper()](w // 2, h // 2, spp)
     s = scenes.Scene()
     white = s.matte((0.8, 0.8, 0.8))
     recipes = {"glass": s.glass, "metal": s.metal, "plastic": s.plastic, "matte": lambda: s.matte((0.5, 0.5, 0.5))}
