@@ -33,6 +33,7 @@ an evenly spread sample of the frame's rows; plus the reference's as-shipped 4 t
 """
 import argparse
 import json
+import re
 import os
 import subprocess
 import sys
@@ -181,12 +182,26 @@ def pmc_traffic(config, build_info):
     return t, f"{os.path.relpath(path, ROOT)} ({t['method']})"
 
 
+def kernel_family(name):
+    """The profile family of a rocprof kernel name (template arguments stripped): k_wf_shade's CAMERA
+    instances (4th template argument true) are the fused level-0 launches, family k_wf_shade_l0."""
+    m = re.search(r"(k_\w+?)(<([^()]*)>)?(\(|$)", name)
+    if not m:
+        return None
+    fam = m.group(1)
+    if fam == "k_wf_shade" and m.group(3):
+        targs = [a.strip() for a in m.group(3).split(",")]
+        if len(targs) >= 4 and targs[3] == "true":
+            fam = "k_wf_shade_l0"
+    return fam
+
+
 def family_traffic(t, family):
     """PMC bytes per frame of one kernel family (rocprof names carry template arguments)."""
     rd = wr = 0.0
     hit = False
     for k, v in t["per_kernel"].items():
-        if k == family or k.startswith(family + "<"):
+        if kernel_family(k) == family:
             rd += v["read_bytes"]
             wr += v["write_bytes"]
             hit = True
@@ -203,6 +218,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU render for the baseline")
     ap.add_argument("--no-model", action="store_true", help="skip the SURVEY-model counting pass")
     ap.add_argument("--serial", action="store_true", help="every window on the serial (one-stream) schedule")
+    ap.add_argument("--per-frame", action="store_true",
+                    help="one pbr_hip_render call per frame (a join between frames) instead of one batch per window")
     ap.add_argument("--cpu-baseline-worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--threads", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--budget", type=float, default=10.0, help=argparse.SUPPRESS)
@@ -249,7 +266,10 @@ def main():
     # multi-GPU: rank 0 gathers the packed RGBA8 tile spans (the FrameBuffer the reference's Render
     # fills) over RCCL; double-buffered outputs let the gather of frame k (communication stream)
     # overlap the render of frame k+1 (render stream)
-    nbuf = 2 if world > 1 else 1
+    # one output pair per frame of a window: the frames of a window are one pbr_hip_render_frames
+    # batch (their chunks continue one rotation over the lanes, no join between frames), so no frame
+    # may overwrite a buffer an earlier frame's gather still reads
+    nbuf = max(2 if world > 1 else 1, args.steps)
     rgbs = [torch.empty((npx, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     rgbas = [torch.empty((npx, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     exchange = FrameGather(W, H, world, dev, channels=4, dtype=torch.uint8) if world > 1 else None
@@ -274,13 +294,27 @@ def main():
                 done.record(comm)
             released[b] = done
 
+    def frames(k):
+        """k frames as one batch (pbr_hip_render_frames); each frame's gather waits for that frame."""
+        r.render_frames(rdr, [rgbs[f].data_ptr() for f in range(k)], [rgbas[f].data_ptr() for f in range(k)],
+                        stream=stream.cuda_stream)
+        if exchange is not None:
+            for f in range(k):
+                r.wait_frame(comm.cuda_stream, f)
+                with torch.cuda.stream(comm):
+                    exchange(rgbas[f], rank)
+            stream.wait_stream(comm)
+
     def window(k):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(k):
-            render()
+        if args.per_frame:
+            for _ in range(k):
+                render()
+        else:
+            frames(k)
         r.sync()
         if world > 1:
             dist.barrier()

@@ -308,6 +308,20 @@ const char* pbr_hip_last_error(const pbr_hip_ctx* ctx);
 /* Waits for the context's asynchronous frames; returns PBR_E_UNSUPPORTED if one of them stopped at
  * a safety bound (see above). */
 int pbr_hip_sync(pbr_hip_ctx* ctx);
+/* n frames of one descriptor in one call — SamplerIntegrator::Render (Integrator.cpp:280-356) n
+ * times, e.g. the frames of an animation or the timed frames of a benchmark.  The frames' chunks
+ * continue one rotation over the chunk lanes with no join between frames, so the launches that end
+ * one frame overlap the ones that start the next (a frame of few chunks — a multi-GPU rank's shard —
+ * otherwise leaves the GPU part idle at its end).  Every frame is the same bits as pbr_hip_render's.
+ * Frame f goes to rgb_outs[f] / rgba_outs[f] (device pointers; either array may be NULL).  Requires
+ * desc->outputs_on_device = 1, collect_stats = 0, no sample table.  Asynchronous: returns once the
+ * frames are enqueued; desc->stream (NULL: the context stream) reaches its tail when all are done;
+ * pbr_hip_wait_frame orders another stream after one frame. */
+int pbr_hip_render_frames(pbr_hip_ctx* ctx, const pbr_render_desc* desc, int n, float* const* rgb_outs,
+                          uint8_t* const* rgba_outs);
+/* Makes `stream` (hipStream_t; NULL = the context stream) wait until frame f of the last
+ * pbr_hip_render_frames call is complete (e.g. before gathering it to another GPU). */
+int pbr_hip_wait_frame(pbr_hip_ctx* ctx, void* stream, int f);
 
 /* ---- schedule (no reference counterpart) ----
  * How a frame is cut into launches on the device.  Every setting renders the same bits (the GPU

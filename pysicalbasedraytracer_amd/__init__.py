@@ -87,6 +87,22 @@ class HipRenderer:
                                             C.byref(st) if st is not None else None), "render")
         return st
 
+    def render_frames(self, rdesc, rgb_ptrs, rgba_ptrs, stream: int | None = None):
+        """n frames of one descriptor into device buffers (pbr_hip_render_frames): their chunks
+        continue one rotation over the lanes with no join between frames.  Asynchronous; `stream`
+        reaches its tail when every frame is done; wait_frame orders another stream after one."""
+        n = max(len(rgb_ptrs), len(rgba_ptrs))
+        rgb = (C.c_void_p * n)(*[p or None for p in rgb_ptrs]) if rgb_ptrs else None
+        rgba = (C.c_void_p * n)(*[p or None for p in rgba_ptrs]) if rgba_ptrs else None
+        rdesc.outputs_on_device = 1
+        rdesc.stream = stream
+        rdesc.collect_stats = 0
+        self._check(self.lib.pbr_hip_render_frames(self.ctx, C.byref(rdesc), n, rgb, rgba), "render_frames")
+
+    def wait_frame(self, stream: int | None, f: int):
+        """Make `stream` wait for frame f of the last render_frames call (pbr_hip_wait_frame)."""
+        self._check(self.lib.pbr_hip_wait_frame(self.ctx, stream, f), "wait_frame")
+
     def set_schedule(self, kernels=capi.KERNELS_AUTO, chunk_log2=0, lanes=0, fuse_camera=capi.FUSE_AUTO, serial=False):
         """How later frames are cut into launches (pbr_hip_set_schedule); no arguments = the measured
         default; serial=True runs every launch on the caller's stream in turn (measurement).  Results

@@ -235,6 +235,9 @@ EXPORTS = {
     "pbr_hip_destroy": (C.c_int, [C.c_void_p]),
     "pbr_hip_last_error": (C.c_char_p, [C.c_void_p]),
     "pbr_hip_sync": (C.c_int, [C.c_void_p]),
+    "pbr_hip_render_frames": (C.c_int, [C.c_void_p, C.POINTER(RenderDesc), C.c_int, C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_void_p)]),
+    "pbr_hip_wait_frame": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "pbr_hip_get_bvh": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int32),
                                   C.POINTER(C.c_int)]),
     "pbr_hip_sampler_values": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -271,7 +274,8 @@ _lib = None
 
 OPTIONAL_FOR_AB = ("pbr_hip_sync", "pbr_hip_set_profiling", "pbr_hip_get_profile", "pbr_hip_query", "pbr_hip_bounds",
                    "pbr_hip_li", "pbr_hip_set_bvh_build", "pbr_hip_bvh_build_info", "pbr_hip_build_bvh",
-                   "pbr_hip_set_schedule", "pbr_hip_sample_index", "pbr_hip_sample_dimensions")
+                   "pbr_hip_set_schedule", "pbr_hip_sample_index", "pbr_hip_sample_dimensions",
+                   "pbr_hip_render_frames", "pbr_hip_wait_frame")
 
 
 def load_library(path: str | None = None) -> C.CDLL:
@@ -297,9 +301,8 @@ def load_library(path: str | None = None) -> C.CDLL:
         fn.restype = res
         fn.argtypes = args
     v = lib.pbr_hip_abi_version()
-    # an experimental build passed by path (A/B timing) may be one ABI version older: v3 → v4 only
-    # added pbr_hip_set_schedule, the descriptors are unchanged
-    if v != ABI_VERSION and not (path is not None and v == ABI_VERSION - 1):
+    # (v5 changed the texture and camera descriptors: an older build cannot take these structures)
+    if v != ABI_VERSION:
         raise RuntimeError("libpbr_hip.so ABI version mismatch")
     if path is None:
         _lib = lib

@@ -303,6 +303,11 @@ struct QuadSlots {   // one quad node's four slots in visit order
     int ref[4];
     bool k[4];       // slab passes (box valid)
 };
+// A quad node's four slots from its fetched 128 B (LX..HZ: SoA boxes, R: child refs, meta: axes,
+// valid mask).
+template <bool ANY>
+__device__ __forceinline__ void quad_slots_of(float4 LX, float4 LY, float4 LZ, float4 HX, float4 HY, float4 HZ, float4 R,
+                                              int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q);
 template <bool ANY>
 __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const Ray& r, f3 inv, bool n0, bool n1, bool n2,
                                            QuadSlots* q) {
@@ -321,6 +326,11 @@ __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const 
         LX = w[0]; LY = w[1]; LZ = w[2]; HX = w[3]; HY = w[4]; HZ = w[5]; R = w[6];
         meta = __float_as_int(w[7].x);
     }
+    quad_slots_of<ANY>(LX, LY, LZ, HX, HY, HZ, R, meta, r, inv, n0, n1, n2, q);
+}
+template <bool ANY>
+__device__ __forceinline__ void quad_slots_of(float4 LX, float4 LY, float4 LZ, float4 HX, float4 HY, float4 HZ, float4 R,
+                                              int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q) {
     float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
     bool k0 = node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t0) & ((meta >> 8) & 1);
     bool k1 = node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t1) & ((meta >> 9) & 1);
@@ -367,17 +377,44 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
 #if PBR_TRAV_DIAG
         h->steps++;
 #endif
-        if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
+        // One memory round trip per step for every lane (traverse_stream): a lane at a leaf fetches
+        // its first primitive, a lane at a quad node the node, before either waits.
+        float4 f0, f1, f2, f3, f4, f5, f6, f7;
+        const bool atLeaf = cur < 0;
+        {
+            const int ucur = __builtin_amdgcn_readfirstlane(cur);
+            if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {   // the wave at one place
+                if (atLeaf) {
+                    const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)(ucur & 0x7fffffff));
+                    f0 = as_f4(tv[0]); f1 = as_f4(tv[1]); f2 = as_f4(tv[2]);
+                } else {
+                    const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
+                    f0 = as_f4(w[0]); f1 = as_f4(w[1]); f2 = as_f4(w[2]); f3 = as_f4(w[3]); f4 = as_f4(w[4]);
+                    f5 = as_f4(w[5]); f6 = as_f4(w[6]); f7 = as_f4(w[7]);
+                }
+            } else {
+                const float4* src = atLeaf ? S.triVerts + 3 * (size_t)(cur & 0x7fffffff) : S.quad + 8 * (size_t)cur;
+                f0 = src[0]; f1 = src[1]; f2 = src[2];
+                if (!atLeaf) { f3 = src[3]; f4 = src[4]; f5 = src[5]; f6 = src[6]; f7 = src[7]; }
+            }
+        }
+        if (atLeaf) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
             int slot = cur & 0x7fffffff;
+            bool first = true;
             while (true) {
                 float4 v0, v1, v2;
-                const int uslot = __builtin_amdgcn_readfirstlane(slot);
-                if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {   // one primitive for the wave
-                    const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
-                    v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
+                if (first) {   // fetched above
+                    v0 = f0; v1 = f1; v2 = f2;
+                    first = false;
                 } else {
-                    const float4* tv = S.triVerts + 3 * (size_t)slot;
-                    v0 = tv[0]; v1 = tv[1]; v2 = tv[2];
+                    const int uslot = __builtin_amdgcn_readfirstlane(slot);
+                    if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {   // one primitive for the wave
+                        const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
+                        v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
+                    } else {
+                        const float4* tv = S.triVerts + 3 * (size_t)slot;
+                        v0 = tv[0]; v1 = tv[1]; v2 = tv[2];
+                    }
                 }
                 int flags = __float_as_int(v0.w);
                 float t, b0 = 0, b1 = 0, b2 = 0;
@@ -395,7 +432,7 @@ __device__ bool traverse_quad(const DeviceScene& S, Ray& r, HitRec* h, f3 inv, b
             }
         } else {
             QuadSlots q;
-            quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
+            quad_slots_of<ANY>(f0, f1, f2, f3, f4, f5, f6, __float_as_int(f7.x), r, inv, n0, n1, n2, &q);
             const float tM = r.tMax;
             const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
                        p3 = q.k[3] && q.t[3] < tM;

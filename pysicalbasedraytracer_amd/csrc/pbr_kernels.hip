@@ -54,7 +54,8 @@ constexpr int kSobolNibHi = 80;                    // index bits 32..51: 5 nibbl
 constexpr int kLdsSobolDims = 34;                  // 34 × 512 B fit the Halton permutation array
 static_assert(kLdsSobolDims * kSobolNib * 4 <= kLdsPermEntries * 2, "Sobol LDS tables share the Halton array");
 __shared__ __align__(16) uint16_t s_halton_perm[kLdsPermEntries];
-__shared__ uint4 s_halton_tab[kLdsDims];           // prime, floor(2^32/prime), primeSums
+__shared__ uint4 s_halton_tab[kLdsDims];           // prime, floor(2^32/prime), primeSums, 1/prime (float bits)
+__shared__ float s_halton_tail[kLdsDims];          // invBase·perm[0] / (1 - invBase), the digit series' tail
 
 __device__ __forceinline__ int sobol_lds_dims(const DeviceSampler& s) {
     return min(min(s.ldsDims, kLdsSobolDims), s.nSobolDims);
@@ -71,8 +72,13 @@ __device__ __forceinline__ void stage_halton_lds(const DeviceSampler& s) {
         return;
     }
     const int nd = s.ldsDims;
-    for (int i = threadIdx.x; i < nd; i += blockDim.x)
-        s_halton_tab[i] = make_uint4(s.primes[i], s.recips[i], s.primeSums[i], 0u);
+    for (int i = threadIdx.x; i < nd; i += blockDim.x) {
+        // ScrambledRadicalInverse's two per-call divisions (LowDiscrepancy.cpp:2302, :2314), formed once:
+        // the same operations on the same values, so the same bits
+        const float invBase = 1.f / (float)s.primes[i];
+        s_halton_tab[i] = make_uint4(s.primes[i], s.recips[i], s.primeSums[i], __float_as_uint(invBase));
+        s_halton_tail[i] = invBase * (float)s.perms[s.primeSums[i]] / (1 - invBase);
+    }
     const int n = nd > 0 ? (int)(s.primeSums[nd - 1] + s.primes[nd - 1]) : 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) s_halton_perm[i] = s.perms[i];
 }
@@ -158,7 +164,7 @@ __device__ __forceinline__ float sample_dimension(const DeviceSampler& s, uint32
     if constexpr (LDS) {
         if (dim < s.ldsDims) {
             uint4 t = s_halton_tab[dim];
-            return scrambled_radical_inverse(t.x, t.y, s_halton_perm + t.z, index);
+            return scrambled_radical_inverse_pre(t.x, t.y, s_halton_perm + t.z, index, __uint_as_float(t.w), s_halton_tail[dim]);
         }
     }
     return scrambled_radical_inverse(s.primes[dim], s.recips[dim], s.perms + s.primeSums[dim], index);
@@ -866,6 +872,12 @@ struct pbr_hip_ctx {
     WfBufs wb[kWfLanes];
     hipStream_t side[kWfLanes] = {};     // lanes 1.. (lane 0 runs on the caller's stream)
     hipEvent_t evFork = nullptr, evJoin[kWfLanes] = {};
+    struct FrameEv {                     // a batch: the end of frame f's last chunk on each lane it used
+        hipEvent_t ev[kWfLanes] = {};
+        unsigned used = 0;
+    };
+    std::vector<FrameEv> frameEv;        // (pbr_hip_wait_frame)
+    int batchFrames = 0;                 // frames of the last batch
     // Whitted: per lane, a stream for the shadow rays and per-level events (shade done, shadow done)
     hipStream_t shadowStream[kWfLanes] = {};
     hipEvent_t evShade[kWfLanes][kWfMaxDepth + 2] = {}, evShadow[kWfLanes][kWfMaxDepth + 2] = {};
@@ -1085,14 +1097,14 @@ struct WfChunks {
     int segCap = 0;   // capacity of one queue segment
     size_t qcap = 0;  // queue entries
 };
-WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25) {
+WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25, bool batch = false) {
     WfChunks c;
     const int chunkLog2 = sch.chunk_log2 > 0 ? std::min(sch.chunk_log2, maxLog2) : maxLog2;   // the default bounds the memory
     c.lanes = sch.serial ? 1 : (sch.lanes > 0 ? sch.lanes : kWfDefaultLanes);
     c.chunkPix = std::max(1LL, (1LL << chunkLog2) / P.spp);
     if (c.chunkPix >= P.nPixels) {   // one chunk: splitting a small frame only adds launch tails
         c.chunkPix = P.nPixels;
-        c.lanes = 1;
+        if (!batch) c.lanes = 1;     // (a batch's one-chunk frames rotate over the lanes)
     } else {
         // Many chunks: make them equal and a whole number per lane (the count rounded down to a
         // multiple of the lanes), so no lane runs a last chunk alone.  Measured (bit-identical,
@@ -1111,7 +1123,22 @@ WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25) 
     c.qcap = std::max(c.cap, (size_t)c.segCap * kWfBlocks);
     return c;
 }
-// Fork lane 1 off `s` at the start of a frame, join it back at the end.
+// The frames of one render call.  One frame (pbr_hip_render): its chunks alternate over the lanes,
+// lane 0 on the caller's stream, forked at the start and joined at the end.  A batch
+// (pbr_hip_render_frames): the frames' chunks continue one rotation over the same lanes, forked once
+// and joined once, so one frame's last launches overlap the next frame's first ones.  No stream
+// waits between frames: frame f's end is one event per lane it used (frameEv[f]), which
+// pbr_hip_wait_frame hands to the caller's other streams.  (A first version ran every lane on a side
+// stream and made the caller's stream wait for each frame: C2 15.7 → 17.0 ms — that stream's waits
+// sat in a hardware queue it shares with a lane, holding the lane's next frame behind them.)
+struct FrameSet {
+    int n = 1;
+    float* const* rgb = nullptr;     // per frame (batch); the single frame's outputs are in KParams
+    uint8_t* const* rgba = nullptr;
+    bool batch = false;
+};
+hipStream_t lane_stream(pbr_hip_ctx* ctx, hipStream_t s, int l) { return l ? ctx->side[l] : s; }
+// Fork the lanes off `s` at the start of a frame (a batch), join them back at the end.
 int wf_fork(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
     if (lanes < 2) return PBR_OK;
     if (!ctx->evFork) HIP_TRY(hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
@@ -1129,6 +1156,19 @@ int wf_join(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
     for (int l = 1; l < lanes; ++l) {
         HIP_TRY(hipEventRecord(ctx->evJoin[l], ctx->side[l]));
         HIP_TRY(hipStreamWaitEvent(s, ctx->evJoin[l], 0));
+    }
+    return PBR_OK;
+}
+// A batch: frame f's chunks ended on the lanes in `used` (bit mask; lane 0 is `s`): one event per
+// lane, recorded after the lane's last launch of the frame (pbr_hip_wait_frame waits on them).
+int wf_frame_done(pbr_hip_ctx* ctx, hipStream_t s, int f, unsigned used) {
+    if ((int)ctx->frameEv.size() <= f) ctx->frameEv.resize(f + 1);
+    pbr_hip_ctx::FrameEv& e = ctx->frameEv[f];
+    e.used = used;
+    for (int l = 0; l < kWfLanes; ++l) {
+        if (!(used & (1u << l))) continue;
+        if (!e.ev[l]) HIP_TRY(hipEventCreateWithFlags(&e.ev[l], hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(e.ev[l], lane_stream(ctx, s, l)));
     }
     return PBR_OK;
 }
@@ -1178,7 +1218,7 @@ void prof_host(pbr_hip_ctx* ctx, int kind, int field, unsigned long long v) {
 
 // Wavefront Whitted: chunks of up to 2^25 samples on two lanes, per level shade → shadow → extend
 // (pbr_wavefront.h).
-int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
+int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, const FrameSet& F) {
     const int spp = P.spp;
     // samples per chunk: queue + record memory ≈ 370 B per sample at depth 5 (12 GB at 2^25);
     // measured on C2 (one lane): 2^23 29.4 ms, 2^24 28.1, 2^25 26.6, 2^27 (whole frame) 26.6
@@ -1194,7 +1234,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     // they stay under 8 GB per lane (C2: 5 levels × 36 B × 2^25 = 6 GB)
     int maxLog2 = 25;
     while (maxLog2 > 20 && (double)levels * (36.0 + (ml ? 17.0 * nL : 0.0)) * (double)(1LL << maxLog2) > 8e9) --maxLog2;
-    const WfChunks ch = wf_chunks(ctx->sched, P, maxLog2);
+    const WfChunks ch = wf_chunks(ctx->sched, P, maxLog2, F.batch);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const int lightsPerShade = ml ? std::max(1, nL) : 1;
     const size_t sqcap = qcap * (size_t)lightsPerShade;   // shadow-queue entries
@@ -1217,7 +1257,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     // only read what shade(L) wrote); the shadow queue alternates between two buffers by level.
     // Default: when the frame is one chunk (no lane overlap).  Measured on C2: a 1/8 shard
     // 3.97 → 3.54 ms; the whole frame (two lanes) 23.43 → 23.76 ms, so off there.
-    const bool shadowOverlap = ch.lanes == 1 && !ctx->sched.serial && maxLevels <= kWfMaxDepth + 2;
+    const bool shadowOverlap = ch.lanes == 1 && !F.batch && !ctx->sched.serial && maxLevels <= kWfMaxDepth + 2;
     WfParams WL[kWfLanes];
     int* cntL[kWfLanes];
     for (int l = 0; l < ch.lanes; ++l) {
@@ -1283,11 +1323,18 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
     const dim3 gShadowML = resident_grid(ctx, (const void*)k_wf_shadow_ml<kShortStack>);
     const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack>);
     if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
-    int chunk = 0;
+    int chunk = 0;   // a batch: one rotation over the lanes through all its frames
+    for (int f = 0; f < F.n; ++f) {
+    unsigned used = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
         const int l = chunk % ch.lanes;
-        const hipStream_t st = l ? ctx->side[l] : s;
+        const hipStream_t st = lane_stream(ctx, s, l);
         WfParams& W = WL[l];
+        if (F.batch) {
+            W.P.rgbOut = F.rgb ? F.rgb[f] : nullptr;
+            W.P.rgbaOut = F.rgba ? F.rgba[f] : nullptr;
+            used |= 1u << l;
+        }
         W.chunkPix0 = p0;
         W.chunkPix = (int)std::min<long long>(ch.chunkPix, P.nPixels - p0);
         W.nSamples = W.chunkPix * spp;
@@ -1313,7 +1360,8 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
                 if (level >= 2) HIP_TRY(hipStreamWaitEvent(st, ctx->evShadow[l][level - 2], 0));
             }
             const int l0 = level == 0 ? 1 : 0;
-            PROF_LAUNCH(KP_WF_SHADE, st,
+            const int kShade = l0 && fuseCamera ? KP_WF_SHADE0 : KP_WF_SHADE;   // (the fused level 0: its own family)
+            PROF_LAUNCH(kShade, st,
             if (textured) {
                 if (ml) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes | kTexturedLobes, false>), gstride, blk, 0, st, W, l0);
                 else hipLaunchKernelGGL((k_wf_shade<kAllLobes | kTexturedLobes, false>), gstride, blk, 0, st, W, l0);
@@ -1331,9 +1379,9 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
             else if (simple) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
             else if (matsLds) hipLaunchKernelGGL((k_wf_shade<kAllLobes, true>), gstride, blk, 0, st, W, l0);
             else hipLaunchKernelGGL((k_wf_shade<kAllLobes, false>), gstride, blk, 0, st, W, l0));
-            if (l0) prof_host(ctx, KP_WF_SHADE, 0, (unsigned long long)W.nSamples);
-            if (l0 && fuseCamera && !textured && !ml) prof_host(ctx, KP_WF_SHADE, 6, (unsigned long long)W.nSamples);
-            if (int rc = prof_sums(ctx, st, KP_WF_SHADE, {l0 ? nullptr : W.cur.segCount, W.shadowSeg, nullptr, nullptr,
+            if (l0) prof_host(ctx, kShade, 0, (unsigned long long)W.nSamples);
+            if (l0 && fuseCamera && !textured && !ml) prof_host(ctx, kShade, 6, (unsigned long long)W.nSamples);
+            if (int rc = prof_sums(ctx, st, kShade, {l0 ? nullptr : W.cur.segCount, W.shadowSeg, nullptr, nullptr,
                                                           W.next.segCount, l0 ? nullptr : W.cur.segCount, nullptr,
                                                           skyDeferred ? W.shadowSeg : nullptr})) return rc;
             if (shadowOverlap) {
@@ -1358,16 +1406,18 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s) {
         prof_host(ctx, KP_WF_FINISH, 0, (unsigned long long)W.chunkPix);
         prof_host(ctx, KP_WF_FINISH, 1, (unsigned long long)W.nSamples);
     }
+    if (F.batch) { if (int rc = wf_frame_done(ctx, s, f, used)) return rc; }
+    }
     HIP_TRY(hipGetLastError());
     return wf_join(ctx, s, ch.lanes);
 }
 
 // Wavefront Path: per bounce shade → shadow → probe → resolve → extend (pbr_wavefront_path.h).
-int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol) {
+int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol, const FrameSet& F) {
     const int spp = P.spp;
     // ≈ 290 B of queues + state per sample: 19.5 GB per 2^26 chunk and lane.  Measured (bit-identical):
     // C3 2^25 349.4 ms, 2^26 336.1, 2^27 340.4; C5 2^25 1979 ms, 2^26 1939, 2^27 1919
-    const WfChunks ch = wf_chunks(ctx->sched, P, 26);
+    const WfChunks ch = wf_chunks(ctx->sched, P, 26, F.batch);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
@@ -1450,13 +1500,20 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
     const int maxLevels = std::max(1, P.maxDepth) + 1 + (ctx->host.anyNoMaterial ? 32 : 0);
     std::vector<int> segHost(kWfBlocks);
     if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
-    int chunk = 0;
+    int chunk = 0;   // a batch: one rotation over the lanes through all its frames
+    for (int f = 0; f < F.n; ++f) {
+    unsigned used = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
         const int l = chunk % ch.lanes;
-        const hipStream_t st = l ? ctx->side[l] : s;
+        const hipStream_t st = lane_stream(ctx, s, l);
         WfvParams& V = VL[l];
         WfpParams& X = V.X;
         WfParams& W = X.W;
+        if (F.batch) {
+            W.P.rgbOut = F.rgb ? F.rgb[f] : nullptr;
+            W.P.rgbaOut = F.rgba ? F.rgba[f] : nullptr;
+            used |= 1u << l;
+        }
         W.chunkPix0 = p0;
         W.chunkPix = (int)std::min<long long>(ch.chunkPix, P.nPixels - p0);
         W.nSamples = W.chunkPix * spp;
@@ -1525,6 +1582,8 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol)
         PROF_LAUNCH(KP_WFP_FINISH, st, hipLaunchKernelGGL(k_wfp_finish, dim3((W.chunkPix + pb - 1) / pb), blk, 0, st, X));
         prof_host(ctx, KP_WFP_FINISH, 0, (unsigned long long)W.chunkPix);
         prof_host(ctx, KP_WFP_FINISH, 1, (unsigned long long)W.nSamples);
+    }
+    if (F.batch) { if (int rc = wf_frame_done(ctx, s, f, used)) return rc; }
     }
     HIP_TRY(hipGetLastError());
     return wf_join(ctx, s, ch.lanes);
@@ -1779,6 +1838,9 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
         if (ctx->shadowStream[l]) (void)hipStreamDestroy(ctx->shadowStream[l]);
     }
     if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
+    for (const pbr_hip_ctx::FrameEv& e : ctx->frameEv)
+        for (int l = 0; l < kWfLanes; ++l)
+            if (e.ev[l]) (void)hipEventDestroy(e.ev[l]);
     for (int l = 0; l < kWfLanes; ++l) {
         if (ctx->evJoin[l]) (void)hipEventDestroy(ctx->evJoin[l]);
         if (ctx->side[l]) (void)hipStreamDestroy(ctx->side[l]);
@@ -1884,10 +1946,14 @@ int pbr_hip_upload_scene(pbr_hip_ctx* ctx, const pbr_scene_desc* desc) {
     return PBR_OK;
 }
 
-int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, uint8_t* rgba_out, pbr_render_stats* stats) {
+static int render_impl(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, uint8_t* rgba_out, pbr_render_stats* stats,
+                       const FrameSet& F) {
     if (!ctx) return PBR_E_INVALID;
     if (!d) return set_err(ctx, PBR_E_INVALID, "null render desc");
     if (!ctx->haveScene) return set_err(ctx, PBR_E_NOSCENE, "no scene uploaded");
+    if (F.batch && (!d->outputs_on_device || d->collect_stats || stats || d->sampler == PBR_SAMPLER_TABLE || F.n < 1))
+        return set_err(ctx, PBR_E_INVALID, "render_frames: device outputs, no stats, no sample table, n >= 1");
+    if (F.batch) ctx->batchFrames = 0;   // (set when the batch is queued)
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(ctx->device));
     // An earlier asynchronous frame that stopped at a safety bound fails this call.  Only scenes with
@@ -1973,24 +2039,32 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
     if (st) hipLaunchKernelGGL((k_render<I, true, 1>), grid, block, 0, s, P);                        \
     else hipLaunchKernelGGL((k_render<I, false, 2>), grid, block, 0, s, P);
         if (wavefront || wavefrontPath) {
-            int rc = wavefront ? render_wavefront(ctx, P, s) : render_wavefront_path(ctx, P, s, d->integrator == PBR_INTEGRATOR_VOLPATH);
+            int rc = wavefront ? render_wavefront(ctx, P, s, F) : render_wavefront_path(ctx, P, s, d->integrator == PBR_INTEGRATOR_VOLPATH, F);
             if (rc) {   // stopped part-way: the forked lane / shadow streams may still run
                 quiesce(ctx, s);
                 return rc;
             }
         } else {
-            PROF_LAUNCH(KP_MEGA, s,
-                switch (d->integrator) {
-                case PBR_INTEGRATOR_WHITTED: PBR_LAUNCH(PBR_INTEGRATOR_WHITTED) break;
-                case PBR_INTEGRATOR_PATH: PBR_LAUNCH(PBR_INTEGRATOR_PATH) break;
-                default: PBR_LAUNCH(PBR_INTEGRATOR_VOLPATH) break;
-                });
-            prof_host(ctx, KP_MEGA, 0, (unsigned long long)npx * (unsigned long long)spp);
-            prof_host(ctx, KP_MEGA, 1, (unsigned long long)npx);
+            for (int f = 0; f < F.n; ++f) {   // (a batch: frame after frame on `s`)
+                if (F.batch) {
+                    P.rgbOut = F.rgb ? F.rgb[f] : nullptr;
+                    P.rgbaOut = F.rgba ? F.rgba[f] : nullptr;
+                }
+                PROF_LAUNCH(KP_MEGA, s,
+                    switch (d->integrator) {
+                    case PBR_INTEGRATOR_WHITTED: PBR_LAUNCH(PBR_INTEGRATOR_WHITTED) break;
+                    case PBR_INTEGRATOR_PATH: PBR_LAUNCH(PBR_INTEGRATOR_PATH) break;
+                    default: PBR_LAUNCH(PBR_INTEGRATOR_VOLPATH) break;
+                    });
+                prof_host(ctx, KP_MEGA, 0, (unsigned long long)npx * (unsigned long long)spp);
+                prof_host(ctx, KP_MEGA, 1, (unsigned long long)npx);
+                if (F.batch) { if (int rc = wf_frame_done(ctx, s, f, 1u)) return rc; }
+            }
         }
 #undef PBR_LAUNCH
         HIP_TRY(hipGetLastError());
     }
+    if (F.batch) ctx->batchFrames = F.n;
     HIP_TRY(hipEventRecord(ctx->ev1, s));
     if (!d->outputs_on_device) {
         if (rgb_out) HIP_TRY(hipMemcpyAsync(rgb_out, P.rgbOut, (size_t)npx * 12, hipMemcpyDeviceToHost, s));
@@ -2025,6 +2099,31 @@ int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, u
         stats->shading_events = hs[3];
         stats->n_launches = blocks > 0 ? 1 : 0;
     }
+    return PBR_OK;
+}
+
+int pbr_hip_render(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_out, uint8_t* rgba_out, pbr_render_stats* stats) {
+    return render_impl(ctx, d, rgb_out, rgba_out, stats, FrameSet{});
+}
+
+int pbr_hip_render_frames(pbr_hip_ctx* ctx, const pbr_render_desc* d, int n, float* const* rgb_outs, uint8_t* const* rgba_outs) {
+    if (!ctx) return PBR_E_INVALID;
+    if (n < 1) return set_err(ctx, PBR_E_INVALID, "render_frames: n must be >= 1");
+    FrameSet F;
+    F.n = n;
+    F.rgb = rgb_outs;
+    F.rgba = rgba_outs;
+    F.batch = true;
+    return render_impl(ctx, d, nullptr, nullptr, nullptr, F);
+}
+
+int pbr_hip_wait_frame(pbr_hip_ctx* ctx, void* stream, int f) {
+    if (!ctx) return PBR_E_INVALID;
+    if (f < 0 || f >= ctx->batchFrames) return set_err(ctx, PBR_E_INVALID, "wait_frame: no such frame in the last batch");
+    HIP_TRY(hipSetDevice(ctx->device));
+    const pbr_hip_ctx::FrameEv& e = ctx->frameEv[f];
+    for (int l = 0; l < kWfLanes; ++l)
+        if (e.used & (1u << l)) HIP_TRY(hipStreamWaitEvent(stream ? (hipStream_t)stream : ctx->stream, e.ev[l], 0));
     return PBR_OK;
 }
 
@@ -2071,7 +2170,7 @@ int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int*
     static const char* kNames[KP_COUNT] = {
         "k_wf_camera_extend", "k_wf_shade", "k_wf_shadow", "k_wf_extend", "k_wf_finish",
         "k_wfp_camera_extend", "k_wfp_shade", "k_wfp_shadow", "k_wfp_probe", "k_wfp_resolve", "k_wfp_finish",
-        "k_wfv_shade", "k_wfv_tr", "k_wfv_resolve", "k_render"};
+        "k_wfv_shade", "k_wfv_tr", "k_wfv_resolve", "k_render", "k_wf_shade_l0"};
     unsigned long long c[KP_COUNT][kProfFields];
     std::memset(c, 0, sizeof(c));
     if (ctx->profOn) HIP_TRY(hipMemcpy(c, ctx->dProf.p, sizeof(c), hipMemcpyDeviceToHost));
@@ -2093,14 +2192,15 @@ int pbr_hip_get_profile(pbr_hip_ctx* ctx, pbr_kernel_profile* out, int max, int*
         const unsigned long long* f = c[k];
         switch (k) {
         case KP_WF_CAMERA: return 52 * f[0];                                   // o, d, hit, index
-        case KP_WF_SHADE:   // ray + hit + index + recA + depth; shadow; next + recF/P
+        case KP_WF_SHADE: case KP_WF_SHADE0:   // ray + hit + index + recA + depth; shadow; next + recF/P
             // (f[6] level-0 samples of fused launches: those read no ray, hit or index; they write the
             // index, 4 B; f[7] shadow pushes carrying a SkyBox direction, 16 B)
             return 72 * f[0] - 48 * f[6] + 4 * f[5] + 52 * f[1] + 52 * f[4] + 16 * f[7];
         case KP_WF_SHADOW:   // o, d, contribution, id; recA RMW (f[2] of the visible: + the SkyBox direction)
             return 52 * f[0] + 32 * f[1] + 16 * f[2];
         case KP_WF_EXTEND: return 64 * f[0];                                   // o, d read; o, hit written
-        case KP_WF_FINISH: return 16 * f[0] + 4 * f[1] + 16 * c[KP_WF_SHADE][0] + 20 * c[KP_WF_SHADE][4];
+        case KP_WF_FINISH:
+            return 16 * f[0] + 4 * f[1] + 16 * (c[KP_WF_SHADE][0] + c[KP_WF_SHADE0][0]) + 20 * (c[KP_WF_SHADE][4] + c[KP_WF_SHADE0][4]);
         case KP_WFP_CAMERA: return 52 * f[0];                                  // o, d, hit, index
         // ray + hit + index (level 0) or id + carried state (queued); stL of the paths that end;
         // shadow, probe, direct record, continuation with its state

@@ -222,6 +222,21 @@ PBR_HD float scrambled_radical_inverse(uint32_t base, uint32_t recip, const uint
     }
     return mn(invBaseN * ((float)rev + invBase * (float)perm[0] / (1 - invBase)), kOneMinusEpsilon);
 }
+// the same with invBase = 1 / base and tail = invBase·perm[0] / (1 - invBase) formed by the caller
+// (per dimension, once: stage_halton_lds)
+PBR_HD float scrambled_radical_inverse_pre(uint32_t base, uint32_t recip, const uint16_t* perm, uint32_t a, float invBase,
+                                           float tail) {
+    uint64_t rev = 0;
+    float invBaseN = 1;
+    while (a) {
+        uint32_t next = div_prime(a, base, recip);
+        uint32_t digit = a - next * base;
+        rev = rev * base + perm[digit];
+        invBaseN *= invBase;
+        a = next;
+    }
+    return mn(invBaseN * ((float)rev + tail), kOneMinusEpsilon);
+}
 PBR_HD uint32_t reverse_bits32(uint32_t n) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return __brev(n);

@@ -38,22 +38,35 @@ def test_whitted_profile_counts_are_consistent(hip, fused):
     if fused == "0":
         cam = prof["k_wf_camera_extend"]
         assert cam["units"] == n and cam["launches"] == fin["launches"]
+        assert "k_wf_shade_l0" not in prof
+        shades = [shade]
+        assert shade["launches"] == fin["launches"] * rd.max_depth == shadow["launches"]
+        # shade's level-0 input is every sample; deeper levels read what the previous level pushed
+        assert shade["units"] == n + extend["units"]
     else:
+        # the fused level-0 launches (camera rays traced in the shade) are their own family
         assert "k_wf_camera_extend" not in prof
-    assert shade["launches"] == fin["launches"] * rd.max_depth == shadow["launches"]
-    # shade's level-0 input is every sample; deeper levels read what the previous level pushed
-    assert shade["units"] == n + extend["units"]
-    assert shadow["units"] == shade["counts"][1] and 0 < shadow["counts"][1] <= shadow["units"]
-    assert extend["units"] == shade["counts"][4] == shade["counts"][5]
+        l0 = prof["k_wf_shade_l0"]
+        shades = [l0, shade]
+        assert l0["launches"] == fin["launches"] and shade["launches"] == fin["launches"] * (rd.max_depth - 1)
+        assert l0["launches"] + shade["launches"] == shadow["launches"]
+        assert l0["units"] == n and shade["units"] == extend["units"]
+        assert l0["counts"][5] == 0
+    assert shadow["units"] == sum(v["counts"][1] for v in shades) and 0 < shadow["counts"][1] <= shadow["units"]
+    assert extend["units"] == sum(v["counts"][4] for v in shades) == sum(v["counts"][5] for v in shades)
     for v in prof.values():
         assert v["ms"] > 0 and v["bytes"] > 0
     # round 4 fields: f[6] = level-0 samples of fused launches (they read no queue entry), f[7] =
     # shadow pushes that carry a SkyBox direction (C2: every one), shadow f[2] = those that got
     # through (the sky lookup reads the direction); the byte formulas of pbr_kernels.hip
-    f = shade["counts"]
-    assert f[6] == (n if fused == "1" else 0)
-    assert f[7] == f[1] and shadow["counts"][2] == shadow["counts"][1]
-    assert shade["bytes"] == 72 * f[0] - 48 * f[6] + 4 * f[5] + 52 * f[1] + 52 * f[4] + 16 * f[7]
+    assert sum(v["counts"][6] for v in shades) == (n if fused == "1" else 0)
+    for v in shades:
+        f = v["counts"]
+        assert f[7] == f[1]
+        assert v["bytes"] == 72 * f[0] - 48 * f[6] + 4 * f[5] + 52 * f[1] + 52 * f[4] + 16 * f[7]
+    assert shadow["counts"][2] == shadow["counts"][1]
+    rec = sum(16 * v["counts"][0] + 20 * v["counts"][4] for v in shades)
+    assert fin["bytes"] == 16 * fin["counts"][0] + 4 * fin["counts"][1] + rec
     g2 = shadow["counts"]
     assert shadow["bytes"] == 52 * g2[0] + 32 * g2[1] + 16 * g2[2]
 

@@ -18,6 +18,8 @@ from pysicalbasedraytracer_amd import HipRenderer, capi, scenes  # noqa: E402
 def scene(kind, w, h, spp):
     if kind in ("c3", "c5"):   # the C3 / C5 scenes at a quarter of their raster
         return scenes.CONFIGS[kind.upper()](w // 2, h // 2, spp)
+    if kind == "c2":           # C2 as benchmarked (1920x1080, 64 spp)
+        return scenes.CONFIGS["C2"]()
     s = scenes.Scene()
     white = s.matte((0.8, 0.8, 0.8))
     recipes = {"glass": s.glass, "metal": s.metal, "plastic": s.plastic, "matte": lambda: s.matte((0.5, 0.5, 0.5))}
@@ -43,6 +45,7 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--libs", nargs="*", default=[None], help="library builds to compare (one context at a time)")
     ap.add_argument("--counters", action="store_true", help="profiling 2: work counters too (units)")
+    ap.add_argument("--frames", type=int, default=0, help="then time this many frames under the default schedule")
     ap.add_argument("kinds", nargs="*", default=["mixed", "glass", "metal", "plastic", "matte"])
     a = ap.parse_args()
     for lib in a.libs:
@@ -79,6 +82,27 @@ def run(a):
                 extra = " stack>6/10/16/24 " + "/".join(f"{c / max(1, v['units']):.4f}" for c in v["counts"][2:6])
             parts.append(f"{k.replace('k_', '')} {v['ms']:.1f} ms {v['units'] / 1e6:.1f} M {ns:.3f} ns/u{extra}")
         h = hashlib.sha256(rgb.cpu().numpy().tobytes()).hexdigest()[:16]
+        if a.frames:
+            r.set_schedule()
+            for _ in range(2):
+                r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(a.frames):
+                r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream, sync=False)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            timing = f"default {e0.elapsed_time(e1) / a.frames:.2f} ms/frame"
+            if hasattr(r.lib, "pbr_hip_render_frames"):   # the same frames as one batch (timing only)
+                r.render_frames(rd, [rgb.data_ptr()] * a.frames, [rgba.data_ptr()] * a.frames, stream=stream.cuda_stream)
+                torch.cuda.synchronize(dev)
+                e0.record(stream)
+                r.render_frames(rd, [rgb.data_ptr()] * a.frames, [rgba.data_ptr()] * a.frames, stream=stream.cuda_stream)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                timing += f", batch {e0.elapsed_time(e1) / a.frames:.2f}"
+            parts.insert(0, timing)
         print(f"{kind:8s} frame {h} " + " | ".join(parts), flush=True)
         r.close()
 

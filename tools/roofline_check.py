@@ -17,8 +17,17 @@ PEAK = 8000.0
 
 
 def family(name):
-    m = re.search(r"(k_\w+?)[<(]", name)
-    return m.group(1) if m else None
+    """bench.py's profile family of a rocprof kernel name (k_wf_shade's fused level-0 instances,
+    4th template argument true, are k_wf_shade_l0)."""
+    m = re.search(r"(k_\w+?)(<([^()]*)>)?\(", name)
+    if not m:
+        return None
+    fam = m.group(1)
+    if fam == "k_wf_shade" and m.group(3):
+        targs = [a.strip() for a in m.group(3).split(",")]
+        if len(targs) >= 4 and targs[3] == "true":
+            fam = "k_wf_shade_l0"
+    return fam
 
 
 def main():

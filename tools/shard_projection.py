@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--ns", default="2,4,8")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--batch", type=int, default=5, help="frames per pbr_hip_render_frames batch, as bench.py's "
+                                                         "timed window (0: one pbr_hip_render per frame)")
     a = ap.parse_args()
     scene, rd = scenes.CONFIGS[a.config]()
     W, H, spp = rd.camera.width, rd.camera.height, rd.spp
@@ -31,22 +33,27 @@ def main():
     r.upload(scene)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
-    rgb = torch.empty((W * H, 3), dtype=torch.float32, device=dev)
-    rgba = torch.empty((W * H, 4), dtype=torch.uint8, device=dev)
+    nb = max(1, a.batch)
+    rgbs = [torch.empty((W * H, 3), dtype=torch.float32, device=dev) for _ in range(nb)]
+    rgbas = [torch.empty((W * H, 4), dtype=torch.uint8, device=dev) for _ in range(nb)]
 
     def timed(desc):
-        r.render_device(desc, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)   # warm-up / tile upload
+        r.render_device(desc, rgbs[0].data_ptr(), rgbas[0].data_ptr(), stream=stream.cuda_stream)   # warm-up / tile upload
         torch.cuda.synchronize(dev)
         ms = []
         for _ in range(a.steps):
             t0 = time.perf_counter()
-            r.render_device(desc, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+            if a.batch > 0:   # bench.py's window: frames of one batch overlap on the lanes
+                r.render_frames(desc, [t.data_ptr() for t in rgbs], [t.data_ptr() for t in rgbas], stream=stream.cuda_stream)
+                r.sync()
+            else:
+                r.render_device(desc, rgbs[0].data_ptr(), rgbas[0].data_ptr(), stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
-            ms.append((time.perf_counter() - t0) * 1e3)
+            ms.append((time.perf_counter() - t0) * 1e3 / nb)
         return sorted(ms)[len(ms) // 2]
 
     full = timed(rd)
-    out = {"config": a.config, "raster": [W, H], "spp": spp, "tile": a.tile, "full_ms": round(full, 3),
+    out = {"config": a.config, "raster": [W, H], "spp": spp, "tile": a.tile, "full_ms": round(full, 3), "batch": a.batch,
            "build": capi.load_library().pbr_hip_build_info().decode(), "ranks": {}}
     print(f"{a.config} whole frame {full:.2f} ms", flush=True)
     for n in (int(x) for x in a.ns.split(",")):
