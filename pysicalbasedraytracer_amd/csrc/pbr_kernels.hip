@@ -1322,9 +1322,17 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, const FrameSet
     const dim3 gShadow = resident_grid(ctx, (const void*)k_wf_shadow<kShortStack>);
     const dim3 gShadowML = resident_grid(ctx, (const void*)k_wf_shadow_ml<kShortStack>);
     const dim3 gExtend = resident_grid(ctx, (const void*)k_wf_extend<kShortStack>);
-    if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
-    int chunk = 0;   // a batch: one rotation over the lanes through all its frames
+    // A batch of frames with fewer chunks than lanes (a rank's shard) continues one rotation over the
+    // lanes through all its frames; frames of more chunks fork and join per frame, as single frames do
+    // (C2, four chunks on three lanes: 15.65 ms per frame joined, 16.11 rotating).
+    const bool rotate = F.batch && nChunks < ch.lanes;
+    if (rotate) { if (int rc = wf_fork(ctx, s, ch.lanes)) return rc; }
+    int chunk = 0;
     for (int f = 0; f < F.n; ++f) {
+    if (!rotate) {
+        if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
+        chunk = 0;
+    }
     unsigned used = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
         const int l = chunk % ch.lanes;
@@ -1406,10 +1414,11 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, const FrameSet
         prof_host(ctx, KP_WF_FINISH, 0, (unsigned long long)W.chunkPix);
         prof_host(ctx, KP_WF_FINISH, 1, (unsigned long long)W.nSamples);
     }
-    if (F.batch) { if (int rc = wf_frame_done(ctx, s, f, used)) return rc; }
+    if (!rotate) { if (int rc = wf_join(ctx, s, ch.lanes)) return rc; }
+    if (F.batch) { if (int rc = wf_frame_done(ctx, s, f, rotate ? used : 1u)) return rc; }
     }
     HIP_TRY(hipGetLastError());
-    return wf_join(ctx, s, ch.lanes);
+    return rotate ? wf_join(ctx, s, ch.lanes) : PBR_OK;
 }
 
 // Wavefront Path: per bounce shade → shadow → probe → resolve → extend (pbr_wavefront_path.h).
@@ -1419,6 +1428,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
     // C3 2^25 349.4 ms, 2^26 336.1, 2^27 340.4; C5 2^25 1979 ms, 2^26 1939, 2^27 1919
     const WfChunks ch = wf_chunks(ctx->sched, P, 26, F.batch);
     const size_t cap = ch.cap, qcap = ch.qcap;
+    const long long nChunks = (P.nPixels + ch.chunkPix - 1) / ch.chunkPix;
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
     const bool micro = (lobes & ~kMicroLobes) == 0;   // Lambert + microfacet reflection/transmission (C4, C5)
@@ -1499,9 +1509,17 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
     // kMaxPassThrough crossings fails the render.
     const int maxLevels = std::max(1, P.maxDepth) + 1 + (ctx->host.anyNoMaterial ? 32 : 0);
     std::vector<int> segHost(kWfBlocks);
-    if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
-    int chunk = 0;   // a batch: one rotation over the lanes through all its frames
+    // A batch of frames with fewer chunks than lanes (a rank's shard) continues one rotation over the
+    // lanes through all its frames; frames of more chunks fork and join per frame, as single frames do
+    // (C2, four chunks on three lanes: 15.65 ms per frame joined, 16.11 rotating).
+    const bool rotate = F.batch && nChunks < ch.lanes;
+    if (rotate) { if (int rc = wf_fork(ctx, s, ch.lanes)) return rc; }
+    int chunk = 0;
     for (int f = 0; f < F.n; ++f) {
+    if (!rotate) {
+        if (int rc = wf_fork(ctx, s, ch.lanes)) return rc;
+        chunk = 0;
+    }
     unsigned used = 0;
     for (long long p0 = 0; p0 < P.nPixels; p0 += ch.chunkPix, ++chunk) {
         const int l = chunk % ch.lanes;
@@ -1583,10 +1601,11 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
         prof_host(ctx, KP_WFP_FINISH, 0, (unsigned long long)W.chunkPix);
         prof_host(ctx, KP_WFP_FINISH, 1, (unsigned long long)W.nSamples);
     }
-    if (F.batch) { if (int rc = wf_frame_done(ctx, s, f, used)) return rc; }
+    if (!rotate) { if (int rc = wf_join(ctx, s, ch.lanes)) return rc; }
+    if (F.batch) { if (int rc = wf_frame_done(ctx, s, f, rotate ? used : 1u)) return rc; }
     }
     HIP_TRY(hipGetLastError());
-    return wf_join(ctx, s, ch.lanes);
+    return rotate ? wf_join(ctx, s, ch.lanes) : PBR_OK;
 }
 
 // The integrator, sampler and scene parameters of a render descriptor (validated): shared by

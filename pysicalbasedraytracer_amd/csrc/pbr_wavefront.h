@@ -281,46 +281,17 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
         if (!have) continue;
         bool done = false;
         bool descend = false;
-        // One memory round trip per step for every lane: a lane at a leaf fetches its (first)
-        // primitive's 48 B, a lane at a quad node the node's 128 B, all issued before any lane waits.
-        // (As two branches, a wave holding lanes of both kinds — nearly every wave of incoherent rays —
-        // waited on two dependent fetches per step.)
-        float4 f0, f1, f2, f3, f4, f5, f6, f7;
-        const bool atLeaf = cur < 0;
-        {
-            const int ucur = __builtin_amdgcn_readfirstlane(cur);
-            if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {   // the wave at one place
-                if (atLeaf) {
-                    const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)(ucur & 0x7fffffff));
-                    f0 = as_f4(tv[0]); f1 = as_f4(tv[1]); f2 = as_f4(tv[2]);
-                } else {
-                    const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
-                    f0 = as_f4(w[0]); f1 = as_f4(w[1]); f2 = as_f4(w[2]); f3 = as_f4(w[3]); f4 = as_f4(w[4]);
-                    f5 = as_f4(w[5]); f6 = as_f4(w[6]); f7 = as_f4(w[7]);
-                }
-            } else {
-                const float4* src = atLeaf ? S.triVerts + 3 * (size_t)(cur & 0x7fffffff) : S.quad + 8 * (size_t)cur;
-                f0 = src[0]; f1 = src[1]; f2 = src[2];
-                if (!atLeaf) { f3 = src[3]; f4 = src[4]; f5 = src[5]; f6 = src[6]; f7 = src[7]; }
-            }
-        }
-        if (atLeaf) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
+        if (cur < 0) {   // leaf: its slots run up to the one flagged PRIM_LEAF_END
             int slot = cur & 0x7fffffff;
-            bool first = true;
             while (true) {
                 float4 v0, v1, v2;
-                if (first) {   // fetched above
-                    v0 = f0; v1 = f1; v2 = f2;
-                    first = false;
+                const int uslot = __builtin_amdgcn_readfirstlane(slot);
+                if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {
+                    const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
+                    v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
                 } else {
-                    const int uslot = __builtin_amdgcn_readfirstlane(slot);
-                    if (kScalarLoads && __builtin_amdgcn_ballot_w64(slot != uslot) == 0ull) {
-                        const ScalarF4Ptr tv = scalar_f4(S.triVerts + 3 * (size_t)uslot);
-                        v0 = as_f4(tv[0]); v1 = as_f4(tv[1]); v2 = as_f4(tv[2]);
-                    } else {
-                        const float4* tv = S.triVerts + 3 * (size_t)slot;
-                        v0 = tv[0]; v1 = tv[1]; v2 = tv[2];
-                    }
+                    const float4* tv = S.triVerts + 3 * (size_t)slot;
+                    v0 = tv[0]; v1 = tv[1]; v2 = tv[2];
                 }
                 const int flags = __float_as_int(v0.w);
                 float t, b0 = 0, b1 = 0, b2 = 0;
@@ -338,7 +309,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             }
         } else {
             QuadSlots q;
-            quad_slots_of<ANY>(f0, f1, f2, f3, f4, f5, f6, __float_as_int(f7.x), r, inv, n0, n1, n2, &q);
+            quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
             const float tM = r.tMax;
             const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
                        p3 = q.k[3] && q.t[3] < tM;

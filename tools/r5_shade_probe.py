@@ -57,7 +57,7 @@ def main():
 
 def run(a):
     dev = torch.device("cuda", 0)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)   # (not the default stream: its handle 0 means "the context's stream")
     rgb = torch.empty((a.w * a.h, 3), dtype=torch.float32, device=dev)
     rgba = torch.empty((a.w * a.h, 4), dtype=torch.uint8, device=dev)
     for kind in a.kinds:
