@@ -331,6 +331,8 @@ __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const 
 template <bool ANY>
 __device__ __forceinline__ void quad_slots_of(float4 LX, float4 LY, float4 LZ, float4 HX, float4 HY, float4 HZ, float4 R,
                                               int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q) {
+    // (The two-slot pairs written as packed fp32 — v_pk_add/v_pk_mul — measured slower: 8-9 more
+    // VGPRs, C4-material extend 119.5 → 129.0 ms; profiles/r5_slp_ab.log.)
     float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
     bool k0 = node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t0) & ((meta >> 8) & 1);
     bool k1 = node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t1) & ((meta >> 9) & 1);

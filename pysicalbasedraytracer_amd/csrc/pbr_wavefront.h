@@ -195,11 +195,13 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 // needs more registers per lane (at 7 the closest-hit loop spilled 19 VGPRs).  Measured (C3 / C5
 // ms per frame of the family, bit-identical): closest hit (extend) 7: 175 / 610, 6: 163 / 587,
 // 5: 155 / 584; any hit (shadow) 7: 107, 6: 126, 5: 122; transmittance (C5) 7: 546, 6: 518, 5: 582.
+// Round 5, built without the SLP vectorizer (62 VGPRs): any hit 8 — C4-material shadow 99.9 → 82.3
+// ms, C3 quarter 19.2 → 15.5 (profiles/r5_slp_ab.log).
 #ifndef PBR_REFILL_OCC
 #define PBR_REFILL_OCC 5
 #endif
 #ifndef PBR_REFILL_OCC_ANY
-#define PBR_REFILL_OCC_ANY 7
+#define PBR_REFILL_OCC_ANY 8
 #endif
 #ifndef PBR_REFILL_OCC_TR
 #define PBR_REFILL_OCC_TR 6
