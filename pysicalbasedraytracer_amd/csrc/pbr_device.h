@@ -248,8 +248,10 @@ __device__ __forceinline__ bool node_slab(f3 lo, f3 hi, const Ray& r, f3 inv, bo
 #ifndef PBR_SHORT_STACK_DEPTH
 #define PBR_SHORT_STACK_DEPTH 6
 #endif
+// Round 5, built without the SLP vectorizer (59-63 VGPRs): 8 — C2 shadow 3.5 → 3.0 ms per frame,
+// the frame 14.78 → 14.73 (profiles/r5_trav_occ_ab.log).
 #ifndef PBR_TRAV_OCC
-#define PBR_TRAV_OCC 7
+#define PBR_TRAV_OCC 8
 #endif
 constexpr int kShortStack = PBR_SHORT_STACK_DEPTH;
 __shared__ int s_trav_ref[kShortStack * 256];
