@@ -259,12 +259,21 @@ __shared__ float s_trav_t[kShortStack * 256];
 // A deeper LDS short stack for the kernels with LDS to spare: the closest-hit lane-refill kernels
 // (5 workgroups per CU) and the camera kernels (no segment scan).  C3 / C5 frame ms with the refill
 // kernels at 6 entries 276.6 / 1416, 10: 271.6 / 1386, 14 (4 workgroups per CU fit): 285.5 / 1403.
+// Round 5 (no SLP: 77 VGPRs, so 6 workgroups per CU fit in registers): 8 entries let 6 fit in LDS
+// too — C4-material extend 118.5 → 112.8 ms, C5 quarter 39.6 → 37.7 (profiles/r5_refill_short_ab.log).
 #ifndef PBR_REFILL_SHORT
-#define PBR_REFILL_SHORT 10
+#define PBR_REFILL_SHORT 8
 #endif
 constexpr int kRefillShort = PBR_REFILL_SHORT;
 __shared__ int s_trav_ref_r[kRefillShort * 256];
 __shared__ float s_trav_t_r[kRefillShort * 256];
+// The any-hit lane-refill kernels (shadow, transmittance) keep no entry distances, so the LDS of a
+// deeper stack costs them 4 B per entry and lane: PBR_ANY_SHORT 1 walks them with kRefillShort entries
+// (a stack diagnostic found 12% of C4-material shadow rays deeper than 6 entries, 0.6% deeper than 10).
+#ifndef PBR_ANY_SHORT
+#define PBR_ANY_SHORT 0
+#endif
+constexpr int kAnyShort = PBR_ANY_SHORT ? kRefillShort : kShortStack;
 // the LDS short stack of depth SHORT ([entry][lane]) for this thread
 template <int SHORT>
 __device__ __forceinline__ void trav_lds(int** ref, float** t) {

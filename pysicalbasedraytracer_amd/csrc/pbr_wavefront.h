@@ -196,9 +196,10 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
 // ms per frame of the family, bit-identical): closest hit (extend) 7: 175 / 610, 6: 163 / 587,
 // 5: 155 / 584; any hit (shadow) 7: 107, 6: 126, 5: 122; transmittance (C5) 7: 546, 6: 518, 5: 582.
 // Round 5, built without the SLP vectorizer (62 VGPRs): any hit 8 — C4-material shadow 99.9 → 82.3
-// ms, C3 quarter 19.2 → 15.5 (profiles/r5_slp_ab.log).
+// ms, C3 quarter 19.2 → 15.5 (profiles/r5_slp_ab.log); closest hit 6 with the 8-entry LDS stack
+// (kRefillShort).
 #ifndef PBR_REFILL_OCC
-#define PBR_REFILL_OCC 5
+#define PBR_REFILL_OCC 6
 #endif
 #ifndef PBR_REFILL_OCC_ANY
 #define PBR_REFILL_OCC_ANY 8

@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_ANY) void k_wfp_shadow(WfpParam
     const int n = seg_scan(W.shadowSeg);
     if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
         unsigned visible = 0;   // profile field 1, added once per wave at the end
-        traverse_stream<true, SHORT>(
+        traverse_stream<true, kAnyShort>(
             W.P.S, n,
             [&](int i, int* key) {
                 const int q = seg_pos(W.segCap, i);
