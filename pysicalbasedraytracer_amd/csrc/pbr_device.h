@@ -267,11 +267,13 @@ __shared__ float s_trav_t[kShortStack * 256];
 constexpr int kRefillShort = PBR_REFILL_SHORT;
 __shared__ int s_trav_ref_r[kRefillShort * 256];
 __shared__ float s_trav_t_r[kRefillShort * 256];
-// The any-hit lane-refill kernels (shadow, transmittance) keep no entry distances, so the LDS of a
-// deeper stack costs them 4 B per entry and lane: PBR_ANY_SHORT 1 walks them with kRefillShort entries
-// (a stack diagnostic found 12% of C4-material shadow rays deeper than 6 entries, 0.6% deeper than 10).
+// The Path shadow kernel's any-hit walk keeps no entry distances, so a deeper LDS stack costs it 4 B
+// per entry and lane: it walks with kRefillShort entries (a stack diagnostic found 12% of C4-material
+// shadow rays deeper than 6 entries, 0.6% deeper than 10).  C4-material shadow 82.2 → 78.7 ms, frame
+// 339.4 → 336.3 (profiles/r5_any_short_ab.log).  VolPath's transmittance kernel keeps 6: its other
+// walk stores distances, and both stacks in LDS would cost it a workgroup per CU.
 #ifndef PBR_ANY_SHORT
-#define PBR_ANY_SHORT 0
+#define PBR_ANY_SHORT 1
 #endif
 constexpr int kAnyShort = PBR_ANY_SHORT ? kRefillShort : kShortStack;
 // the LDS short stack of depth SHORT ([entry][lane]) for this thread

@@ -22,7 +22,11 @@
 #pragma once
 
 constexpr int kWfMaxDepth = 16;   // Whitted levels of the wavefront schedule (deeper: the megakernel)
-constexpr int kWfBlocks = 2048;   // workgroups of the queue kernels = segments of a queue
+#ifndef PBR_WF_BLOCKS
+#define PBR_WF_BLOCKS 2048
+#endif
+constexpr int kWfBlocks = PBR_WF_BLOCKS;   // workgroups of the queue kernels = segments of a queue
+static_assert(kWfBlocks % 256 == 0, "the segment scan reads kWfBlocks / 256 counts per thread");
 
 // Per-kernel profile (pbr_hip_set_profiling): kernel families and their work counters
 // [kind * kProfFields + field].  Field 0 counts the units a family processed, fields 1..4 the

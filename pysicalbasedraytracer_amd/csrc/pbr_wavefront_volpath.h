@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_TR) void k_wfv_tr(WfvParams V) 
     const int n = seg_scan(V.trSeg);
     if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
         if (V.anyHitTr) {   // the walk is one any-hit query (below): lane-refill traversal
-            traverse_stream<true, kAnyShort>(
+            traverse_stream<true, SHORT>(   // (not kAnyShort: see pbr_device.h)
                 S, n,
                 [&](int i, int* key) {
                     const int q = seg_pos(X.W.segCap, i);
