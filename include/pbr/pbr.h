@@ -667,20 +667,25 @@ class GlobalSampler : public Sampler {
     // Extensions: batched forms (defaults: one call each; the device samplers answer a whole batch
     // with one query), the current interval sample index, the number of dimensions the sampler has
     int CurrentDimension() const override { return dimension; }
-    int64_t CurrentIndex() const { return intervalSampleIndex; }
+    int64_t CurrentIndex() const;
     virtual void SampleDimensions(int64_t index, int firstDim, int n, float* out) const;
     virtual void GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const;
+    // dimensions [firstDim, firstDim + n) of `count` indices, index-major (default: SampleDimensions
+    // per index; the device samplers answer it with one query)
+    virtual void SampleDimensionsOf(const int64_t* index, int count, int firstDim, int n, float* out) const;
     virtual int MaxDimensions() const { return 1 << 30; }
     // the value of dimension `dim` for sample `sampleNum` of the current pixel, and a batch of them
     float SampleValue(int64_t sampleNum, int dim) const;
     void SampleValues(const std::vector<int64_t>& sampleNums, const std::vector<int>& dims, float* out) const;
     static constexpr int kValueBlock = 32;
 
-  protected:
-    int64_t intervalSampleIndex = 0;
-
   private:
     float value(int dim);
+    int64_t indexOf(int64_t sampleNum) const;   // the pixel's indices, fetched once in StartPixel
+    std::vector<int64_t> pixelIndex;
+    int64_t intervalSample = 0;                 // the current sample number; its index on first use
+    mutable int64_t intervalSampleIndex = 0;
+    mutable bool intervalKnown = false;
     int dimension = 0;
     static const int arrayStartDim = 5;
     int arrayEndDim = 5;
@@ -695,6 +700,7 @@ class HaltonSampler : public GlobalSampler {   // Sampler/Halton.h
     float SampleDimension(int64_t index, int dimension) const override;   // Halton.cpp:83-92, on the device
     void SampleDimensions(int64_t index, int firstDim, int n, float* out) const override;
     void GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const override;
+    void SampleDimensionsOf(const int64_t* index, int count, int firstDim, int n, float* out) const override;
     int DeviceSampler() const override;
     Point2i SampleRaster() const override;
     int MaxDimensions() const override { return 1000; }   // PrimeTableSize
@@ -712,6 +718,7 @@ class SobolSampler : public GlobalSampler {
     float SampleDimension(int64_t index, int dimension) const override;   // pbrt-v3 sobol.cpp, on the device
     void SampleDimensions(int64_t index, int firstDim, int n, float* out) const override;
     void GetIndicesForSamples(int64_t firstSample, int n, int64_t* out) const override;
+    void SampleDimensionsOf(const int64_t* index, int count, int firstDim, int n, float* out) const override;
     int DeviceSampler() const override;
     Point2i SampleRaster() const override;
     int MaxDimensions() const override { return 1024; }   // NumSobolDimensions

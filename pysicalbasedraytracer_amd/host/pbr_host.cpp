@@ -650,12 +650,30 @@ float GlobalSampler::SampleValue(int64_t sampleNum, int dim) const {
     SampleDimensions(GetIndexForSample(sampleNum), dim, 1, &v);
     return v;
 }
+void GlobalSampler::SampleDimensionsOf(const int64_t* index, int count, int firstDim, int n, float* out) const {
+    for (int k = 0; k < count; ++k) SampleDimensions(index[k], firstDim, n, out + (size_t)k * n);
+}
+// GetIndexForSample is a pure function of the pixel and the sample number (Sampler.h:69), so the
+// pixel's spp indices are fetched once, in StartPixel (one device query for the device samplers),
+// and a sample's index is looked up when its first value is (the reference computes it in
+// StartNextSample, including the unused one past the last sample).
+int64_t GlobalSampler::indexOf(int64_t sampleNum) const {
+    if (sampleNum >= 0 && sampleNum < (int64_t)pixelIndex.size()) return pixelIndex[(size_t)sampleNum];
+    return GetIndexForSample(sampleNum);
+}
+int64_t GlobalSampler::CurrentIndex() const {
+    if (!intervalKnown) {
+        intervalSampleIndex = indexOf(intervalSample);
+        intervalKnown = true;
+    }
+    return intervalSampleIndex;
+}
 // SampleDimension(intervalSampleIndex, dim) through a block cache: a device sampler answers the
 // block with one query
 float GlobalSampler::value(int dim) {
     if (cacheBase < 0 || dim < cacheBase || dim >= cacheBase + kValueBlock) {
         const int n = std::max(1, std::min(kValueBlock, MaxDimensions() - dim));
-        SampleDimensions(intervalSampleIndex, dim, n, cache);
+        SampleDimensions(CurrentIndex(), dim, n, cache);
         cacheBase = dim;
     }
     return cache[dim - cacheBase];
@@ -664,37 +682,40 @@ void GlobalSampler::StartPixel(const Point2i& p) {
     Sampler::StartPixel(p);
     dimension = 0;
     cacheBase = -1;
-    intervalSampleIndex = GetIndexForSample(0);
+    pixelIndex.assign((size_t)samplesPerPixel, 0);
+    GetIndicesForSamples(0, (int)samplesPerPixel, pixelIndex.data());
+    intervalSample = 0;
+    intervalKnown = false;
     arrayEndDim = arrayStartDim + (int)sampleArray1D.size() + 2 * (int)sampleArray2D.size();
-    // the arrays of every sample of the pixel (Sampler.cpp:103-122)
+    // the arrays of every sample of the pixel (Sampler.cpp:103-122): one batch per array
     for (size_t i = 0; i < samples1DArraySizes.size(); ++i) {
         const int nSamples = samples1DArraySizes[i] * (int)samplesPerPixel;
         std::vector<int64_t> idx(nSamples);
         GetIndicesForSamples(0, nSamples, idx.data());
-        for (int j = 0; j < nSamples; ++j) SampleDimensions(idx[j], arrayStartDim + (int)i, 1, &sampleArray1D[i][j]);
+        SampleDimensionsOf(idx.data(), nSamples, arrayStartDim + (int)i, 1, sampleArray1D[i].data());
     }
     int dim = arrayStartDim + (int)samples1DArraySizes.size();
     for (size_t i = 0; i < samples2DArraySizes.size(); ++i, dim += 2) {
         const int nSamples = samples2DArraySizes[i] * (int)samplesPerPixel;
         std::vector<int64_t> idx(nSamples);
         GetIndicesForSamples(0, nSamples, idx.data());
-        for (int j = 0; j < nSamples; ++j) {
-            float v[2];
-            SampleDimensions(idx[j], dim, 2, v);
-            sampleArray2D[i][j] = Point2f(v[0], v[1]);
-        }
+        std::vector<float> v(2 * (size_t)nSamples);
+        SampleDimensionsOf(idx.data(), nSamples, dim, 2, v.data());
+        for (int j = 0; j < nSamples; ++j) sampleArray2D[i][j] = Point2f(v[2 * j], v[2 * j + 1]);
     }
 }
 bool GlobalSampler::StartNextSample() {
     dimension = 0;
     cacheBase = -1;
-    intervalSampleIndex = GetIndexForSample(currentPixelSampleIndex + 1);
+    intervalSample = currentPixelSampleIndex + 1;
+    intervalKnown = false;
     return Sampler::StartNextSample();
 }
 bool GlobalSampler::SetSampleNumber(int64_t sampleNum) {
     dimension = 0;
     cacheBase = -1;
-    intervalSampleIndex = GetIndexForSample(sampleNum);
+    intervalSample = sampleNum;
+    intervalKnown = false;
     return Sampler::SetSampleNumber(sampleNum);
 }
 float GlobalSampler::Get1D() {
@@ -730,6 +751,23 @@ void device_dimensions(int type, Point2i raster, const Point2i& pixel, int64_t i
     pbr_hip_ctx* h = helper_ctx();
     check(h, pbr_hip_sample_dimensions(h, type, raster.x, raster.y, n, idx.data(), q.data(), out), "pbr_hip_sample_dimensions");
 }
+// dimensions [first, first + n) of `count` indices in one query (index-major)
+void device_dimensions_of(int type, Point2i raster, const Point2i& pixel, const int64_t* index, int count, int first, int n,
+                          int maxDims, float* out) {
+    if (count <= 0 || n <= 0) return;
+    if (first < 0 || first + n > maxDims) throw std::out_of_range("sampler dimension beyond the sampler's tables");
+    const size_t m = (size_t)count * n;
+    std::vector<int64_t> idx(m);
+    std::vector<int32_t> q(3 * m);
+    for (int k = 0; k < count; ++k)
+        for (int d = 0; d < n; ++d) {
+            const size_t e = (size_t)k * n + d;
+            idx[e] = index[k];
+            q[3 * e] = pixel.x; q[3 * e + 1] = pixel.y; q[3 * e + 2] = first + d;
+        }
+    pbr_hip_ctx* h = helper_ctx();
+    check(h, pbr_hip_sample_dimensions(h, type, raster.x, raster.y, (int)m, idx.data(), q.data(), out), "pbr_hip_sample_dimensions");
+}
 }  // namespace
 int64_t HaltonSampler::GetIndexForSample(int64_t sampleNum) const {
     int64_t v = 0;
@@ -747,6 +785,9 @@ float HaltonSampler::SampleDimension(int64_t index, int dimension) const {
 void HaltonSampler::SampleDimensions(int64_t index, int firstDim, int n, float* out) const {
     device_dimensions(PBR_SAMPLER_HALTON, SampleRaster(), currentPixel, index, firstDim, n, MaxDimensions(), out);
 }
+void HaltonSampler::SampleDimensionsOf(const int64_t* index, int count, int firstDim, int n, float* out) const {
+    device_dimensions_of(PBR_SAMPLER_HALTON, SampleRaster(), currentPixel, index, count, firstDim, n, MaxDimensions(), out);
+}
 int64_t SobolSampler::GetIndexForSample(int64_t sampleNum) const {
     int64_t v = 0;
     device_indices(PBR_SAMPLER_SOBOL, SampleRaster(), samplesPerPixel, currentPixel, sampleNum, 1, &v);
@@ -762,6 +803,9 @@ float SobolSampler::SampleDimension(int64_t index, int dimension) const {
 }
 void SobolSampler::SampleDimensions(int64_t index, int firstDim, int n, float* out) const {
     device_dimensions(PBR_SAMPLER_SOBOL, SampleRaster(), currentPixel, index, firstDim, n, MaxDimensions(), out);
+}
+void SobolSampler::SampleDimensionsOf(const int64_t* index, int count, int firstDim, int n, float* out) const {
+    device_dimensions_of(PBR_SAMPLER_SOBOL, SampleRaster(), currentPixel, index, count, firstDim, n, MaxDimensions(), out);
 }
 
 // ============================================================================ flattening
