@@ -184,15 +184,24 @@ PBR_HD f3 offset_ray_origin(f3 p, f3 pError, f3 n, f3 w) {
 // ---------------------------------------------------------------- Halton (Sampler/Halton.cpp)
 // Exact 32-bit division by a runtime prime: approximate quotient from a 32-bit reciprocal,
 // corrected by at most two steps. Valid for every 32-bit numerator.
-PBR_HD uint32_t div_prime(uint32_t n, uint32_t d, uint32_t recip /* floor(2^32/d) */) {
+// recip <= 2^32/d makes the estimate at most floor(n/d) and n·recip/2^32 > n/d − 1 at least
+// floor(n/d) − 1, so one conditional step corrects it (and the remainder, the digit, comes with it).
+PBR_HD uint32_t divrem_prime(uint32_t n, uint32_t d, uint32_t recip /* floor(2^32/d) */, uint32_t* rem) {
 #if defined(__HIP_DEVICE_COMPILE__)
     uint32_t q = __umulhi(n, recip);
 #else
     uint32_t q = (uint32_t)(((uint64_t)n * recip) >> 32);
 #endif
     uint32_t r = n - q * d;
-    while (r >= d) { ++q; r -= d; }
+    const bool c = r >= d;
+    q += c ? 1u : 0u;
+    r -= c ? d : 0u;
+    *rem = r;
     return q;
+}
+PBR_HD uint32_t div_prime(uint32_t n, uint32_t d, uint32_t recip /* floor(2^32/d) */) {
+    uint32_t r;
+    return divrem_prime(n, d, recip, &r);
 }
 // LowDiscrepancy.cpp:212-225 RadicalInverseSpecialized<base> (64-bit digit accumulator)
 PBR_HD float radical_inverse_b(uint32_t base, uint32_t recip, uint32_t a) {
@@ -224,16 +233,24 @@ PBR_HD float scrambled_radical_inverse(uint32_t base, uint32_t recip, const uint
 }
 // the same with invBase = 1 / base and tail = invBase·perm[0] / (1 - invBase) formed by the caller
 // (per dimension, once: stage_halton_lds)
+// Two digits per step while two remain: both permutation lookups are issued together (they are
+// independent), rev gets the same integer and invBaseN the same sequence of products.
 PBR_HD float scrambled_radical_inverse_pre(uint32_t base, uint32_t recip, const uint16_t* perm, uint32_t a, float invBase,
                                            float tail) {
     uint64_t rev = 0;
     float invBaseN = 1;
-    while (a) {
-        uint32_t next = div_prime(a, base, recip);
-        uint32_t digit = a - next * base;
-        rev = rev * base + perm[digit];
+    while (a >= base) {
+        uint32_t d0, d1;
+        const uint32_t a1 = divrem_prime(a, base, recip, &d0);
+        a = divrem_prime(a1, base, recip, &d1);
+        const uint32_t p0 = perm[d0], p1 = perm[d1];
+        rev = (rev * base + p0) * base + p1;
         invBaseN *= invBase;
-        a = next;
+        invBaseN *= invBase;
+    }
+    if (a) {   // the last digit is a itself
+        rev = rev * base + perm[a];
+        invBaseN *= invBase;
     }
     return mn(invBaseN * ((float)rev + tail), kOneMinusEpsilon);
 }
