@@ -15,7 +15,7 @@
     defined(PBR_REFILL_OCC) || defined(PBR_REFILL_OCC_ANY) || defined(PBR_REFILL_OCC_TR) ||                          \
     defined(PBR_CAMERA_SHORT) || defined(PBR_WF_SHADE_OCC) || defined(PBR_WF_SHADE_OCC_MM) ||                        \
     defined(PBR_WF_FUSED_OCC) || defined(PBR_WFP_OCC) || defined(PBR_WFV_OCC) || defined(PBR_LANES_DEFAULT) ||       \
-    defined(PBR_INLINE_TRANS) || defined(PBR_DIAG_SHADE) || defined(PBR_STACK_DIAG) || defined(PBR_ANY_SHORT) || defined(PBR_WF_BLOCKS)
+    defined(PBR_INLINE_TRANS) || defined(PBR_DIAG_SHADE) || defined(PBR_STACK_DIAG) || defined(PBR_ANY_SHORT) || defined(PBR_WF_BLOCKS) || defined(PBR_CLASSED_SHADE)
 #error "tuning switches are development builds only: add -DPBR_DEV_KNOBS=1"
 #endif
 #endif
@@ -28,4 +28,9 @@
 // deeper than 6 / 10 / 16 / 24 entries into profile fields 2-5 of their family.
 #ifndef PBR_STACK_DIAG
 #define PBR_STACK_DIAG 0
+#endif
+// Path: one shade launch per material lobe set when the scene's materials have several (k_wfp_shade
+// CLASSED)
+#ifndef PBR_CLASSED_SHADE
+#define PBR_CLASSED_SHADE 1
 #endif

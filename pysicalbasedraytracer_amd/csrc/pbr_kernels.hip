@@ -865,6 +865,8 @@ struct pbr_hip_ctx {
     DevBuf dTiles, dTileStart, dRgb, dRgba, dStats, dScratchIn, dScratchOut;
     DevBuf dTable;                       // PBR_SAMPLER_TABLE values of the current frame
     std::vector<int32_t> tilesHost;      // what dTiles / dTileStart hold (re-uploaded on change only)
+    DevBuf dMatPass;                     // the classed Path shade: each material's pass
+    std::vector<int32_t> matPassHost;
     std::vector<long long> startsHost;
     hipStream_t lastStream = nullptr;    // stream of the last asynchronous render (may still run)
     bool inFlight = false;
@@ -1437,6 +1439,40 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
     const bool mm = (lobes & ~kMatteMirrorLobes) == 0;   // Lambert + mirror only (C3)
     const bool textured = (lobes & kTexturedLobes) != 0;
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats;   // templates staged in LDS
+    // The classed Path shade (k_wfp_shade CLASSED): with materials of several lobe sets (C4's glass,
+    // metal, plastic and matte), one launch per lobe set shades that set's hits with a kernel
+    // compiled for it.  A material goes to the first of these sets that holds its lobes; misses and
+    // material-less hits to pass 0.
+    static constexpr int kPassLobes[] = {1 << L_LAMBERT, 1 << L_MF_R, (1 << L_LAMBERT) | (1 << L_MF_R),
+                                         (1 << L_MF_R) | (1 << L_MF_T), kMicroLobes};
+    std::vector<int> passKind;                                   // pass → kPassLobes index
+    std::vector<int32_t> matPass(ctx->host.materials.size() / 2, 0);
+    if (PBR_CLASSED_SHADE && !vol && !textured && matsLds && halton && micro) {
+        std::vector<int> kindOf(matPass.size(), -1);
+        for (size_t m = 0; m < matPass.size(); ++m) {
+            const MatTemplate& mt = ctx->host.materials[2 * m + 1];   // the Path/VolPath lobes (make_bsdf)
+            if (!mt.valid) continue;
+            int mask = 0;
+            for (int i = 0; i < mt.nLobes; ++i) mask |= 1 << mt.lobes[i].kind;
+            for (int k = 0; k < 5; ++k)
+                if ((mask & ~kPassLobes[k]) == 0) { kindOf[m] = k; break; }
+        }
+        for (int k = 0; k < 5; ++k)
+            for (size_t m = 0; m < matPass.size(); ++m)
+                if (kindOf[m] == k) {
+                    for (size_t j = 0; j < matPass.size(); ++j)
+                        if (kindOf[j] == k) matPass[j] = (int32_t)passKind.size();
+                    passKind.push_back(k);
+                    break;
+                }
+        if (passKind.size() < 2) passKind.clear();
+    }
+    const bool classed = !passKind.empty();
+    if (classed && matPass != ctx->matPassHost) {
+        HIP_TRY(hipStreamSynchronize(s));   // an earlier async copy may still read the host copy
+        ctx->matPassHost = matPass;
+        HIP_TRY(ctx->dMatPass.upload(ctx->matPassHost, s));
+    }
     // (the level-0 shade tracing its own camera rays, as Whitted's does, measured slower here: C3
     // 254 → 268-271 ms, C4 6575 → 6702 ms at 3 shading waves per SIMD; profiles/r3_fused_ab.log)
     WfvParams VL[kWfLanes];
@@ -1462,6 +1498,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
         std::memset(&V, 0, sizeof(V));
         WfpParams& X = V.X;
         WfParams& W = X.W;
+        X.matPass = classed ? (const int*)ctx->dMatPass.p : nullptr;
         if (vol) {
             V.anyHitTr = ctx->host.anyNoMaterial ? 0 : 1;
             HIP_TRY(B.wtO.ensure(qcap * 16)); HIP_TRY(B.wtD.ensure(qcap * 16)); HIP_TRY(B.wtP.ensure(qcap * 16));
@@ -1554,17 +1591,29 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
                     else if (micro && matsLds) hipLaunchKernelGGL((k_wfv_shade<kMicroLobes, true>), gshade, blk, 0, st, V, l0);
                     else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0);
                     else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0));
+            } else if (classed) {   // one launch per material pass, each compiled for its lobes
+                for (int p = 0; p < (int)passKind.size(); ++p) {
+                    constexpr int H = PBR_SAMPLER_HALTON, O = PBR_WFP_OCC;
+                    PROF_LAUNCH(KP_WFP_SHADE, st,
+                        switch (passKind[p]) {
+                        case 0: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[0], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
+                        case 1: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[1], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
+                        case 2: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[2], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
+                        case 3: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[3], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
+                        default: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[4], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
+                        });
+                }
             } else {
                 PROF_LAUNCH(KP_WFP_SHADE, st,
-                    if (textured) hipLaunchKernelGGL((k_wfp_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, X, l0);
-                    else if (mm && matsLds && sobol) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true, PBR_WFP_OCC, PBR_SAMPLER_SOBOL>), gshade, blk, 0, st, X, l0);
-                    else if (mm && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true>), gshade, blk, 0, st, X, l0);
-                    else if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0);
-                    else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0);
-                    else if (micro && matsLds && halton) hipLaunchKernelGGL((k_wfp_shade<kMicroLobes, true, PBR_WFP_OCC, PBR_SAMPLER_HALTON>), gshade, blk, 0, st, X, l0);
-                    else if (micro && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMicroLobes, true>), gshade, blk, 0, st, X, l0);
-                    else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, st, X, l0);
-                    else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, st, X, l0));
+                    if (textured) hipLaunchKernelGGL((k_wfp_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, X, l0, 0);
+                    else if (mm && matsLds && sobol) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true, PBR_WFP_OCC, PBR_SAMPLER_SOBOL>), gshade, blk, 0, st, X, l0, 0);
+                    else if (mm && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true>), gshade, blk, 0, st, X, l0, 0);
+                    else if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0, 0);
+                    else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0, 0);
+                    else if (micro && matsLds && halton) hipLaunchKernelGGL((k_wfp_shade<kMicroLobes, true, PBR_WFP_OCC, PBR_SAMPLER_HALTON>), gshade, blk, 0, st, X, l0, 0);
+                    else if (micro && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMicroLobes, true>), gshade, blk, 0, st, X, l0, 0);
+                    else if (matsLds) hipLaunchKernelGGL((k_wfp_shade<kAllLobes, true>), gshade, blk, 0, st, X, l0, 0);
+                    else hipLaunchKernelGGL((k_wfp_shade<kAllLobes, false>), gshade, blk, 0, st, X, l0, 0));
             }
             if (l0) prof_host(ctx, kShade, 0, (unsigned long long)W.nSamples);
             if (int rc = prof_sums(ctx, st, kShade, {l0 ? nullptr : W.cur.segCount, vol ? V.trSeg : W.shadowSeg, X.probeSeg,

@@ -42,7 +42,16 @@ struct WfpParams {
     int* dTgt;             // where the path's L is when the estimate resolves: the continuation's
                            // position in the next queue, or ~id (stL[id]) when the path ended
     int lastLevel;         // this shade is the schedule's last: a continuation ends the path instead
+    const int* matPass;    // the classed shade (CLASSED): the pass that shades each material's hits
 };
+
+// The material pass of a queued hit (the classed shade): misses and material-less hits go to pass 0.
+__device__ __forceinline__ int entry_pass(const WfpParams& X, int q) {
+    const int slot = __float_as_int(X.W.cur.hit[q].x);
+    if (slot < 0) return 0;
+    const int mat = X.W.P.S.primInfo[slot].y;
+    return mat < 0 ? 0 : X.matPass[mat];
+}
 
 __device__ __forceinline__ int pack_path(int dim, int bounces, bool specular) {
     return (dim & 0xffff) | ((bounces & 0x7f) << 16) | (specular ? (1 << 23) : 0);
@@ -90,9 +99,15 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
 #define PBR_WFP_OCC 3
 #endif
 // SMP: the frame's sampler type when the launch knows it (the other samplers' code — and the kernel
-// parameters it reads, which otherwise spill from SGPRs into VGPR lanes — is compiled out), else -1
-template <int LOBES, bool MATS_LDS, int OCC = PBR_WFP_OCC, int SMP = -1>
-__global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0) {
+// parameters it reads, which otherwise spill from SGPRs into VGPR lanes — is compiled out), else -1.
+// CLASSED: one of several launches per bounce, each shading the hits of the materials whose lobe set
+// it is compiled for (X.matPass, pass `pass`): the workgroup walks its queue entries as before,
+// gathers those of its pass into an LDS ring, and shades them 256 at a time, so every wave runs one
+// material class with that class's registers.  Pushes continue the segment counts of the pass before.
+// Entries land in the queues in another order, which nothing depends on (records are indexed by
+// sample or by queue position, and every L update keeps its order: pbr_wavefront_path.h header).
+template <int LOBES, bool MATS_LDS, int OCC = PBR_WFP_OCC, int SMP = -1, bool CLASSED = false>
+__global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0, int pass) {
     WfParams& W = X.W;
     const KParams& P = W.P;
     const DeviceScene& S = P.S;
@@ -107,16 +122,21 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
         mats = s_mats;
     }
     __shared__ int s_push[4];   // shadow, probe, direct, next
-    if (threadIdx.x < 4) s_push[threadIdx.x] = 0;
+    if (threadIdx.x < 4) {
+        int v = 0;   // (a later pass of the classed shade continues the segments)
+        if (CLASSED && pass > 0) {
+            const int b = wf_block();
+            v = threadIdx.x == 0 ? W.shadowSeg[b] : threadIdx.x == 1 ? X.probeSeg[b] : threadIdx.x == 2 ? X.directSeg[b] : W.next.segCount[b];
+        }
+        s_push[threadIdx.x] = v;
+    }
     __syncthreads();
     const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;
     const int base = wf_block() * W.segCap;
-    for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
-        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-        const bool active = i < n;
-        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
+    // one queued ray; every lane of the workgroup calls it together (wave_push needs convergent lanes)
+    auto shade = [&](const bool active, const int q) {
         // Two phases around the light-estimate pushes: the estimate's record, shadow and probe rays
         // are written as soon as they exist, so their registers are free during the path's BSDF
         // sample; only the record's target (the continuation's position) is written at the end.
@@ -322,6 +342,43 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0)
             W.next.s1[ni] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
         }
         if (pushDirect) X.dTgt[di] = pushNext ? ni : ~id;
+    };
+    if constexpr (!CLASSED) {
+        for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
+            const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
+            const bool active = i < n;
+            shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
+        }
+    } else {
+        // ring of queue positions of this pass: appended per iteration (at most 256), shaded 256 at a
+        // time once that many are pending, so fewer than 256 wait and 512 slots never overrun
+        __shared__ int s_ring[512];
+        __shared__ int s_tail;
+        if (threadIdx.x == 0) s_tail = 0;
+        __syncthreads();
+        int head = 0;   // workgroup-uniform
+        for (int it = 0; it < nIter; ++it) {
+            const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
+            const int q = i < n ? (level0 ? i : seg_pos(W.segCap, i)) : 0;
+            const bool mine = i < n && entry_pass(X, q) == pass;
+            const int at = wave_push(&s_tail, mine);
+            if (mine) s_ring[at & 511] = q;
+            __syncthreads();
+            const bool full = s_tail - head >= 256;   // (the same for every lane: no append until the barrier below)
+            const int qq = full ? s_ring[(head + threadIdx.x) & 511] : 0;
+            __syncthreads();   // the counter and the entries are read before any wave appends again
+            if (full) {
+                shade(true, qq);
+                head += 256;
+            }
+        }
+        __syncthreads();
+        const int tail = s_tail;
+        if (head < tail) {
+            const bool active = head + (int)threadIdx.x < tail;
+            const int qq = active ? s_ring[(head + threadIdx.x) & 511] : 0;
+            shade(active, qq);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
