@@ -1596,7 +1596,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
                     constexpr int H = PBR_SAMPLER_HALTON, O = PBR_WFP_OCC;
                     PROF_LAUNCH(KP_WFP_SHADE, st,
                         switch (passKind[p]) {
-                        case 0: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[0], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
+                        case 0: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[0], true, PBR_WFP_OCC_L, H, true>), gshade, blk, 0, st, X, l0, p); break;
                         case 1: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[1], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
                         case 2: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[2], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
                         case 3: hipLaunchKernelGGL((k_wfp_shade<kPassLobes[3], true, O, H, true>), gshade, blk, 0, st, X, l0, p); break;
@@ -1606,7 +1606,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
             } else {
                 PROF_LAUNCH(KP_WFP_SHADE, st,
                     if (textured) hipLaunchKernelGGL((k_wfp_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, X, l0, 0);
-                    else if (mm && matsLds && sobol) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true, PBR_WFP_OCC, PBR_SAMPLER_SOBOL>), gshade, blk, 0, st, X, l0, 0);
+                    else if (mm && matsLds && sobol) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true, PBR_WFP_OCC_MM, PBR_SAMPLER_SOBOL>), gshade, blk, 0, st, X, l0, 0);
                     else if (mm && matsLds) hipLaunchKernelGGL((k_wfp_shade<kMatteMirrorLobes, true>), gshade, blk, 0, st, X, l0, 0);
                     else if (simple && matsLds) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, true>), gshade, blk, 0, st, X, l0, 0);
                     else if (simple) hipLaunchKernelGGL((k_wfp_shade<kSimpleLobes, false>), gshade, blk, 0, st, X, l0, 0);

@@ -98,6 +98,13 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
 #ifndef PBR_WFP_OCC
 #define PBR_WFP_OCC 3
 #endif
+// the Lambert + mirror kernel on Sobol frames (C3) and the classed shade's Lambert pass
+#ifndef PBR_WFP_OCC_MM
+#define PBR_WFP_OCC_MM PBR_WFP_OCC
+#endif
+#ifndef PBR_WFP_OCC_L
+#define PBR_WFP_OCC_L PBR_WFP_OCC
+#endif
 // SMP: the frame's sampler type when the launch knows it (the other samplers' code — and the kernel
 // parameters it reads, which otherwise spill from SGPRs into VGPR lanes — is compiled out), else -1.
 // CLASSED: one of several launches per bounce, each shading the hits of the materials whose lobe set

@@ -63,10 +63,10 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;
     const int base = wf_block() * W.segCap;
-    for (int it = 0; it < nIter; ++it) {
-        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-        const bool active = i < n;
-        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
+    // one queued ray; every lane of the workgroup calls it together (wave_push needs convergent lanes).
+    // (As a lambda the body's registers are allocated apart from the loop's: k_wfp_shade 149 → 115
+    // VGPRs for C3, profiles/r5_classed_shade_ab.log.)
+    auto shade = [&](const bool active, const int q) {
         // Two phases around the light-estimate pushes (as k_wfp_shade): the record, the transmittance
         // walk and the probe ray are written before the path's phase-function / BSDF sample.
         bool pushTr = false, pushProbe = false, pushDirect = false, pushNext = false;
@@ -341,6 +341,11 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
             W.next.s1[ni] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
         }
         if (pushDirect) X.dTgt[di] = pushNext ? ni : ~id;
+    };
+    for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
+        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
+        const bool active = i < n;
+        shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
     }
     __syncthreads();
     if (threadIdx.x == 0) {
