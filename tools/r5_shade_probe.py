@@ -81,7 +81,8 @@ def run(a):
             if a.counters and any(v["counts"][2:6]):   # PBR_STACK_DIAG: rays with a stack deeper than 6/10/16/24
                 extra = " stack>6/10/16/24 " + "/".join(f"{c / max(1, v['units']):.4f}" for c in v["counts"][2:6])
             parts.append(f"{k.replace('k_', '')} {v['ms']:.1f} ms {v['units'] / 1e6:.1f} M {ns:.3f} ns/u{extra}")
-        h = hashlib.sha256(rgb.cpu().numpy().tobytes()).hexdigest()[:16]
+        npx = rd.camera.width * rd.camera.height   # (the buffers are sized for the largest kind)
+        h = hashlib.sha256(rgb[:npx].cpu().numpy().tobytes()).hexdigest()[:16]
         if a.frames:
             r.set_schedule()
             for _ in range(2):
