@@ -1380,9 +1380,9 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, const FrameSet
                 else if (simple) hipLaunchKernelGGL((k_wf_shade_ml<kSimpleLobes, false>), gstride, blk, 0, st, W, l0);
                 else if (matsLds) hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, true>), gstride, blk, 0, st, W, l0);
                 else hipLaunchKernelGGL((k_wf_shade_ml<kAllLobes, false>), gstride, blk, 0, st, W, l0);
-            } else if (fuseCamera && l0 && mm && skyHalton && !(P.cam.lensRadius > 0)) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true, true>), gstride, blk, 0, st, W, l0);
-            else if (fuseCamera && l0 && mm) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
-            else if (fuseCamera && l0) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true, PBR_WF_FUSED_OCC, true>), gstride, blk, 0, st, W, l0);
+            } else if (fuseCamera && l0 && mm && skyHalton && !(P.cam.lensRadius > 0)) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, PBR_WF_FUSED_MATS_LDS != 0, PBR_WF_FUSED_OCC, true, true>), gstride, blk, 0, st, W, l0);
+            else if (fuseCamera && l0 && mm) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_SHADE_OCC, true>), gstride, blk, 0, st, W, l0);
+            else if (fuseCamera && l0) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true, PBR_WF_SHADE_OCC, true>), gstride, blk, 0, st, W, l0);
             else if (mm && matsLds && skyHalton) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true, PBR_WF_SHADE_OCC_MM, false, true>), gstride, blk, 0, st, W, l0);
             else if (mm && matsLds) hipLaunchKernelGGL((k_wf_shade<kMatteMirrorLobes, true>), gstride, blk, 0, st, W, l0);
             else if (simple && matsLds) hipLaunchKernelGGL((k_wf_shade<kSimpleLobes, true>), gstride, blk, 0, st, W, l0);

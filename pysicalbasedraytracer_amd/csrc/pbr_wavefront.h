@@ -478,8 +478,15 @@ __shared__ MatTemplate s_mats[kLdsMats];
 #ifndef PBR_WF_SHADE_OCC_MM
 #define PBR_WF_SHADE_OCC_MM PBR_WF_SHADE_OCC
 #endif
+// Round 5: with the per-ray body as a lambda the fused level-0 SkyBox shade needs 96 VGPRs (112
+// before), so 5 workgroups per CU fit in registers; they fit in LDS once its material templates are
+// read from global memory instead of an LDS copy (30.4 KB instead of 37.8).  C2 14.58 → 14.15 ms
+// (profiles/r5_fused_occ_ab.log; the LDS copy alone at 4: 14.63).
 #ifndef PBR_WF_FUSED_OCC
-#define PBR_WF_FUSED_OCC PBR_WF_SHADE_OCC
+#define PBR_WF_FUSED_OCC 5
+#endif
+#ifndef PBR_WF_FUSED_MATS_LDS
+#define PBR_WF_FUSED_MATS_LDS 0
 #endif
 // k_wf_camera_extend's work for queue position q inside the level-0 shade (CAMERA): the camera
 // sample's ray and its closest hit, as the queue entry the shade would have read.  Every lane of
@@ -555,10 +562,8 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     const int stride = gridDim.x * blockDim.x;
     const int nIter = (n + stride - 1) / stride;   // <= segCap / 256: a segment holds all pushes
     const int base = wf_block() * W.segCap, sbase = wf_block() * W.shadowSegCap;
-    for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
-        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-        const bool active = i < n;
-        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
+    // one queued ray (a lambda: its registers are allocated apart from the loop's, as k_wfp_shade's)
+    auto shade = [&](const bool active, const int q) {
         bool pushShadow = false, pushNext = false;
         int id = 0, depth = 0, dim = 0, emitDepth = 0;
         Ray ray, shadow, cont;
@@ -711,6 +716,11 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
             W.next.d[ni] = make_float4(cont.d.x, cont.d.y, cont.d.z, __int_as_float(pack_dd(dim, depth)));
             W.next.id[ni] = id;
         }
+    };
+    for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
+        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
+        const bool active = i < n;
+        shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
     }
     __syncthreads();
     if (threadIdx.x == 0) { W.shadowSeg[wf_block()] = s_push[0]; W.next.segCount[wf_block()] = s_push[1]; }
