@@ -103,3 +103,22 @@ def test_profile_timing_only_window(hip):
     assert prof["k_wf_camera_extend"]["launches"] == 2
     assert prof["k_wf_camera_extend"]["units"] == 0   # timings only: no counting launches
     assert all(v["ms"] > 0 for v in prof.values())
+
+
+@pytest.mark.gpu
+def test_classed_shade_one_launch_per_material_set(hip):
+    """C4's materials hold four lobe sets (rough glass, metal, plastic, matte): the Path shade runs one
+    launch per set and bounce (k_wfp_shade CLASSED), each shading only its set's hits, and the
+    counts of the bounce still add up (every queued ray shaded once)."""
+    s, rd = scenes.config_c4(64, 48, 8)
+    hip.upload(s)
+    hip.set_profiling(2)
+    hip.render(rd)
+    prof = hip.get_profile()
+    hip.set_profiling(0)
+    n = 64 * 48 * 8
+    shade = prof["k_wfp_shade"]
+    assert shade["launches"] == 4 * prof["k_wfp_resolve"]["launches"]
+    assert shade["units"] == n + prof["k_wf_extend"]["units"]
+    assert prof["k_wfp_shadow"]["units"] == shade["counts"][1]
+    assert prof["k_wfp_probe"]["units"] == shade["counts"][2]
