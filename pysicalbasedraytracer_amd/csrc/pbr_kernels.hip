@@ -832,6 +832,7 @@ struct WfBufs {
     DevBuf wRecC, wRecV;              // multi-light Whitted: per-light contributions, visibility
     // wavefront Path (pbr_wavefront_path.h): probe + direct queues, per-sample state and records
     DevBuf wqS0[2], wqS1[2];          // Path/VolPath: the path state carried with the ray
+    DevBuf wPassList, wPassCnt;       // the classed Path shade: passes 1..'s queue positions, counts
     DevBuf wpO, wpD, wpId, sL, rA, rB, rBeta, rLi, rFlags, rLight, rTgt;
     DevBuf wtO, wtD, wtP, wtE, wtN, wtId, rLiA, rTr, rWA;   // VolPath transmittance walk
 };
@@ -1499,6 +1500,14 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
         WfpParams& X = V.X;
         WfParams& W = X.W;
         X.matPass = classed ? (const int*)ctx->dMatPass.p : nullptr;
+        X.nPasses = classed ? (int)passKind.size() : 0;
+        if (classed) {   // pass 0 files the entries of passes 1.. per segment
+            HIP_TRY(B.wPassList.ensure((passKind.size() - 1) * qcap * 4));
+            HIP_TRY(B.wPassCnt.ensure((passKind.size() - 1) * kWfBlocks * sizeof(int)));
+            X.passList = (int*)B.wPassList.p;
+            X.passCnt = (int*)B.wPassCnt.p;
+            X.passStride = (int)qcap;
+        }
         if (vol) {
             V.anyHitTr = ctx->host.anyNoMaterial ? 0 : 1;
             HIP_TRY(B.wtO.ensure(qcap * 16)); HIP_TRY(B.wtD.ensure(qcap * 16)); HIP_TRY(B.wtP.ensure(qcap * 16));

@@ -43,6 +43,10 @@ struct WfpParams {
                            // position in the next queue, or ~id (stL[id]) when the path ended
     int lastLevel;         // this shade is the schedule's last: a continuation ends the path instead
     const int* matPass;    // the classed shade (CLASSED): the pass that shades each material's hits
+    int* passList;         // ... the queue positions of passes 1.. ([pass - 1][segmented], filed by pass 0)
+    int* passCnt;          // ... their counts ([pass - 1][workgroup])
+    int passStride;        // ... entries per pass list
+    int nPasses;
 };
 
 // The material pass of a queued hit (the classed shade): misses and material-less hits go to pass 0.
@@ -108,9 +112,11 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wfp_camera_extend(WfpPara
 // SMP: the frame's sampler type when the launch knows it (the other samplers' code — and the kernel
 // parameters it reads, which otherwise spill from SGPRs into VGPR lanes — is compiled out), else -1.
 // CLASSED: one of several launches per bounce, each shading the hits of the materials whose lobe set
-// it is compiled for (X.matPass, pass `pass`): the workgroup walks its queue entries as before,
-// gathers those of its pass into an LDS ring, and shades them 256 at a time, so every wave runs one
-// material class with that class's registers.  Pushes continue the segment counts of the pass before.
+// it is compiled for (X.matPass, pass `pass`).  Pass 0 walks the workgroup's queue entries as before,
+// gathers its own into an LDS ring and shades them 256 at a time, and files every other entry's
+// position in the list of its pass; a later pass shades its list, dense, 256 at a time.  So every
+// wave runs one material class with that class's registers, and only pass 0 reads every entry's
+// hit to classify it.  Pushes continue the segment counts of the pass before.
 // Entries land in the queues in another order, which nothing depends on (records are indexed by
 // sample or by queue position, and every L update keeps its order: pbr_wavefront_path.h header).
 template <int LOBES, bool MATS_LDS, int OCC = PBR_WFP_OCC, int SMP = -1, bool CLASSED = false>
@@ -356,18 +362,33 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0,
             const bool active = i < n;
             shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
         }
+    } else if (pass > 0) {   // this pass's list, filed by pass 0
+        const int cnt = X.passCnt[(pass - 1) * kWfBlocks + wf_block()];
+        const int* list = X.passList + (size_t)(pass - 1) * X.passStride + base;
+        for (int k0 = 0; k0 < cnt; k0 += 256) {   // uniform trip count
+            const int k = k0 + (int)threadIdx.x;
+            const bool active = k < cnt;
+            shade(active, active ? list[k] : 0);
+        }
     } else {
         // ring of queue positions of this pass: appended per iteration (at most 256), shaded 256 at a
         // time once that many are pending, so fewer than 256 wait and 512 slots never overrun
         __shared__ int s_ring[512];
         __shared__ int s_tail;
+        __shared__ int s_list[8];   // entries filed per later pass
         if (threadIdx.x == 0) s_tail = 0;
+        if (threadIdx.x < 8) s_list[threadIdx.x] = 0;
         __syncthreads();
         int head = 0;   // workgroup-uniform
         for (int it = 0; it < nIter; ++it) {
             const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
             const int q = i < n ? (level0 ? i : seg_pos(W.segCap, i)) : 0;
-            const bool mine = i < n && entry_pass(X, q) == pass;
+            const int cls = i < n ? entry_pass(X, q) : -1;
+            const bool mine = cls == 0;
+            for (int c = 1; c < X.nPasses; ++c) {   // file the other passes' entries (per segment, dense)
+                const int at = wave_push(&s_list[c - 1], cls == c);
+                if (cls == c) X.passList[(size_t)(c - 1) * X.passStride + base + at] = q;
+            }
             const int at = wave_push(&s_tail, mine);
             if (mine) s_ring[at & 511] = q;
             __syncthreads();
@@ -386,6 +407,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0,
             const int qq = active ? s_ring[(head + threadIdx.x) & 511] : 0;
             shade(active, qq);
         }
+        if ((int)threadIdx.x + 1 < X.nPasses) X.passCnt[threadIdx.x * kWfBlocks + wf_block()] = s_list[threadIdx.x];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
