@@ -1448,7 +1448,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
                                          (1 << L_MF_R) | (1 << L_MF_T), kMicroLobes};
     std::vector<int> passKind;                                   // pass → kPassLobes index
     std::vector<int32_t> matPass(ctx->host.materials.size() / 2, 0);
-    if (PBR_CLASSED_SHADE && !vol && !textured && matsLds && halton && micro) {
+    if (PBR_CLASSED_SHADE && !textured && matsLds && halton && micro) {
         std::vector<int> kindOf(matPass.size(), -1);
         for (size_t m = 0; m < matPass.size(); ++m) {
             const MatTemplate& mt = ctx->host.materials[2 * m + 1];   // the Path/VolPath lobes (make_bsdf)
@@ -1458,7 +1458,10 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
             for (int k = 0; k < 5; ++k)
                 if ((mask & ~kPassLobes[k]) == 0) { kindOf[m] = k; break; }
         }
-        for (int k = 0; k < 5; ++k)
+        // VolPath: pass 0 is compiled for every lobe (it takes the rays inside media, which may reach
+        // any surface), and materials of the union set stay in it
+        if (vol) passKind.push_back(4);
+        for (int k = 0; k < (vol ? 4 : 5); ++k)
             for (size_t m = 0; m < matPass.size(); ++m)
                 if (kindOf[m] == k) {
                     for (size_t j = 0; j < matPass.size(); ++j)
@@ -1591,15 +1594,27 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
             const int l0 = level == 0 ? 1 : 0;
             const int kShade = vol ? KP_WFV_SHADE : KP_WFP_SHADE;
             X.lastLevel = level + 1 >= maxLevels && !ctx->host.anyNoMaterial;
-            if (vol) {
+            if (vol && classed) {   // one launch per pass (pass 0: media, misses, the union set)
+                for (int p = 0; p < (int)passKind.size(); ++p) {
+                    constexpr int H = PBR_SAMPLER_HALTON, O = PBR_WFV_OCC;
+                    PROF_LAUNCH(KP_WFV_SHADE, st,
+                        switch (passKind[p]) {
+                        case 0: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[0], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
+                        case 1: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[1], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
+                        case 2: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[2], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
+                        case 3: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[3], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
+                        default: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[4], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
+                        });
+                }
+            } else if (vol) {
                 PROF_LAUNCH(KP_WFV_SHADE, st,
-                    if (textured) hipLaunchKernelGGL((k_wfv_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, V, l0);
-                    else if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0);
-                    else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, st, V, l0);
-                    else if (micro && matsLds && halton) hipLaunchKernelGGL((k_wfv_shade<kMicroLobes, true, PBR_WFV_OCC, PBR_SAMPLER_HALTON>), gshade, blk, 0, st, V, l0);
-                    else if (micro && matsLds) hipLaunchKernelGGL((k_wfv_shade<kMicroLobes, true>), gshade, blk, 0, st, V, l0);
-                    else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0);
-                    else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0));
+                    if (textured) hipLaunchKernelGGL((k_wfv_shade<kAllLobes | kTexturedLobes, false>), gshade, blk, 0, st, V, l0, 0);
+                    else if (simple && matsLds) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, true>), gshade, blk, 0, st, V, l0, 0);
+                    else if (simple) hipLaunchKernelGGL((k_wfv_shade<kSimpleLobes, false>), gshade, blk, 0, st, V, l0, 0);
+                    else if (micro && matsLds && halton) hipLaunchKernelGGL((k_wfv_shade<kMicroLobes, true, PBR_WFV_OCC, PBR_SAMPLER_HALTON>), gshade, blk, 0, st, V, l0, 0);
+                    else if (micro && matsLds) hipLaunchKernelGGL((k_wfv_shade<kMicroLobes, true>), gshade, blk, 0, st, V, l0, 0);
+                    else if (matsLds) hipLaunchKernelGGL((k_wfv_shade<kAllLobes, true>), gshade, blk, 0, st, V, l0, 0);
+                    else hipLaunchKernelGGL((k_wfv_shade<kAllLobes, false>), gshade, blk, 0, st, V, l0, 0));
             } else if (classed) {   // one launch per material pass, each compiled for its lobes
                 for (int p = 0; p < (int)passKind.size(); ++p) {
                     constexpr int H = PBR_SAMPLER_HALTON, O = PBR_WFP_OCC;

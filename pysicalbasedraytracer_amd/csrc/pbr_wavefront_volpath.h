@@ -40,8 +40,16 @@ __device__ __forceinline__ void set_interface(const DeviceScene& S, Isect* it, i
 #ifndef PBR_WFV_OCC
 #define PBR_WFV_OCC 3
 #endif
-template <int LOBES, bool MATS_LDS, int OCC = PBR_WFV_OCC, int SMP = -1>   // SMP: as k_wfp_shade's
-__global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0) {
+// The material pass of a queued VolPath ray (the classed shade): a ray inside a medium may scatter
+// there or reach any surface, so it goes to pass 0 (compiled for every lobe of the scene), as do
+// misses and material-less hits; a ray outside media goes to its hit material's pass.
+__device__ __forceinline__ int entry_pass_vol(const WfpParams& X, int q) {
+    if (((__float_as_int(X.W.cur.d[q].w) >> 24) & 0xff) != 0) return 0;   // in a medium (pack_vol)
+    return entry_pass(X, q);
+}
+// CLASSED: as k_wfp_shade's (pass 0 classifies and files, later passes read their lists)
+template <int LOBES, bool MATS_LDS, int OCC = PBR_WFV_OCC, int SMP = -1, bool CLASSED = false>   // SMP: as k_wfp_shade's
+__global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0, int pass) {
     WfpParams& X = V.X;
     WfParams& W = X.W;
     const KParams& P = W.P;
@@ -57,7 +65,14 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
         mats = s_mats;
     }
     __shared__ int s_push[4];   // transmittance walk, probe, direct, next
-    if (threadIdx.x < 4) s_push[threadIdx.x] = 0;
+    if (threadIdx.x < 4) {
+        int v = 0;   // (a later pass of the classed shade continues the segments)
+        if (CLASSED && pass > 0) {
+            const int b = wf_block();
+            v = threadIdx.x == 0 ? V.trSeg[b] : threadIdx.x == 1 ? X.probeSeg[b] : threadIdx.x == 2 ? X.directSeg[b] : W.next.segCount[b];
+        }
+        s_push[threadIdx.x] = v;
+    }
     __syncthreads();
     const int n = level0 ? W.nSamples : seg_scan(W.cur.segCount);
     const int stride = gridDim.x * blockDim.x;
@@ -342,10 +357,55 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0)
         }
         if (pushDirect) X.dTgt[di] = pushNext ? ni : ~id;
     };
-    for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
-        const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-        const bool active = i < n;
-        shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
+    if constexpr (!CLASSED) {
+        for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
+            const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
+            const bool active = i < n;
+            shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
+        }
+    } else if (pass > 0) {   // this pass's list, filed by pass 0
+        const int cnt = X.passCnt[(pass - 1) * kWfBlocks + wf_block()];
+        const int* list = X.passList + (size_t)(pass - 1) * X.passStride + base;
+        for (int k0 = 0; k0 < cnt; k0 += 256) {
+            const int k = k0 + (int)threadIdx.x;
+            const bool active = k < cnt;
+            shade(active, active ? list[k] : 0);
+        }
+    } else {   // pass 0: k_wfp_shade's ring, and the other passes' lists
+        __shared__ int s_ring[512];
+        __shared__ int s_tail;
+        __shared__ int s_list[8];
+        if (threadIdx.x == 0) s_tail = 0;
+        if (threadIdx.x < 8) s_list[threadIdx.x] = 0;
+        __syncthreads();
+        int head = 0;
+        for (int it = 0; it < nIter; ++it) {
+            const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
+            const int q = i < n ? (level0 ? i : seg_pos(W.segCap, i)) : 0;
+            const int cls = i < n ? entry_pass_vol(X, q) : -1;
+            for (int c = 1; c < X.nPasses; ++c) {
+                const int at = wave_push(&s_list[c - 1], cls == c);
+                if (cls == c) X.passList[(size_t)(c - 1) * X.passStride + base + at] = q;
+            }
+            const int at = wave_push(&s_tail, cls == 0);
+            if (cls == 0) s_ring[at & 511] = q;
+            __syncthreads();
+            const bool full = s_tail - head >= 256;
+            const int qq = full ? s_ring[(head + threadIdx.x) & 511] : 0;
+            __syncthreads();
+            if (full) {
+                shade(true, qq);
+                head += 256;
+            }
+        }
+        __syncthreads();
+        const int tail = s_tail;
+        if (head < tail) {
+            const bool active = head + (int)threadIdx.x < tail;
+            const int qq = active ? s_ring[(head + threadIdx.x) & 511] : 0;
+            shade(active, qq);
+        }
+        if ((int)threadIdx.x + 1 < X.nPasses) X.passCnt[threadIdx.x * kWfBlocks + wf_block()] = s_list[threadIdx.x];
     }
     __syncthreads();
     if (threadIdx.x == 0) {

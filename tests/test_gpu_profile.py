@@ -122,3 +122,17 @@ def test_classed_shade_one_launch_per_material_set(hip):
     assert shade["units"] == n + prof["k_wf_extend"]["units"]
     assert prof["k_wfp_shadow"]["units"] == shade["counts"][1]
     assert prof["k_wfp_probe"]["units"] == shade["counts"][2]
+
+
+@pytest.mark.gpu
+def test_classed_volpath_shade_passes(hip):
+    """C5's VolPath scene (matte floor and light, rough glass dragon filled with a medium): pass 0
+    takes the rays inside the medium and the misses, compiled for every lobe; the matte hits and the
+    glass hits outside the medium get a pass each — three k_wfv_shade launches per bounce."""
+    s, rd = scenes.config_c5(64, 48, 8)
+    hip.upload(s)
+    hip.set_profiling(2)
+    hip.render(rd)
+    prof = hip.get_profile()
+    hip.set_profiling(0)
+    assert prof["k_wfv_shade"]["launches"] == 3 * prof["k_wfv_resolve"]["launches"]
