@@ -1440,12 +1440,14 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
     const bool mm = (lobes & ~kMatteMirrorLobes) == 0;   // Lambert + mirror only (C3)
     const bool textured = (lobes & kTexturedLobes) != 0;
     const bool matsLds = ctx->host.materials.size() <= (size_t)kLdsMats;   // templates staged in LDS
-    // The classed Path shade (k_wfp_shade CLASSED): with materials of several lobe sets (C4's glass,
-    // metal, plastic and matte), one launch per lobe set shades that set's hits with a kernel
-    // compiled for it.  A material goes to the first of these sets that holds its lobes; misses and
-    // material-less hits to pass 0.
+    // The classed Path/VolPath shade (k_wfp_shade / k_wfv_shade CLASSED): with materials of several
+    // lobe sets (C4's glass, metal, plastic and matte), one launch per lobe set shades that set's hits
+    // with a kernel compiled for it.  A material goes to the first of these sets that holds its lobes;
+    // misses and material-less hits to pass 0.  VolPath: pass 0 is the medium pass (no lobes: the
+    // rays inside a medium, misses, material-less hits) and every lobe set present has a pass.
     static constexpr int kPassLobes[] = {1 << L_LAMBERT, 1 << L_MF_R, (1 << L_LAMBERT) | (1 << L_MF_R),
                                          (1 << L_MF_R) | (1 << L_MF_T), kMicroLobes};
+    constexpr int kMediumPassKind = 5;                          // VolPath's pass 0 (k_wfv_shade<0, …>)
     std::vector<int> passKind;                                   // pass → kPassLobes index
     std::vector<int32_t> matPass(ctx->host.materials.size() / 2, 0);
     if (PBR_CLASSED_SHADE && !textured && matsLds && halton && micro) {
@@ -1458,10 +1460,8 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
             for (int k = 0; k < 5; ++k)
                 if ((mask & ~kPassLobes[k]) == 0) { kindOf[m] = k; break; }
         }
-        // VolPath: pass 0 is compiled for every lobe (it takes the rays inside media, which may reach
-        // any surface), and materials of the union set stay in it
-        if (vol) passKind.push_back(4);
-        for (int k = 0; k < (vol ? 4 : 5); ++k)
+        if (vol) passKind.push_back(kMediumPassKind);
+        for (int k = 0; k < 5; ++k)
             for (size_t m = 0; m < matPass.size(); ++m)
                 if (kindOf[m] == k) {
                     for (size_t j = 0; j < matPass.size(); ++j)
@@ -1594,7 +1594,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
             const int l0 = level == 0 ? 1 : 0;
             const int kShade = vol ? KP_WFV_SHADE : KP_WFP_SHADE;
             X.lastLevel = level + 1 >= maxLevels && !ctx->host.anyNoMaterial;
-            if (vol && classed) {   // one launch per pass (pass 0: media, misses, the union set)
+            if (vol && classed) {   // one launch per pass (pass 0: the medium pass)
                 for (int p = 0; p < (int)passKind.size(); ++p) {
                     constexpr int H = PBR_SAMPLER_HALTON, O = PBR_WFV_OCC;
                     PROF_LAUNCH(KP_WFV_SHADE, st,
@@ -1603,7 +1603,8 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
                         case 1: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[1], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
                         case 2: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[2], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
                         case 3: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[3], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
-                        default: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[4], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
+                        case 4: hipLaunchKernelGGL((k_wfv_shade<kPassLobes[4], true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
+                        default: hipLaunchKernelGGL((k_wfv_shade<0, true, O, H, true>), gshade, blk, 0, st, V, l0, p); break;
                         });
                 }
             } else if (vol) {

@@ -40,16 +40,21 @@ __device__ __forceinline__ void set_interface(const DeviceScene& S, Isect* it, i
 #ifndef PBR_WFV_OCC
 #define PBR_WFV_OCC 3
 #endif
-// The material pass of a queued VolPath ray (the classed shade): a ray inside a medium may scatter
-// there or reach any surface, so it goes to pass 0 (compiled for every lobe of the scene), as do
-// misses and material-less hits; a ray outside media goes to its hit material's pass.
+// The material pass of a queued VolPath ray (the classed shade): a ray inside a medium goes to pass
+// 0, as do misses and material-less hits; a ray outside media goes to its hit material's pass.
+// Pass 0 is the medium pass (k_wfv_shade<0, …, CLASSED>: no BSDF lobes): it samples the medium of
+// every ray inside one and shades the medium events; a ray that reaches a surface with a material
+// instead leaves its state after the medium sample (β, the sampler dimension) in its queue entry
+// and is filed, flagged kDeferred, into that material's pass, which continues it from there.
 __device__ __forceinline__ int entry_pass_vol(const WfpParams& X, int q) {
     if (((__float_as_int(X.W.cur.d[q].w) >> 24) & 0xff) != 0) return 0;   // in a medium (pack_vol)
     return entry_pass(X, q);
 }
+constexpr int kDeferred = (int)0x80000000;   // pass-list entry: the medium pass sampled its medium
 // CLASSED: as k_wfp_shade's (pass 0 classifies and files, later passes read their lists)
 template <int LOBES, bool MATS_LDS, int OCC = PBR_WFV_OCC, int SMP = -1, bool CLASSED = false>   // SMP: as k_wfp_shade's
 __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0, int pass) {
+    constexpr bool kMediumPass = CLASSED && LOBES == 0;   // pass 0 of the classed shade
     WfpParams& X = V.X;
     WfParams& W = X.W;
     const KParams& P = W.P;
@@ -65,6 +70,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
         mats = s_mats;
     }
     __shared__ int s_push[4];   // transmittance walk, probe, direct, next
+    __shared__ int s_list[8];   // the classed shade's pass 0: entries filed into passes 1..
     if (threadIdx.x < 4) {
         int v = 0;   // (a later pass of the classed shade continues the segments)
         if (CLASSED && pass > 0) {
@@ -81,7 +87,9 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
     // one queued ray; every lane of the workgroup calls it together (wave_push needs convergent lanes).
     // (As a lambda the body's registers are allocated apart from the loop's: k_wfp_shade 149 → 115
     // VGPRs for C3, profiles/r5_classed_shade_ab.log.)
-    auto shade = [&](const bool active, const int q) {
+    // deferredIn: the medium pass left this entry after its medium sample.  Returns the pass a
+    // medium-pass entry was deferred to (0: shaded here).
+    auto shade = [&](const bool active, const int q, const bool deferredIn) -> int {
         // Two phases around the light-estimate pushes (as k_wfp_shade): the record, the transmittance
         // walk and the probe ray are written before the path's phase-function / BSDF sample.
         bool pushTr = false, pushProbe = false, pushDirect = false, pushNext = false;
@@ -99,6 +107,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
         bool estimate = false, mediumEvent = false;
         float g = 0;
         int di = -1;
+        int deferTo = 0;
         {
         Ray shadow, probe;
         VisPt vis;
@@ -116,7 +125,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
             ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, medium);
             const int slot = __float_as_int(hr.x);
             const bool found = slot >= 0;
-            if (level0) {
+            if (level0 && !deferredIn) {
                 L = sp(0.f); beta = sp(1.f); etaScale = 1.f;
                 sIndex = W.sampleIndex[q];
             } else {
@@ -136,7 +145,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
                 set_interface(S, &isect, ray.medium);
             }
             // HomogeneousMedium::Sample (HomogeneousMedium.cpp:15-45)
-            if (ray.medium >= 0) {
+            if (ray.medium >= 0 && !deferredIn) {
                 const float* md = S.media + 10 * ray.medium;
                 int channel = (int)(get1d<true, SMP>(P.smp, st) * 3);
                 if (channel > 2) channel = 2;
@@ -160,7 +169,20 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
                 if (pdf == 0) pdf = 1;
                 beta = beta * (sampled ? (Tr * sp3(md[3], md[4], md[5]) / pdf) : (Tr / pdf));
             }
-            bool alive = !black(beta);
+            if constexpr (kMediumPass) {
+                // a surface with a material reached from inside the medium: its material's pass
+                // continues the path from the state after the medium sample
+                if (ray.medium >= 0 && !mediumEvent && found) {
+                    const int mat = S.primInfo[slot].y;
+                    if (mat >= 0 && mats[2 * mat + 1].valid) deferTo = X.matPass[mat];
+                }
+                if (deferTo > 0) {
+                    W.cur.d[q] = make_float4(d.x, d.y, d.z, __int_as_float(pack_vol(st.dim, bounces, specularBounce, ray.medium)));
+                    W.cur.s0[q] = make_float4(L.r, L.g, L.b, beta.r);
+                    W.cur.s1[q] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
+                }
+            }
+            bool alive = deferTo == 0 && !black(beta);
             if (alive && mediumEvent) {
                 if (bounces >= P.maxDepth) alive = false;
                 else estimate = true;
@@ -299,7 +321,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
                 X.pid[pi] = di;
             }
         }
-        if (active) {
+        if (active && deferTo == 0) {
             bool doRR = false;
             if (estimate) {
                 if (mediumEvent) {   // HenyeyGreenstein::Sample_p, then the ray leaves the interaction
@@ -356,12 +378,22 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
             W.next.s1[ni] = make_float4(beta.g, beta.b, etaScale, __uint_as_float(sIndex));
         }
         if (pushDirect) X.dTgt[di] = pushNext ? ni : ~id;
+        return deferTo;
+    };
+    // the medium pass files a deferred entry into its material's pass list (convergent lanes)
+    auto file_deferred = [&](const int dp, const int q) {
+        if constexpr (kMediumPass) {
+            for (int c = 1; c < X.nPasses; ++c) {
+                const int at = wave_push(&s_list[c - 1], dp == c);
+                if (dp == c) X.passList[(size_t)(c - 1) * X.passStride + base + at] = q | kDeferred;
+            }
+        }
     };
     if constexpr (!CLASSED) {
         for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
             const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
             const bool active = i < n;
-            shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
+            shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)), false);
         }
     } else if (pass > 0) {   // this pass's list, filed by pass 0
         const int cnt = X.passCnt[(pass - 1) * kWfBlocks + wf_block()];
@@ -369,12 +401,12 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
         for (int k0 = 0; k0 < cnt; k0 += 256) {
             const int k = k0 + (int)threadIdx.x;
             const bool active = k < cnt;
-            shade(active, active ? list[k] : 0);
+            const int e = active ? list[k] : 0;
+            shade(active, e & ~kDeferred, (e & kDeferred) != 0);
         }
     } else {   // pass 0: k_wfp_shade's ring, and the other passes' lists
         __shared__ int s_ring[512];
         __shared__ int s_tail;
-        __shared__ int s_list[8];
         if (threadIdx.x == 0) s_tail = 0;
         if (threadIdx.x < 8) s_list[threadIdx.x] = 0;
         __syncthreads();
@@ -394,7 +426,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
             const int qq = full ? s_ring[(head + threadIdx.x) & 511] : 0;
             __syncthreads();
             if (full) {
-                shade(true, qq);
+                file_deferred(shade(true, qq, false), qq);
                 head += 256;
             }
         }
@@ -403,8 +435,9 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
         if (head < tail) {
             const bool active = head + (int)threadIdx.x < tail;
             const int qq = active ? s_ring[(head + threadIdx.x) & 511] : 0;
-            shade(active, qq);
+            file_deferred(shade(active, qq, false), qq);
         }
+        if constexpr (kMediumPass) __syncthreads();   // every wave's deferred entries are filed
         if ((int)threadIdx.x + 1 < X.nPasses) X.passCnt[threadIdx.x * kWfBlocks + wf_block()] = s_list[threadIdx.x];
     }
     __syncthreads();

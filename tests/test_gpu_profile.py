@@ -126,9 +126,10 @@ def test_classed_shade_one_launch_per_material_set(hip):
 
 @pytest.mark.gpu
 def test_classed_volpath_shade_passes(hip):
-    """C5's VolPath scene (matte floor and light, rough glass dragon filled with a medium): pass 0
-    takes the rays inside the medium and the misses, compiled for every lobe; the matte hits and the
-    glass hits outside the medium get a pass each — three k_wfv_shade launches per bounce."""
+    """C5's VolPath scene (matte floor and light, rough glass dragon filled with a medium): pass 0,
+    the medium pass, takes the rays inside the medium and the misses; the matte hits and the glass
+    hits (from outside, and from inside once the medium pass has sampled the medium) get a pass
+    each — three k_wfv_shade launches per bounce."""
     s, rd = scenes.config_c5(64, 48, 8)
     hip.upload(s)
     hip.set_profiling(2)
