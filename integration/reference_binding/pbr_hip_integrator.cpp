@@ -460,14 +460,17 @@ void HipSamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     std::vector<uint8_t> rgba((size_t)W * H * 4);
     std::vector<float> rgb((size_t)W * H * 3);
     check(pbr_hip_render(ctx_, &rd, rgb.data(), rgba.data(), nullptr), "render");
+    lastDesc_ = rd;
     // Integrator.cpp:327-344: pixel (x, y) → set_uc(x, height - 1 - y); the device produced the same
     // bytes (ToXYZ, XYZToRGB, GammaCorrect, +0.5, clamp) with alpha 255.  The FrameBuffer's float
-    // buffer, which the reference allocates but never writes, gets colObj / spp (linear
-    // RGB, alpha 1) at the same place through its own set_fc.
+    // buffer, which the reference allocates but never writes, is left as the caller had it
+    // unless SetWriteFloatBuffer(true) asked for colObj / spp (linear RGB, alpha 1) there, at the same
+    // place, through its own set_fc.
     if (fb_) {
         for (int y = 0; y < H; ++y)
             for (int x = 0; x < W; ++x) {
                 for (int c = 0; c < 4; ++c) fb_->set_uc(x, H - y - 1, c, rgba[((size_t)y * W + x) * 4 + c]);
+                if (!writeFloat_) continue;
                 for (int c = 0; c < 3; ++c) fb_->set_fc(x, H - y - 1, c, rgb[((size_t)y * W + x) * 3 + c]);
                 fb_->set_fc(x, H - y - 1, 3, 1.f);
             }

@@ -83,9 +83,16 @@ class HipSamplerIntegrator : public PBR::SamplerIntegrator {
     ~HipSamplerIntegrator();
     void Render(const PBR::Scene& scene, double& timeConsume);
     void SetDevice(int device) { device_ = device; }
+    // Off by default, as in the reference's Render, which never writes the FrameBuffer's float buffer
+    // (Integrator.cpp:341-344 writes only set_uc): on, Render also stores colObj / spp (linear RGB,
+    // alpha 1) there through set_fc — the parity harness reads the device's floats that way.
+    void SetWriteFloatBuffer(bool on) { writeFloat_ = on; }
     // the device context (after the first Render): parity tests read the uploaded BVH through it
     pbr_hip_ctx* Context() const { return ctx_; }
     const FlatScene* Flat() const { return flat_.get(); }
+    // the render descriptor of the last Render (whole raster, host outputs): with Flat()->desc, what a
+    // parity harness hands a CPU restatement to render the same frame
+    const pbr_render_desc& LastRenderDesc() const { return lastDesc_; }
 
   private:
     const int integrator_, maxDepth_;
@@ -95,6 +102,8 @@ class HipSamplerIntegrator : public PBR::SamplerIntegrator {
     const PBR::Bounds2i bounds_;
     ::FrameBuffer* fb_;
     int device_ = 0;
+    bool writeFloat_ = false;
+    pbr_render_desc lastDesc_{};
     pbr_hip_ctx* ctx_ = nullptr;
     const PBR::Scene* uploaded_ = nullptr;
     std::shared_ptr<FlatScene> flat_;

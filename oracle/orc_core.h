@@ -31,7 +31,21 @@ inline float gamma(int n) {
     return (float)((n * eps) / (1 - n * eps));
 }
 
-// Transcendentals: correctly rounded convention (see pbr_oracle.h header).
+// Transcendentals: correctly rounded convention (see pbr_oracle.h header).  ORC_LIBM_FLOAT (the
+// liboracle_libm.so diagnostic build, oracle/Makefile) calls the float overloads the reference calls
+// instead — glibc's sinf, expf, logf, ... — to show that the oracle's differences from the reference
+// are those functions' last bits and nothing else (tests/test_ref_fullsize.py).
+#ifdef ORC_LIBM_FLOAT
+inline float t_sin(float x) { return std::sin(x); }
+inline float t_cos(float x) { return std::cos(x); }
+inline float t_tan(float x) { return std::tan(x); }
+inline float t_exp(float x) { return std::exp(x); }
+inline float t_log(float x) { return std::log(x); }
+inline float t_pow(float x, float y) { return std::pow(x, y); }
+inline float t_atan2(float y, float x) { return std::atan2(y, x); }
+inline float t_asin(float x) { return std::asin(x); }
+inline float t_acos(float x) { return std::acos(x); }
+#else
 inline float t_sin(float x) { return (float)std::sin((double)x); }
 inline float t_cos(float x) { return (float)std::cos((double)x); }
 inline float t_tan(float x) { return (float)std::tan((double)x); }
@@ -41,6 +55,7 @@ inline float t_pow(float x, float y) { return (float)std::pow((double)x, (double
 inline float t_atan2(float y, float x) { return (float)std::atan2((double)y, (double)x); }
 inline float t_asin(float x) { return (float)std::asin((double)x); }
 inline float t_acos(float x) { return (float)std::acos((double)x); }
+#endif
 
 // std::min / std::max / Clamp semantics (NaN-sensitive order), Core/PBR.h:183-191
 inline float fmin_(float a, float b) { return (b < a) ? b : a; }

@@ -6,6 +6,7 @@
 #include "orc_envmap.h"
 
 #include <chrono>
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -1540,8 +1541,9 @@ static int mat_index(const pbr_scene_desc* d, int m) {
 
 static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
     if (!d || d->abi_version != PBR_HIP_ABI_VERSION) throw std::runtime_error("bad scene desc");
-    // the restatement always builds its own BVHAccel (a caller-built tree is a product upload option)
-    if (d->bvh_nodes) throw std::runtime_error("the oracle builds its own BVH (bvh_nodes unsupported)");
+    // A caller-built tree (pbr_scene_desc::bvh_nodes: the reference's own BVHAccel, primitives given
+    // in its leaf order) is adopted as is, as the product's upload adopts it; else BVHAccel is built.
+    if (d->bvh_nodes && d->n_bvh_nodes <= 0) throw std::runtime_error("bvh_nodes without n_bvh_nodes");
     std::unique_ptr<Scene> s(new Scene);
     std::vector<Prim> prims;
     int ns = d->n_shapes;
@@ -1682,7 +1684,16 @@ static std::unique_ptr<Scene> BuildScene(const pbr_scene_desc* d) {
         }
         s->lights.push_back(std::move(l));
     }
-    BuildBVH(*s, prims, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1, d->split_method);
+    if (d->bvh_nodes) {
+        s->nodes.resize(d->n_bvh_nodes);
+        std::memcpy(s->nodes.data(), d->bvh_nodes, sizeof(OrcLinearBVHNode) * (size_t)d->n_bvh_nodes);
+        s->prims = prims;
+        s->primIds.resize(prims.size());
+        s->primOfOriginal.resize(prims.size());
+        for (size_t i = 0; i < prims.size(); ++i) s->primIds[i] = s->primOfOriginal[i] = (int)i;
+    } else {
+        BuildBVH(*s, prims, d->max_prims_in_node > 0 ? d->max_prims_in_node : 1, d->split_method);
+    }
     for (Light& l : s->lights)
         if (l.type == PBR_LIGHT_DIFFUSE_AREA) l.area = TriangleArea(*s, s->prims[s->primOfOriginal[l.prim]]);
     for (Light& l : s->lights)

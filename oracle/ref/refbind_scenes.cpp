@@ -335,6 +335,7 @@ int refbind_render(int config, int res, int spp, uint8_t* ref_out, uint8_t* hip_
             FrameBuffer fb;
             fb.InitBuffer(res, res, 4);
             auto hip = make_hip(&fb);
+            hip->SetWriteFloatBuffer(hip_rgb != nullptr);   // the device's floats, read back below
             double t = 0;
             hip->Render(*B->scene, t);
             std::memcpy(hip_out, fb.getUCbuffer(), (size_t)res * res * 4);
@@ -358,6 +359,43 @@ int refbind_render(int config, int res, int spp, uint8_t* ref_out, uint8_t* hip_
         return 0;
     } catch (const std::exception& e) {
         ref_frame_arena(0);
+        if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", e.what());
+        return -1;
+    }
+}
+
+// The binding's own flattened scene and render descriptor for scene `config` (what its Render hands
+// the C-ABI) rendered by two CPU restatements whose oracle_render entry points the caller passes in:
+// `oracle` (oracle/liboracle.so, correctly rounded transcendentals) into ora_rgb and `libm`
+// (oracle/liboracle_libm.so, glibc's float functions as the reference calls them) into libm_rgb —
+// res·res·3 floats, image rows top to bottom.  Test infrastructure: it separates the drop-in's
+// differences from the reference into the restatement's (none: device = oracle) and libm's last bits
+// (libm twin = reference).
+typedef int (*oracle_render_fn)(const pbr_scene_desc*, const pbr_render_desc*, float*, uint8_t*, int, double*);
+int refbind_render_oracles(int config, int res, int spp, void* oracle, void* libm, float* ora_rgb, float* libm_rgb,
+                           char* err, int errlen) {
+    try {
+        std::unique_ptr<Built> B = build(config, res);
+        const Bounds2i bounds(Point2i(0, 0), Point2i(res, res));
+        auto sampler = std::make_shared<HaltonSampler>(spp, bounds);
+        const int integ = integrator_of(config);
+        FrameBuffer fb;
+        fb.InitBuffer(res, res, 4);
+        std::shared_ptr<pbrhip::HipSamplerIntegrator> hip;
+        if (integ == 0) hip = std::make_shared<pbrhip::HipWhittedIntegrator>(5, B->cam, sampler, bounds, &fb);
+        else if (integ == 1) hip = std::make_shared<pbrhip::HipPathIntegrator>(8, B->cam, sampler, bounds, 0.8f, "uniform", &fb);
+        else hip = std::make_shared<pbrhip::HipVolPathIntegrator>(10, B->cam, sampler, bounds, 1.f, "uniform", &fb);
+        double t = 0;
+        hip->Render(*B->scene, t);
+        pbr_render_desc rd = hip->LastRenderDesc();
+        std::vector<uint8_t> rgba((size_t)res * res * 4);
+        double sec = 0;
+        if (ora_rgb && oracle_render_fn(oracle)(&hip->Flat()->desc, &rd, ora_rgb, rgba.data(), 0, &sec) != 0)
+            throw std::runtime_error("oracle_render failed");
+        if (libm_rgb && oracle_render_fn(libm)(&hip->Flat()->desc, &rd, libm_rgb, rgba.data(), 0, &sec) != 0)
+            throw std::runtime_error("oracle_render (libm twin) failed");
+        return 0;
+    } catch (const std::exception& e) {
         if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", e.what());
         return -1;
     }

@@ -91,13 +91,21 @@ class HipRenderer:
         """n frames of one descriptor into device buffers (pbr_hip_render_frames): their chunks
         continue one rotation over the lanes with no join between frames.  Asynchronous; `stream`
         reaches its tail when every frame is done; wait_frame orders another stream after one."""
+        rgb_ptrs, rgba_ptrs = list(rgb_ptrs or []), list(rgba_ptrs or [])
+        if rgb_ptrs and rgba_ptrs and len(rgb_ptrs) != len(rgba_ptrs):
+            raise ValueError(f"render_frames: {len(rgb_ptrs)} float outputs but {len(rgba_ptrs)} RGBA8 outputs")
         n = max(len(rgb_ptrs), len(rgba_ptrs))
+        if n == 0:
+            raise ValueError("render_frames: no output buffers")
         rgb = (C.c_void_p * n)(*[p or None for p in rgb_ptrs]) if rgb_ptrs else None
         rgba = (C.c_void_p * n)(*[p or None for p in rgba_ptrs]) if rgba_ptrs else None
-        rdesc.outputs_on_device = 1
-        rdesc.stream = stream
-        rdesc.collect_stats = 0
-        self._check(self.lib.pbr_hip_render_frames(self.ctx, C.byref(rdesc), n, rgb, rgba), "render_frames")
+        # the caller's descriptor is left as it was: the batch's settings go on a copy (its tile
+        # pointer still refers to the caller's arrays, which rdesc keeps alive for this call)
+        d = type(rdesc).from_buffer_copy(rdesc)
+        d.outputs_on_device = 1
+        d.stream = stream
+        d.collect_stats = 0
+        self._check(self.lib.pbr_hip_render_frames(self.ctx, C.byref(d), n, rgb, rgba), "render_frames")
 
     def wait_frame(self, stream: int | None, f: int):
         """Make `stream` wait for frame f of the last render_frames call (pbr_hip_wait_frame)."""

@@ -899,7 +899,9 @@ struct pbr_hip_ctx {
     double bvhMs = 0, bvhKernelMs = 0;   // the last upload's BVH build: wall / device time
     int bvhWhereLast = PBR_BVH_BUILD_HOST;   // ... and where it ran (Middle / EqualCounts: always the host)
     DevBuf dGuard;                       // DeviceScene::guard (kGuard* bits of tripped safety bounds)
-    int* guardHost = nullptr;            // pinned copy, refreshed at the end of frames that can trip one
+    int* guardHost = nullptr;            // pinned copy, refreshed at the end of every frame
+    hipEvent_t evGuard = nullptr;        // recorded after the last frame's guard copy, on that frame's stream
+    bool guardPending = false;           // that copy may still be in flight: guardHost is read once it landed
 };
 
 namespace {
@@ -951,12 +953,23 @@ void quiesce(pbr_hip_ctx* ctx, hipStream_t s) {
 // end; synchronous renders check it before returning, asynchronous ones at the next call.
 // The caller has made ctx->device current and drained the context (the pinned copy of an
 // asynchronous frame lands only when that frame ends); the reset is ordered on the context's stream.
+// The copy of an asynchronous frame is read only once its event has completed (a copy still in
+// flight is checked by a later call or pbr_hip_sync, which drains first).  A tripped bit is reset on
+// the context's stream ordered after that copy, and guardHost is cleared only after the reset has
+// run, so no copy queued before it can land later and fail an unrelated frame.
 int check_guard(pbr_hip_ctx* ctx) {
+    if (ctx->guardPending) {
+        const hipError_t q = hipEventQuery(ctx->evGuard);
+        if (q == hipErrorNotReady) return PBR_OK;
+        HIP_TRY(q);
+        ctx->guardPending = false;
+    }
     const int g = ctx->guardHost ? *(volatile int*)ctx->guardHost : 0;
     if (!g) return PBR_OK;
-    *ctx->guardHost = 0;
+    HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->evGuard, 0));
     HIP_TRY(hipMemsetAsync(ctx->dGuard.p, 0, sizeof(int), ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *ctx->guardHost = 0;
     std::string what;
     if (g & kGuardWhittedPassThrough) what += "a Whitted path crossed more than 1024 material-less surfaces; ";
     if (g & kGuardTransmittance) what += "a transmittance walk crossed more than 256 medium interfaces; ";
@@ -1100,7 +1113,14 @@ struct WfChunks {
     int segCap = 0;   // capacity of one queue segment
     size_t qcap = 0;  // queue entries
 };
-WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25, bool batch = false) {
+// A batch's one-chunk frames rotate over the lanes, and every lane holds queue and record buffers for
+// the whole frame: they keep several lanes only while the lanes' buffers together stay within this
+// many bytes (bytesPerSample × samples per lane, estimated from the schedule's buffers).  A C2 rank
+// shard (≤ 2^25 samples, ≈ 12 GB per lane) keeps three; a Path frame at the 2^26-sample cap (≈ 23
+// GB per lane) two; the single-frame call would run such a frame on one lane.
+constexpr double kBatchLaneBytes = 48e9;
+WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25, bool batch = false,
+                   double bytesPerSample = 0) {
     WfChunks c;
     const int chunkLog2 = sch.chunk_log2 > 0 ? std::min(sch.chunk_log2, maxLog2) : maxLog2;   // the default bounds the memory
     c.lanes = sch.serial ? 1 : (sch.lanes > 0 ? sch.lanes : kWfDefaultLanes);
@@ -1108,6 +1128,10 @@ WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25, 
     if (c.chunkPix >= P.nPixels) {   // one chunk: splitting a small frame only adds launch tails
         c.chunkPix = P.nPixels;
         if (!batch) c.lanes = 1;     // (a batch's one-chunk frames rotate over the lanes)
+        else if (c.lanes > 1 && bytesPerSample > 0) {
+            const double perLane = bytesPerSample * (double)P.nPixels * (double)P.spp;
+            c.lanes = (int)std::max(1.0, std::min((double)c.lanes, std::floor(kBatchLaneBytes / perLane)));
+        }
     } else {
         // Many chunks: make them equal and a whole number per lane (the count rounded down to a
         // multiple of the lanes), so no lane runs a last chunk alone.  Measured (bit-identical,
@@ -1237,9 +1261,12 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, const FrameSet
     // they stay under 8 GB per lane (C2: 5 levels × 36 B × 2^25 = 6 GB)
     int maxLog2 = 25;
     while (maxLog2 > 20 && (double)levels * (36.0 + (ml ? 17.0 * nL : 0.0)) * (double)(1LL << maxLog2) > 8e9) --maxLog2;
-    const WfChunks ch = wf_chunks(ctx->sched, P, maxLog2, F.batch);
-    const size_t cap = ch.cap, qcap = ch.qcap;
     const int lightsPerShade = ml ? std::max(1, nL) : 1;
+    // the lane buffers below, per sample: two ray queues, the shadow queue(s), the records
+    const double bytesPerSample = 2 * 52.0 + (52.0 + (skyDeferred ? 16.0 : 0.0)) * lightsPerShade + 16.0 +
+                                  levels * (36.0 + (ml ? 17.0 * nL : 0.0)) + 8.0;
+    const WfChunks ch = wf_chunks(ctx->sched, P, maxLog2, F.batch, bytesPerSample);
+    const size_t cap = ch.cap, qcap = ch.qcap;
     const size_t sqcap = qcap * (size_t)lightsPerShade;   // shadow-queue entries
     const int lobes = scene_lobe_kinds(ctx->host);
     const bool simple = (lobes & ~kSimpleLobes) == 0;
@@ -1429,7 +1456,10 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
     const int spp = P.spp;
     // ≈ 290 B of queues + state per sample: 19.5 GB per 2^26 chunk and lane.  Measured (bit-identical):
     // C3 2^25 349.4 ms, 2^26 336.1, 2^27 340.4; C5 2^25 1979 ms, 2^26 1939, 2^27 1919
-    const WfChunks ch = wf_chunks(ctx->sched, P, 26, F.batch);
+    // the lane buffers below, per sample: two ray queues with their state (84 B each), shadow and probe
+    // queues, the direct records, the sample's L and index (+ VolPath's transmittance walk and
+    // records), and the class pass lists (at most 5 passes)
+    const WfChunks ch = wf_chunks(ctx->sched, P, 26, F.batch, (vol ? 460.0 : 340.0) + 4.0 * 5);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const long long nChunks = (P.nPixels + ch.chunkPix - 1) / ch.chunkPix;
     const int lobes = scene_lobe_kinds(ctx->host);
@@ -1829,8 +1859,11 @@ int pbr_hip_li(pbr_hip_ctx* ctx, const pbr_render_desc* d, int n, const float* r
     else hipLaunchKernelGGL(k_li<PBR_INTEGRATOR_VOLPATH>, g, b, 0, ctx->stream, P, n, (const float*)in, qd, o);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(rgb_out, o, ob, hipMemcpyDeviceToHost, ctx->stream));
-    if (ctx->host.anyNoMaterial || d->sampler == PBR_SAMPLER_TABLE)
+    if (ctx->host.anyNoMaterial || d->sampler == PBR_SAMPLER_TABLE) {
         HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipEventRecord(ctx->evGuard, ctx->stream));
+        ctx->guardPending = true;
+    }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return check_guard(ctx);
 }
@@ -1896,7 +1929,8 @@ int pbr_hip_create(int device, pbr_hip_ctx** out) {
     ctx->device = device;
     if (hipSetDevice(device) != hipSuccess) return PBR_E_HIP;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return PBR_E_HIP;
-    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return PBR_E_HIP;
+    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->evGuard, hipEventDisableTiming) != hipSuccess) return PBR_E_HIP;
     build_halton_tables(1000, &ctx->halton);
     pbr_hip_ctx* c = ctx.get();
     {
@@ -1944,6 +1978,7 @@ int pbr_hip_destroy(pbr_hip_ctx* ctx) {
     }
     ctx->profEv.clear();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->evGuard) (void)hipEventDestroy(ctx->evGuard);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->guardHost) (void)hipHostFree(ctx->guardHost);
     hipStream_t s = ctx->stream;
@@ -2169,6 +2204,8 @@ static int render_impl(pbr_hip_ctx* ctx, const pbr_render_desc* d, float* rgb_ou
     // fails this call (synchronous frames) or the next one / pbr_hip_sync (asynchronous ones), and a
     // bit is never left behind to fail an unrelated later frame
     HIP_TRY(hipMemcpyAsync(ctx->guardHost, ctx->dGuard.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(ctx->evGuard, s));
+    ctx->guardPending = true;
     if (!d->outputs_on_device || d->collect_stats || stats || d->sampler == PBR_SAMPLER_TABLE) {
         HIP_TRY(hipStreamSynchronize(s));
         if (int rc = check_guard(ctx)) return rc;

@@ -1245,12 +1245,23 @@ void SamplerIntegrator::Render(const Scene& scene, double& timeConsume) {
     std::vector<float> rgb(npx * 3);
     std::vector<uint8_t> rgba(npx * 4);
     pbr_render_stats st;
-    for (;;) {
+    // Retry only when the sample-table bound is the ONE guard bit the frame tripped (check_guard lists
+    // the bits in a fixed order and the sample table's comes last, so its clause then opens the
+    // message), at most kMaxTableRetries times; any other failure — or a table that would outgrow
+    // kMaxSampleTableBytes — reports the render's original error.
+    static const char kTableOnly[] = "a path asked the sample table for a dimension beyond table_dims; ";
+    constexpr int kMaxTableRetries = 4;
+    for (int retry = 0;; ++retry) {
         const int rc = pbr_hip_render(ctx, &rd, rgb.data(), rgba.data(), &st);
-        if (rc == PBR_E_UNSUPPORTED && rd.sampler == PBR_SAMPLER_TABLE &&
-            std::strstr(pbr_hip_last_error(ctx), "sample table") != nullptr) {
+        if (rc == PBR_E_UNSUPPORTED && rd.sampler == PBR_SAMPLER_TABLE && retry < kMaxTableRetries &&
+            std::strncmp(pbr_hip_last_error(ctx), kTableOnly, sizeof(kTableOnly) - 1) == 0) {
+            const std::string original = pbr_hip_last_error(ctx);
             dims *= 2;   // a path went past the table (medium boundaries): more dimensions, same frame
-            tabulate(dims);
+            try {
+                tabulate(dims);
+            } catch (const std::invalid_argument&) {
+                throw std::runtime_error(std::string("pbr_hip_render: ") + original);
+            }
             continue;
         }
         check(ctx, rc, "pbr_hip_render");

@@ -62,6 +62,31 @@ def render(scene, rdesc, threads=0):
     return rgb, rgba, sec.value
 
 
+_libm = None
+
+
+def render_libm(scene, rdesc, threads=0):
+    """render() through oracle/liboracle_libm.so: the same restatement calling the float libm
+    functions the reference calls (glibc sinf, expf, logf, ...) instead of the correctly rounded
+    (float)f((double)x) — a diagnostic that isolates libm's last bits as the cause of every
+    difference from the reference (tests/test_ref_fullsize.py)."""
+    global _libm
+    if _libm is None:
+        path = os.path.join(ORACLE_DIR, "liboracle_libm.so")
+        if not os.path.exists(path):
+            subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+        _libm = C.CDLL(path)
+        _libm.oracle_render.argtypes = [C.POINTER(capi.SceneDesc), C.POINTER(capi.RenderDesc), C.c_void_p, C.c_void_p,
+                                        C.c_int, C.POINTER(C.c_double)]
+    d = scene.desc()
+    n = n_pixels(rdesc)
+    rgb = np.empty((n, 3), dtype=np.float32)
+    rgba = np.empty((n, 4), dtype=np.uint8)
+    sec = C.c_double()
+    assert _libm.oracle_render(C.byref(d), C.byref(rdesc), rgb.ctypes.data, rgba.ctypes.data, threads, C.byref(sec)) == 0
+    return rgb, rgba, sec.value
+
+
 def render_stats(scene, rdesc, threads=0):
     lib = load()
     d = scene.desc()

@@ -213,11 +213,35 @@ def frame_cases():
     return out
 
 
-def fullsize_pixels(width, height, n=64, seed=0):
+def default_chunk_starts(n_pixels, spp, integrator, max_depth, lanes=3):
+    """First packed pixel of every chunk of the default wavefront schedule for a one-tile frame —
+    wf_chunks (pysicalbasedraytracer_amd/csrc/pbr_kernels.hip, `WfChunks wf_chunks`): at most 2^25
+    samples per Whitted chunk (fewer while levels x 36 B x 2^k > 8 GB), 2^26 for Path/VolPath; 24 or
+    more chunks are equalised to a whole number per lane.  Parity tests pick the pixels either side
+    of each boundary, where one lane's chunk hands over to the next."""
+    if integrator == capi.INTEGRATOR_WHITTED:
+        log2 = 25
+        while log2 > 20 and max(1, max_depth) * 36.0 * (1 << log2) > 8e9:
+            log2 -= 1
+    else:
+        log2 = 26
+    chunk = max(1, (1 << log2) // spp)
+    if chunk >= n_pixels:
+        return [0]
+    n = (n_pixels + chunk - 1) // chunk
+    if n >= 24:
+        n = max(lanes, n // lanes * lanes)
+        chunk = (n_pixels + n - 1) // n
+    return list(range(0, n_pixels, chunk))
+
+
+def fullsize_pixels(width, height, n=1024, seed=0, boundaries=()):
     """n distinct pixels of a width x height raster as one-pixel tiles (x0, y0, x1, y1): the four
     corners, the centre, one on the area light, a jittered 4x4 grid over the whole frame and a
     jittered 6x7 grid over the dragon's part of the frame (x 0.38-0.65, y 0.2-0.62 of the raster,
-    where the paths are longest), seeded."""
+    where the paths are longest) — the 64 pixels of round 5, kept first — then the two pixels either
+    side of every chunk boundary of the default schedule (`boundaries`: packed row-major indices),
+    then jittered 16x16 grids over the frame and 24x24 over the dragon until n, seeded."""
     rng = np.random.default_rng(seed)
     px = [(0, 0), (width - 1, 0), (0, height - 1), (width - 1, height - 1), (width // 2, height // 2),
           (width // 2, height // 50)]
@@ -231,6 +255,13 @@ def fullsize_pixels(width, height, n=64, seed=0):
 
     grid(4, 4, 0.0, 1.0, 0.0, 1.0)
     grid(6, 7, 0.38, 0.65, 0.2, 0.62)
+    for p0 in boundaries:
+        for p in (p0 - 1, p0):
+            if 0 <= p < width * height:
+                px.append((p % width, p // width))
+    while len(set(px)) < n:
+        grid(16, 16, 0.0, 1.0, 0.0, 1.0)
+        grid(24, 24, 0.38, 0.65, 0.2, 0.62)
     out, seen = [], set()
     for p in px:
         if p not in seen:
@@ -239,11 +270,15 @@ def fullsize_pixels(width, height, n=64, seed=0):
     return [(x, y, x + 1, y + 1) for x, y in out[:n]]
 
 
+FULLSIZE_PIXELS = 1024
+
+
 def fullsize_cases():
     """name → (scene, render desc with one-pixel tiles): the BASELINE configs at their real size —
-    the 100,352-triangle dragon stand-in, full raster, full spp, full depth — on 64 pixels each.
-    C3 runs on the Halton sampler (the reference has no Sobol sampler, F3); C4 is 3840x2160 at
-    1024 spp.  The raster and spp fix the sample indices, so these are the benchmarked samples."""
+    the 100,352-triangle dragon stand-in, full raster, full spp, full depth — on 1024 pixels each,
+    among them both sides of every chunk boundary of the benchmarked schedule.  C3 runs on the Halton
+    sampler (the reference has no Sobol sampler, F3); C4 is 3840x2160 at 1024 spp.  The raster and
+    spp fix the sample indices, so these are the benchmarked samples."""
     mesh = scenes.dragon_standin()
     mesh = (mesh[0], mesh[1], "standin:displaced-uv-sphere-224")
     out = {}
@@ -251,7 +286,8 @@ def fullsize_cases():
                            ("c4", scenes.config_c4, 4), ("c5", scenes.config_c5, 5)):
         s, rd = fn(mesh=mesh)
         cam = rd.camera
-        tiles = fullsize_pixels(cam.width, cam.height, seed=seed)
+        starts = default_chunk_starts(cam.width * cam.height, rd.spp, rd.integrator, rd.max_depth)
+        tiles = fullsize_pixels(cam.width, cam.height, n=FULLSIZE_PIXELS, seed=seed, boundaries=starts[1:])
         out[name] = (s, scenes.render_desc(cam, rd.integrator, rd.spp, rd.max_depth, rd.rr_threshold,
                                            rd.light_strategy, capi.SAMPLER_HALTON, tiles=tiles))
     return out

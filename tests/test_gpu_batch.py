@@ -113,3 +113,25 @@ def test_batch_refusals(hip):
     import ctypes as C
     rc = hip.lib.pbr_hip_render_frames(hip.ctx, C.byref(rd), 0, None, None)
     assert rc == capi.PBR_E_INVALID
+
+
+def test_batch_of_frames_at_the_chunk_cap_bounds_lane_memory(hip):
+    """A one-chunk Path frame at the 2^26-sample cap (256x256 at 1024 spp): a batch rotates such frames
+    over as many lanes as fit the lane budget (wf_chunks' kBatchLaneBytes: two here, ≈ 24 GB each), not
+    over all three, and every frame is still the single call's bits."""
+    s, rd = scenes.config_c4(256, 256, 1024, mesh=small_dragon(40))
+    npx = 256 * 256
+    hip.upload(s)
+    hip.set_schedule()
+    free0, _ = torch.cuda.mem_get_info(0)
+    ref, ref8, _ = hip.render(rd)   # one lane
+    stream = torch.cuda.Stream(torch.device("cuda", 0))
+    rgbs, rgbas = batch(hip, rd, npx, 3, stream)
+    hip.sync()
+    torch.cuda.synchronize()
+    used = (free0 - torch.cuda.mem_get_info(0)[0]) / 1e9
+    print(f"lane buffers + outputs after the batch: {used:.1f} GB")
+    assert used < 60, f"{used:.1f} GB: the batch kept more lanes than the budget allows"
+    for f in range(3):
+        assert np.array_equal(rgbs[f].cpu().numpy().view(np.uint32), ref.reshape(npx, 3).view(np.uint32)), f"frame {f}"
+        assert np.array_equal(rgbas[f].cpu().numpy(), ref8.reshape(npx, 4)), f"frame {f}"

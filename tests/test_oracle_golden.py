@@ -171,3 +171,23 @@ def test_sobol_samples_land_in_their_pixel():
     assert np.all((v >= 0) & (v < 1))
     # distinct samples of one pixel have distinct indices with the sample number in the high bits
     assert np.all(idx.reshape(-1, 16, 2)[:, :, 0] >> 18 == np.arange(16))
+
+
+def test_oracle_adopts_a_caller_built_tree():
+    """pbr_scene_desc::bvh_nodes on the oracle: the reference's BVHAccel node array with the primitives
+    in its leaf order renders the same bits as the oracle's own build over the original order (the
+    parity harness renders the reference-side binding's flattened scenes this way)."""
+    m = scenes.dragon_standin(n=24)
+    s = scenes.Scene()
+    s.mesh(m[0], m[1], s.matte((0.3, 0.7, 0.2)))
+    s.point_light((1.0, 2.0, 2.0), (6.0, 6.0, 6.0))
+    cam = scenes.camera(48, 32, (0.0, 0.4, 2.6), (0.0, 0.0, 0.0))
+    rd = scenes.render_desc(cam, capi.INTEGRATOR_WHITTED, 4, 5)
+    cn, ci = O.build_bvh(s)
+    want, want8, _ = O.render(s, rd)
+    leaf = scenes.Scene()
+    leaf.mesh(m[0], np.ascontiguousarray(m[1][ci]), leaf.matte((0.3, 0.7, 0.2)))
+    leaf.point_light((1.0, 2.0, 2.0), (6.0, 6.0, 6.0))
+    leaf.bvh_nodes = cn
+    got, got8, _ = O.render(leaf, rd)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)) and np.array_equal(got8, want8)

@@ -11,17 +11,22 @@ textures' and InfiniteAreaLight's MIPMap level 0, its camera's RasterToCamera) i
 renders through the C-ABI.  Besides the 8-bit FrameBuffers, the reference's float colObj / spp comes
 from its per-pixel body on the same objects and the drop-in's from the FrameBuffer's float buffer.
 
-Bar (tests/parity.py's, against the reference itself): the device walks the reference's own tree;
-wherever a float pixel is bit-identical its FrameBuffer bytes are identical; the float pixels that
-are not differ by a last-bit libm difference (glibc's float sinf/expf/logf/powf in the reference,
-correctly rounded transcendentals on the device) or — rarely — by one sample's flipped
-discrete decision (Russian roulette, a lobe or medium-event choice), so at most 2% of the pixels may
-differ by one 8-bit step and at most 0.1% by more."""
+Bar, against the reference itself, with every difference accounted for.  The binding's own flattened
+scene and descriptor are also rendered by the oracle (correctly rounded transcendentals, as the
+device) and by its libm twin (glibc's float sinf/expf/logf/... as the reference calls them):
+- the drop-in's float pixels ARE the oracle's, bit for bit, and the reference's ARE the libm twin's;
+- on every pixel where the oracle and its twin agree (libm's last bits never reached its samples) the
+  drop-in IS the reference, float and RGBA8, bit for bit — inside north_star's per-pixel L∞ 1e-3;
+- the few remaining pixels carry a libm last bit, or a path it diverted, and are bounded by the
+  measured shares (MIN_WITHIN of the pixels within L∞ 1e-3, MIN_EXACT bit-identical), the RGBA8 bytes
+  identical wherever the float pixel is, at most 2% one 8-bit step and 0.1% more."""
 import ctypes as C
 import os
 
 import numpy as np
 import pytest
+
+from parity import LINF
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "_ref", "libpbr_refbind.so")
@@ -35,6 +40,9 @@ def lib():
     L.refbind_render.restype = C.c_int
     L.refbind_render.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_char_p, C.c_int]
+    L.refbind_render_oracles.restype = C.c_int
+    L.refbind_render_oracles.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_char_p, C.c_int]
     L.refbind_flatten.restype = C.c_int
     L.refbind_flatten.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p,
                                   C.c_int]
@@ -93,6 +101,31 @@ def render(config, res, spp):
     return rc, err.value.decode(), ref, hip, ref_rgb, hip_rgb, same_tree.value, secs
 
 
+# measured on the GPU box (profiles/r6_gpu_tests.log, -s), floors just under: share of the 128x128
+# float pixels bit-identical to the reference's (2: 0.9982, 3: 0.9895, 4: 0.9939, 5: 0.9875,
+# 6: 0.7532 — the InfiniteAreaLight's atan2/acos per lookup, 7: 0.9987) and within L∞ 1e-3 (every
+# pixel but 2 of config 4 and 7 of config 5: paths that diverged on a libm last bit)
+MIN_EXACT = {2: 0.997, 3: 0.985, 4: 0.99, 5: 0.98, 6: 0.74, 7: 0.997}
+MIN_WITHIN = {2: 1.0, 3: 1.0, 4: 0.9995, 5: 0.999, 6: 1.0, 7: 1.0}
+
+
+def oracles(config, res, spp):
+    """The binding's flattened scene rendered by oracle/liboracle.so and its libm twin (res·res x 3)."""
+    import oracle_lib as O
+    twin_lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle_libm.so"))   # (built with liboracle.so)
+
+    def fn(so):
+        return C.cast(so.oracle_render, C.c_void_p)
+    ora = np.zeros(res * res * 3, np.float32)
+    twin = np.zeros(res * res * 3, np.float32)
+    err = C.create_string_buffer(512)
+    L = lib()
+    rc = L.refbind_render_oracles(config, res, spp, fn(O.load()), fn(twin_lib), ora.ctypes.data, twin.ctypes.data,
+                                  err, 512)
+    assert rc == 0, err.value.decode()
+    return ora.reshape(-1, 3), twin.reshape(-1, 3)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,res,spp", [(2, 128, 8), (3, 128, 16), (4, 128, 16), (5, 128, 8), (6, 128, 16),
                                             (7, 128, 8)])
@@ -108,15 +141,32 @@ def test_reference_render_equals_binding_render(config, res, spp):
     assert np.isfinite(hf).all()
     same_f = np.all(rf.view(np.uint32) == hf.view(np.uint32), axis=1)
     d8 = np.abs(r8 - h8).max(axis=1)
-    print(f"config {config}: {same_f.mean():.4f} of the float pixels bit-identical, u8: {(d8 == 0).mean():.4f} "
-          f"identical, {int((d8 == 1).sum())} one step, {int((d8 > 1).sum())} more (max {int(d8.max())}); "
-          f"float L∞ {float(np.abs(rf - hf).max()):.3g}; reference {secs[0]:.2f} s, binding {secs[1]:.3f} s")
+    dF = np.abs(rf.astype(np.float64) - hf.astype(np.float64)).max(axis=1)
+    within = float(np.mean(dF <= LINF))
+    print(f"config {config}: {same_f.mean():.4f} of the float pixels bit-identical, {within:.4f} within L∞ {LINF}, "
+          f"u8: {(d8 == 0).mean():.4f} identical, {int((d8 == 1).sum())} one step, {int((d8 > 1).sum())} more "
+          f"(max {int(d8.max())}); float L∞ {float(dF.max()):.3g}; reference {secs[0]:.2f} s, binding {secs[1]:.3f} s")
+    # Where do the differences come from?  The binding's own flattened scene and descriptor rendered by
+    # the oracle (correctly rounded transcendentals) and by its libm twin (glibc's sinf, expf, ... as
+    # the reference calls them): the device IS the oracle and the libm twin IS the reference, bit for
+    # bit, so the only difference between the drop-in and the reference is libm's last bits.
+    ora, twin = oracles(config, res, spp)
+    assert np.array_equal(hf.view(np.uint32), ora.view(np.uint32)), "the drop-in's floats differ from the oracle's"
+    assert np.array_equal(rf.view(np.uint32), twin.view(np.uint32)), "the reference's floats differ from the libm twin's"
+    # On every pixel whose samples libm's last bits never reached (the oracle and its twin agree there)
+    # the drop-in IS the reference, bit for bit — far inside north_star's L∞ 1e-3; the measured shares
+    # are floors
+    untouched = np.all(ora.view(np.uint32) == twin.view(np.uint32), axis=1)
+    assert np.array_equal(hf[untouched].view(np.uint32), rf[untouched].view(np.uint32)), \
+        f"a pixel libm does not explain differs (L∞ {dF[untouched].max():.3g})"
+    print(f"config {config}: {untouched.mean():.4f} of the pixels untouched by libm's last bits")
+    assert within >= MIN_WITHIN[config], f"only {within:.4f} of the float pixels within L∞ {LINF} (max {dF.max():.3g})"
+    assert same_f.mean() >= MIN_EXACT[config], f"only {same_f.mean():.4f} of the float pixels bit-identical"
     assert (r8[:, 3] == 255).all() and (h8[:, 3] == 255).all()
     assert (d8[same_f] == 0).all(), "8-bit output differs where the float pixel is bit-identical"
     n = d8.size
     assert (d8 == 1).sum() <= 0.02 * n, f"{int((d8 == 1).sum())} pixels differ by one step"
     assert (d8 > 1).sum() <= 0.001 * n, f"{int((d8 > 1).sum())} pixels differ by more than one step"
-    assert same_f.mean() >= 0.5, f"only {same_f.mean():.4f} of the float pixels bit-identical"
     assert r8[:, :3].std() > 1.0   # a real image, not a blank frame
 
 
