@@ -221,21 +221,27 @@ __device__ __forceinline__ bool prim_hit(const DeviceScene& S, int slot, const R
 // the node's split axis) so ties between primitives resolve exactly as on the CPU (F8).
 // The slab part of node_hit: everything but the final (tMin < ray.tMax), which is the only term
 // that depends on ray.tMax.  Returns false where node_hit would whatever ray.tMax is.
-__device__ __forceinline__ bool node_slab(f3 lo, f3 hi, const Ray& r, f3 inv, bool n0, bool n1, bool n2, float* tEnter) {
-    float tMin = ((n0 ? hi.x : lo.x) - r.o.x) * inv.x;
-    float tMax = ((n0 ? lo.x : hi.x) - r.o.x) * inv.x;
-    float tyMin = ((n1 ? hi.y : lo.y) - r.o.y) * inv.y;
-    float tyMax = ((n1 ? lo.y : hi.y) - r.o.y) * inv.y;
+// node_slab on the box's near and far planes, already picked by the direction signs (nr = the
+// planes the ray enters through: hi on a negative axis, lo on a positive one; fr the others).
+__device__ __forceinline__ bool slab_nf(f3 nr, f3 fr, const Ray& r, f3 inv, float* tEnter) {
+    float tMin = (nr.x - r.o.x) * inv.x;
+    float tMax = (fr.x - r.o.x) * inv.x;
+    float tyMin = (nr.y - r.o.y) * inv.y;
+    float tyMax = (fr.y - r.o.y) * inv.y;
     if (tMin > tyMax || tyMin > tMax) return false;
     if (tyMin > tMin) tMin = tyMin;
     if (tyMax < tMax) tMax = tyMax;
-    float tzMin = ((n2 ? hi.z : lo.z) - r.o.z) * inv.z;
-    float tzMax = ((n2 ? lo.z : hi.z) - r.o.z) * inv.z;
+    float tzMin = (nr.z - r.o.z) * inv.z;
+    float tzMax = (fr.z - r.o.z) * inv.z;
     if (tMin > tzMax || tzMin > tMax) return false;
     if (tzMin > tMin) tMin = tzMin;
     if (tzMax < tMax) tMax = tzMax;
     *tEnter = tMin;
     return tMax > 0;
+}
+__device__ __forceinline__ bool node_slab(f3 lo, f3 hi, const Ray& r, f3 inv, bool n0, bool n1, bool n2, float* tEnter) {
+    return slab_nf(mk(n0 ? hi.x : lo.x, n1 ? hi.y : lo.y, n2 ? hi.z : lo.z),
+                   mk(n0 ? lo.x : hi.x, n1 ? lo.y : hi.y, n2 ? lo.z : hi.z), r, inv, tEnter);
 }
 
 // Short traversal stack in LDS for the 256-lane wavefront kernels: entries [0, SHORT) live in LDS
@@ -319,38 +325,95 @@ struct QuadSlots {   // one quad node's four slots in visit order
 // A quad node's four slots from its fetched 128 B (LX..HZ: SoA boxes, R: child refs, meta: axes,
 // valid mask).
 template <bool ANY>
-__device__ __forceinline__ void quad_slots_of(float4 LX, float4 LY, float4 LZ, float4 HX, float4 HY, float4 HZ, float4 R,
+__device__ __forceinline__ void quad_slots_nf(float4 NX, float4 NY, float4 NZ, float4 FX, float4 FY, float4 FZ, float4 R,
                                               int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q);
+// PBR_NF_ROWS: the near and far planes of a quad node are fetched as rows picked by the direction
+// signs (a lane walking alone: per-lane row addresses; a packet: the wave's common signs, scalar
+// addresses) instead of fetching lo and hi and picking each value with a select — the same floats
+// reach the same operations, so the results are the same bits, with 24 VALU selects fewer per node
+// (4 slots × 3 axes × near/far).  Per-lane row addresses take more VGPRs: the lane-refill walks
+// (NF = true) have the room; the plain per-lane walk (traverse_quad: Whitted's shadow rays at 8
+// waves per SIMD, 60 VGPRs) spilled with them (6 VGPRs) and keeps the selects.
+#ifndef PBR_NF_ROWS
+#define PBR_NF_ROWS 1
+#endif
 template <bool ANY>
+__device__ __forceinline__ void quad_slots_lohi(float4 LX, float4 LY, float4 LZ, float4 HX, float4 HY, float4 HZ, float4 R,
+                                                int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q);
+template <bool ANY, bool NF = false>
 __device__ __forceinline__ void quad_slots(const DeviceScene& S, int cur, const Ray& r, f3 inv, bool n0, bool n1, bool n2,
                                            QuadSlots* q) {
-    float4 LX, LY, LZ, HX, HY, HZ, R;
+    if constexpr (!NF || !PBR_NF_ROWS) {   // lo and hi fetched, each plane picked per slot (node_slab)
+        float4 LX, LY, LZ, HX, HY, HZ, R;
+        int meta;
+        const int ucur = __builtin_amdgcn_readfirstlane(cur);
+        if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
+            const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
+            LX = as_f4(w[0]); LY = as_f4(w[1]); LZ = as_f4(w[2]); HX = as_f4(w[3]); HY = as_f4(w[4]);
+            HZ = as_f4(w[5]); R = as_f4(w[6]);
+            meta = __float_as_int(w[7].x);
+        } else {
+            const float4* w = S.quad + 8 * (size_t)cur;
+            LX = w[0]; LY = w[1]; LZ = w[2]; HX = w[3]; HY = w[4]; HZ = w[5]; R = w[6];
+            meta = __float_as_int(w[7].x);
+        }
+        quad_slots_lohi<ANY>(LX, LY, LZ, HX, HY, HZ, R, meta, r, inv, n0, n1, n2, q);
+        return;
+    }
+    float4 NX, NY, NZ, FX, FY, FZ, R;
     int meta;
     // Coherent waves (a pixel's samples share a wave) often have every active lane at the
     // same node: then it is fetched once through the scalar cache.
     const int ucur = __builtin_amdgcn_readfirstlane(cur);
     if (kScalarLoads && __builtin_amdgcn_ballot_w64(cur != ucur) == 0ull) {
         const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)ucur);
-        LX = as_f4(w[0]); LY = as_f4(w[1]); LZ = as_f4(w[2]); HX = as_f4(w[3]); HY = as_f4(w[4]);
-        HZ = as_f4(w[5]); R = as_f4(w[6]);
+        const float4 LX = as_f4(w[0]), LY = as_f4(w[1]), LZ = as_f4(w[2]), HX = as_f4(w[3]), HY = as_f4(w[4]),
+                     HZ = as_f4(w[5]);
+        NX = n0 ? HX : LX; FX = n0 ? LX : HX;
+        NY = n1 ? HY : LY; FY = n1 ? LY : HY;
+        NZ = n2 ? HZ : LZ; FZ = n2 ? LZ : HZ;
+        R = as_f4(w[6]);
         meta = __float_as_int(w[7].x);
     } else {
         const float4* w = S.quad + 8 * (size_t)cur;
-        LX = w[0]; LY = w[1]; LZ = w[2]; HX = w[3]; HY = w[4]; HZ = w[5]; R = w[6];
+        // rows 0-2: lo.x/y/z, 3-5: hi.x/y/z of the four slots
+        NX = w[n0 ? 3 : 0]; FX = w[n0 ? 0 : 3];
+        NY = w[n1 ? 4 : 1]; FY = w[n1 ? 1 : 4];
+        NZ = w[n2 ? 5 : 2]; FZ = w[n2 ? 2 : 5];
+        R = w[6];
         meta = __float_as_int(w[7].x);
     }
-    quad_slots_of<ANY>(LX, LY, LZ, HX, HY, HZ, R, meta, r, inv, n0, n1, n2, q);
+    quad_slots_nf<ANY>(NX, NY, NZ, FX, FY, FZ, R, meta, r, inv, n0, n1, n2, q);
 }
 template <bool ANY>
-__device__ __forceinline__ void quad_slots_of(float4 LX, float4 LY, float4 LZ, float4 HX, float4 HY, float4 HZ, float4 R,
-                                              int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q) {
-    // (The two-slot pairs written as packed fp32 — v_pk_add/v_pk_mul — measured slower: 8-9 more
-    // VGPRs, C4-material extend 119.5 → 129.0 ms; profiles/r5_slp_ab.log.)
+__device__ __forceinline__ void quad_order(bool k0, bool k1, bool k2, bool k3, float t0, float t1, float t2, float t3,
+                                           float4 R, int meta, bool n0, bool n1, bool n2, QuadSlots* q);
+template <bool ANY>
+__device__ __forceinline__ void quad_slots_lohi(float4 LX, float4 LY, float4 LZ, float4 HX, float4 HY, float4 HZ, float4 R,
+                                                int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q) {
     float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
     bool k0 = node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t0) & ((meta >> 8) & 1);
     bool k1 = node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t1) & ((meta >> 9) & 1);
     bool k2 = node_slab(mk(LX.z, LY.z, LZ.z), mk(HX.z, HY.z, HZ.z), r, inv, n0, n1, n2, &t2) & ((meta >> 10) & 1);
     bool k3 = node_slab(mk(LX.w, LY.w, LZ.w), mk(HX.w, HY.w, HZ.w), r, inv, n0, n1, n2, &t3) & ((meta >> 11) & 1);
+    quad_order<ANY>(k0, k1, k2, k3, t0, t1, t2, t3, R, meta, n0, n1, n2, q);
+}
+template <bool ANY>
+__device__ __forceinline__ void quad_slots_nf(float4 NX, float4 NY, float4 NZ, float4 FX, float4 FY, float4 FZ, float4 R,
+                                              int meta, const Ray& r, f3 inv, bool n0, bool n1, bool n2, QuadSlots* q) {
+    // (The two-slot pairs written as packed fp32 — v_pk_add/v_pk_mul — measured slower: 8-9 more
+    // VGPRs, C4-material extend 119.5 → 129.0 ms; profiles/r5_slp_ab.log.)
+    float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    bool k0 = slab_nf(mk(NX.x, NY.x, NZ.x), mk(FX.x, FY.x, FZ.x), r, inv, &t0) & ((meta >> 8) & 1);
+    bool k1 = slab_nf(mk(NX.y, NY.y, NZ.y), mk(FX.y, FY.y, FZ.y), r, inv, &t1) & ((meta >> 9) & 1);
+    bool k2 = slab_nf(mk(NX.z, NY.z, NZ.z), mk(FX.z, FY.z, FZ.z), r, inv, &t2) & ((meta >> 10) & 1);
+    bool k3 = slab_nf(mk(NX.w, NY.w, NZ.w), mk(FX.w, FY.w, FZ.w), r, inv, &t3) & ((meta >> 11) & 1);
+    quad_order<ANY>(k0, k1, k2, k3, t0, t1, t2, t3, R, meta, n0, n1, n2, q);
+}
+// the four slots in visit order (closest hit) or build order (any hit)
+template <bool ANY>
+__device__ __forceinline__ void quad_order(bool k0, bool k1, bool k2, bool k3, float t0, float t1, float t2, float t3,
+                                           float4 R, int meta, bool n0, bool n1, bool n2, QuadSlots* q) {
     int r0 = __float_as_int(R.x), r1 = __float_as_int(R.y), r2 = __float_as_int(R.z), r3 = __float_as_int(R.w);
     auto swp = [](bool c, auto& a, auto& b) { auto x = c ? b : a; b = c ? a : b; a = x; };
     auto neg = [&](int axis) { return axis == 0 ? n0 : (axis == 1 ? n1 : n2); };
@@ -518,15 +581,28 @@ __device__ bool traverse_packet(const DeviceScene& S, Ray& r, HitRec* h, f3 inv,
             if (ANY && __builtin_amdgcn_ballot_w64(alive) == 0ull) break;
         } else {
             const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)cur);
-            const float4 LX = as_f4(w[0]), LY = as_f4(w[1]), LZ = as_f4(w[2]), HX = as_f4(w[3]), HY = as_f4(w[4]),
-                         HZ = as_f4(w[5]), R = as_f4(w[6]);
+            // near / far plane rows (PBR_NF_ROWS): closest hit picks them by the wave's common signs
+            // with scalar addresses — no selects; any hit keeps each lane's own signs
+            float4 NX, NY, NZ, FX, FY, FZ;
+            if constexpr (!ANY && PBR_NF_ROWS) {
+                NX = as_f4(w[u0 ? 3 : 0]); FX = as_f4(w[u0 ? 0 : 3]);
+                NY = as_f4(w[u1 ? 4 : 1]); FY = as_f4(w[u1 ? 1 : 4]);
+                NZ = as_f4(w[u2 ? 5 : 2]); FZ = as_f4(w[u2 ? 2 : 5]);
+            } else {
+                const float4 LX = as_f4(w[0]), LY = as_f4(w[1]), LZ = as_f4(w[2]), HX = as_f4(w[3]), HY = as_f4(w[4]),
+                             HZ = as_f4(w[5]);
+                NX = n0 ? HX : LX; FX = n0 ? LX : HX;
+                NY = n1 ? HY : LY; FY = n1 ? LY : HY;
+                NZ = n2 ? HZ : LZ; FZ = n2 ? LZ : HZ;
+            }
+            const float4 R = as_f4(w[6]);
             const int meta = __float_as_int(w[7].x);
             float t[4] = {0.f, 0.f, 0.f, 0.f};
             bool p[4];
-            p[0] = active && node_slab(mk(LX.x, LY.x, LZ.x), mk(HX.x, HY.x, HZ.x), r, inv, n0, n1, n2, &t[0]) && ((meta >> 8) & 1) && t[0] < r.tMax;
-            p[1] = active && node_slab(mk(LX.y, LY.y, LZ.y), mk(HX.y, HY.y, HZ.y), r, inv, n0, n1, n2, &t[1]) && ((meta >> 9) & 1) && t[1] < r.tMax;
-            p[2] = active && node_slab(mk(LX.z, LY.z, LZ.z), mk(HX.z, HY.z, HZ.z), r, inv, n0, n1, n2, &t[2]) && ((meta >> 10) & 1) && t[2] < r.tMax;
-            p[3] = active && node_slab(mk(LX.w, LY.w, LZ.w), mk(HX.w, HY.w, HZ.w), r, inv, n0, n1, n2, &t[3]) && ((meta >> 11) & 1) && t[3] < r.tMax;
+            p[0] = active && slab_nf(mk(NX.x, NY.x, NZ.x), mk(FX.x, FY.x, FZ.x), r, inv, &t[0]) && ((meta >> 8) & 1) && t[0] < r.tMax;
+            p[1] = active && slab_nf(mk(NX.y, NY.y, NZ.y), mk(FX.y, FY.y, FZ.y), r, inv, &t[1]) && ((meta >> 9) & 1) && t[1] < r.tMax;
+            p[2] = active && slab_nf(mk(NX.z, NY.z, NZ.z), mk(FX.z, FY.z, FZ.z), r, inv, &t[2]) && ((meta >> 10) & 1) && t[2] < r.tMax;
+            p[3] = active && slab_nf(mk(NX.w, NY.w, NZ.w), mk(FX.w, FY.w, FZ.w), r, inv, &t[3]) && ((meta >> 11) & 1) && t[3] < r.tMax;
             const unsigned long long bm[4] = {__builtin_amdgcn_ballot_w64(p[0]), __builtin_amdgcn_ballot_w64(p[1]),
                                               __builtin_amdgcn_ballot_w64(p[2]), __builtin_amdgcn_ballot_w64(p[3])};
             // visit position → slot column (quad_slots' swaps; any hit: build order)
@@ -572,15 +648,28 @@ __device__ bool traverse_packet(const DeviceScene& S, Ray& r, HitRec* h, f3 inv,
             const unsigned long long m = smask[sp];   // a uniform LDS address: the same value in every lane
             const int parent = e >> 2, c = e & 3;
             const ScalarF4Ptr w = scalar_f4(S.quad + 8 * (size_t)parent);
-            const float4 LX = as_f4(w[0]), LY = as_f4(w[1]), LZ = as_f4(w[2]), HX = as_f4(w[3]), HY = as_f4(w[4]),
-                         HZ = as_f4(w[5]), R = as_f4(w[6]);
-            auto pick = [c](float4 v) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
+            // the slot's one box: its six floats are scalars, column c of each row (PBR_NF_ROWS:
+            // the rows picked by the wave's common signs, scalar addresses, as above)
+            const float* wf = (const float*)(S.quad + 8 * (size_t)parent);
+            f3 nr, fr;
+            if constexpr (!ANY && PBR_NF_ROWS) {
+                const __attribute__((address_space(4))) float* sf = (const __attribute__((address_space(4))) float*)(size_t)wf;
+                nr = mk(sf[(u0 ? 12 : 0) + c], sf[(u1 ? 16 : 4) + c], sf[(u2 ? 20 : 8) + c]);
+                fr = mk(sf[(u0 ? 0 : 12) + c], sf[(u1 ? 4 : 16) + c], sf[(u2 ? 8 : 20) + c]);
+            } else {
+                auto pick = [c](float4 v) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
+                const f3 lo = mk(pick(as_f4(w[0])), pick(as_f4(w[1])), pick(as_f4(w[2])));
+                const f3 hi = mk(pick(as_f4(w[3])), pick(as_f4(w[4])), pick(as_f4(w[5])));
+                nr = mk(n0 ? hi.x : lo.x, n1 ? hi.y : lo.y, n2 ? hi.z : lo.z);
+                fr = mk(n0 ? lo.x : hi.x, n1 ? lo.y : hi.y, n2 ? lo.z : hi.z);
+            }
+            const __attribute__((address_space(4))) float* rf = (const __attribute__((address_space(4))) float*)(size_t)(wf + 24);
             float tt = 0.f;
             bool a = (m & lanebit) != 0ull && (!ANY || alive);
-            a = a && node_slab(mk(pick(LX), pick(LY), pick(LZ)), mk(pick(HX), pick(HY), pick(HZ)), r, inv, n0, n1, n2, &tt) && tt < r.tMax;
+            a = a && slab_nf(nr, fr, r, inv, &tt) && tt < r.tMax;
             if (__builtin_amdgcn_ballot_w64(a) != 0ull) {
                 active = a;
-                cur = __builtin_amdgcn_readfirstlane(__float_as_int(pick(R)));
+                cur = __builtin_amdgcn_readfirstlane(__float_as_int(rf[c]));
                 more = true;
                 break;
             }

@@ -1277,10 +1277,14 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, const FrameSet
     // chunks than lanes (rank shards of a multi-GPU C2 job) keep the separate kernels by default:
     // there the camera kernel's 8 waves per SIMD win (C2 shard 0/8, one chunk: 2.58 → 3.10 ms fused;
     // shard 0/2, two chunks: 9.58-9.63 → 10.12-10.22).
+    // Round 6: a batch whose few-chunk frames rotate over the lanes (a rank's shard) fuses as well — its
+    // frames overlap on the lanes, which hides the fused kernel's lower occupancy: C2 8-rank shards
+    // 2.10-2.19 → 1.99-2.02 ms, 4-rank 4.13-4.31 → 3.95-4.01 (profiles/r6_shard_c2*.json).
     const long long nChunks = (P.nPixels + ch.chunkPix - 1) / ch.chunkPix;
     const int fuse = ctx->sched.fuse_camera;
+    const bool rotating = F.batch && nChunks < ch.lanes;
     const bool fuseCamera = kPacket && kQuadTraversal && fuse != PBR_FUSE_OFF && (mm || simple) && matsLds && !textured &&
-                            !ml && (nChunks >= std::max(2, ch.lanes) || fuse == PBR_FUSE_ON);
+                            !ml && (nChunks >= std::max(2, ch.lanes) || fuse == PBR_FUSE_ON || rotating);
     // + pass-through levels only when some primitive has no material (Whitted's no-BSDF branch)
     const int maxLevels = levels;   // no material-less primitives here (those scenes run the megakernel)
     // Shadow rays of level L run on a second stream, overlapping extend(L+1) and shade(L+1) (they

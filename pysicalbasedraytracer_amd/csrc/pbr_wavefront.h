@@ -316,7 +316,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             }
         } else {
             QuadSlots q;
-            quad_slots<ANY>(S, cur, r, inv, n0, n1, n2, &q);
+            quad_slots<ANY, true>(S, cur, r, inv, n0, n1, n2, &q);
             const float tM = r.tMax;
             const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
                        p3 = q.k[3] && q.t[3] < tM;

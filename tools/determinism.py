@@ -3,7 +3,7 @@ contexts, in different orders, with device memory filled with junk and handed ba
 between (hipMalloc'd queues of a new context may then start out as that junk), and prints each
 frame's hash.  Every hash of one scene must be the same.
 
-    python tools/r5_determinism.py [--w 960 --h 540 --spp 256] [--junk-gb 64]
+    python tools/determinism.py [--w 960 --h 540 --spp 256] [--junk-gb 64]
 """
 import argparse
 import hashlib

@@ -4,7 +4,7 @@
 
 bench.py's `roofline.kernels` come from its serial window (one lane, shadow rays on the render
 stream: every kernel runs alone) timed with HIP events.  The CSV is `rocprofv3 --kernel-trace
---stats` of `bench.py --serial` on the same build (tools/r4_measure.sh).  For each family this prints
+--stats` of `bench.py --serial` on the same build (tools/archive/r4_measure.sh).  For each family this prints
 the launches' mean duration from the CSV (all template instances of the family's kernel), the
 family's algorithmic bytes per launch from the bench line, the resulting GB/s and fraction of the
 8 TB/s peak, and the bench line's own figures beside them."""

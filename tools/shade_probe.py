@@ -1,7 +1,7 @@
 """How much of the Path shade's cost is material divergence?  C4's scene with the three dragons'
 materials varied (mixed as in C4, or all one recipe), serial schedule, per-family ns per unit.
 
-    python tools/r5_shade_probe.py [--w 1920 --h 1080 --spp 256] [--lib path]
+    python tools/shade_probe.py [--w 1920 --h 1080 --spp 256] [--lib path]
 """
 import argparse
 import hashlib

@@ -24,13 +24,22 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--ns", default="2,4,8")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--schedule", default="", help="pbr_hip_set_schedule for every render: comma-separated "
+                                                     "kernels=mega, chunk_log2=N, lanes=N, fuse=on|off (tune_wavefront.py)")
+    ap.add_argument("--lib", default=None, help="an experimental build of libpbr_hip.so")
     ap.add_argument("--batch", type=int, default=5, help="frames per pbr_hip_render_frames batch, as bench.py's "
                                                          "timed window (0: one pbr_hip_render per frame)")
     a = ap.parse_args()
+    if a.lib:
+        capi._lib = capi.load_library(a.lib)
     scene, rd = scenes.CONFIGS[a.config]()
     W, H, spp = rd.camera.width, rd.camera.height, rd.spp
     r = HipRenderer(0)
     r.upload(scene)
+    kw = dict(kv.split("=") for kv in a.schedule.split(",") if kv)
+    r.set_schedule(kernels=capi.KERNELS_MEGAKERNEL if kw.get("kernels") == "mega" else capi.KERNELS_AUTO,
+                   chunk_log2=int(kw.get("chunk_log2", 0)), lanes=int(kw.get("lanes", 0)),
+                   fuse_camera={"on": capi.FUSE_ON, "off": capi.FUSE_OFF}.get(kw.get("fuse"), capi.FUSE_AUTO))
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     nb = max(1, a.batch)
@@ -54,6 +63,7 @@ def main():
 
     full = timed(rd)
     out = {"config": a.config, "raster": [W, H], "spp": spp, "tile": a.tile, "full_ms": round(full, 3), "batch": a.batch,
+           "schedule": a.schedule or "default",
            "build": capi.load_library().pbr_hip_build_info().decode(), "ranks": {}}
     print(f"{a.config} whole frame {full:.2f} ms", flush=True)
     for n in (int(x) for x in a.ns.split(",")):
