@@ -44,6 +44,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 HBM_COPY_GBS = 6290.0        # measured device-to-device copy rate in the same guide
+# The chip's VALU issue rate in wave64 instructions per second: 256 CUs x 4 SIMD-32 units, a wave64
+# VALU instruction issues over 2 cycles, 2400 MHz (MI355X_MICROARCH.md, chip table and § Wave scheduling)
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 # SURVEY §8(d) per-sample model (32 B per node test, 48 per primitive test, 96 per ray, 64 per
 # shading event): reported for reference only — it counts cache-served BVH/mesh fetches as HBM
 # bytes, so it is not a bound
@@ -194,6 +197,30 @@ def kernel_family(name):
         if len(targs) >= 4 and targs[3] == "true":
             fam = "k_wf_shade_l0"
     return fam
+
+
+def family_counts(t, family):
+    """SQ / TCC counts per frame of one kernel family (summed over its template instances), or None."""
+    keys = ("valu_insts", "waves", "wave_cycles", "wait_any", "wait_inst_any", "active_inst_any", "tcc_hit", "tcc_miss")
+    out, hit = dict.fromkeys(keys, 0.0), False
+    for k, v in t["per_kernel"].items():
+        if kernel_family(k) == family and "valu_insts" in v:
+            for c in keys:
+                out[c] += v.get(c, 0.0)
+            hit = True
+    return out if hit else None
+
+
+def binding_bound(hbm_frac, issue_frac, wait_share):
+    """The bound a family sits on: the larger of its HBM and VALU-issue fractions once either passes
+    half of its peak; below that, 'latency' when its waves are parked on memory (s_waitcnt) for 40%
+    or more of their cycles; else the larger fraction.  Returns (bound, fraction of that bound)."""
+    h, i = hbm_frac or 0.0, issue_frac or 0.0
+    if max(h, i) >= 0.5:
+        return ("hbm", h) if h >= i else ("issue", i)
+    if wait_share is not None and wait_share >= 0.4:
+        return "latency", wait_share
+    return ("hbm", h) if h >= i else ("issue", i)
 
 
 def family_traffic(t, family):
@@ -398,6 +425,23 @@ def main():
                         k["traffic_per_launch"] = round(fb / lpf)
                         k["traffic_gbs"] = round(fb / lpf / (avg_ms * 1e-3) / 1e9, 1)
                         k["traffic_frac"] = round(k["traffic_gbs"] / HBM_PEAK_GBS, 4)
+                    # the issue side (VALU wave-instructions per frame over this window's time per
+                    # frame, against the chip's issue rate), the parked share of wave-cycles and
+                    # the L2 hit rate, from the same build's SQ / TCC passes
+                    cc = family_counts(pmc, fam)
+                    if cc is not None and tv["ms"] > 0:
+                        ms_frame = tv["ms"] / args.steps
+                        k["valu_insts_per_frame"] = round(cc["valu_insts"])
+                        k["valu_issue_frac"] = round(cc["valu_insts"] / (ms_frame * 1e-3) / VALU_ISSUE_PEAK, 4)
+                        wc = cc["wave_cycles"] or 1.0
+                        k["wait_any_share"] = round(cc["wait_any"] / wc, 3)
+                        k["issue_stall_share"] = round(cc["wait_inst_any"] / wc, 3)
+                        k["active_share"] = round(cc["active_inst_any"] / wc, 3)
+                        if cc["tcc_hit"] + cc["tcc_miss"] > 0:
+                            k["l2_hit"] = round(cc["tcc_hit"] / (cc["tcc_hit"] + cc["tcc_miss"]), 3)
+                        b, f = binding_bound(k.get("traffic_frac", k["frac"]), k["valu_issue_frac"], k["wait_any_share"])
+                        k["bound"] = b
+                        k["bound_frac"] = round(f, 4)
                 kernels[fam] = k
             return kernels
 
@@ -420,6 +464,15 @@ def main():
                     "unit": "GB/s", "frac": dk.get("frac"), "traffic": dk.get("traffic_per_launch"),
                     "frame": frame,
                     "traffic_gbs": dk.get("traffic_gbs"), "traffic_frac": dk.get("traffic_frac"),
+                    # what actually binds the dominant family (HBM bytes, VALU issue or memory
+                    # latency) and at what fraction: `frac` above prices it against HBM only
+                    "binding": ({"bound": dk["bound"], "frac": dk["bound_frac"], "hbm_frac": dk.get("traffic_frac", dk.get("frac")),
+                                 "valu_issue_frac": dk.get("valu_issue_frac"), "wait_any_share": dk.get("wait_any_share"),
+                                 "issue_stall_share": dk.get("issue_stall_share"), "l2_hit": dk.get("l2_hit"),
+                                 "valu_issue_peak": VALU_ISSUE_PEAK,
+                                 "rule": "hbm or issue when that fraction of its peak is >= 0.5 (the larger); below, "
+                                         "latency when >= 0.4 of the wave-cycles are parked (SQ_WAIT_ANY); else the "
+                                         "larger fraction"} if dk.get("bound") else None),
                     "copy_peak_gbs": HBM_COPY_GBS,
                     "frac_of_copy_peak": round(dk["achieved_gbs"] / HBM_COPY_GBS, 4) if dk.get("achieved_gbs") else None,
                     "alg_bytes_per_launch": dk.get("alg_bytes_per_launch"), "avg_launch_us": dk.get("avg_launch_us"),

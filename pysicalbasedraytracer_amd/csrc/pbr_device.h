@@ -899,6 +899,13 @@ PBR_HD float tr_lambda(const Lobe& l, f3 w) {
 }
 PBR_HD float tr_G1(const Lobe& l, f3 w) { return 1 / (1 + tr_lambda(l, w)); }
 PBR_HD float tr_G(const Lobe& l, f3 wo, f3 wi) { return 1 / (1 + tr_lambda(l, wo) + tr_lambda(l, wi)); }
+// Lambda(wo) handed down by a caller that evaluated it once for a shading event (lamWo: NaN = not
+// given).  A material's microfacet lobes share (ax, ay) — one lobe, or a rough dielectric's reflection
+// and transmission built from the same roughness — and wo is fixed for the event, so the light
+// sample's f and pdf, the BSDF sample's pdf and the sum of f over the lobes all read one value, the
+// same bits each would compute (C4/C5: 2-6 evaluations of Lambda(wo) per event before).
+constexpr float kNoLambda = __builtin_nanf("");
+PBR_HD float lam_or(const Lobe& l, f3 wo, float lamWo) { return lamWo == lamWo ? lamWo : tr_lambda(l, wo); }
 PBR_HD void tr_sample11(float cosTheta, float U1, float U2, float* sx, float* sy) {
     if ((double)cosTheta > .9999) {   // the reference's unqualified sqrt/cos/sin resolve to double
         float r = (float)sqrt((double)(U1 / (1 - U1)));
@@ -940,7 +947,9 @@ PBR_HD f3 tr_sample_wh(const Lobe& l, f3 wo, float u0, float u1) {
     if (flip) wh = -wh;
     return wh;
 }
-PBR_HD float tr_pdf(const Lobe& l, f3 wo, f3 wh) { return tr_D(l, wh) * tr_G1(l, wo) * absdot(wo, wh) / abscos_t(wo); }
+PBR_HD float tr_pdf(const Lobe& l, f3 wo, f3 wh, float lamWo = kNoLambda) {
+    return tr_D(l, wh) * (1 / (1 + lam_or(l, wo, lamWo))) * absdot(wo, wh) / abscos_t(wo);   // tr_G1(wo)
+}
 
 // K: bit mask of the LobeKinds the caller can meet (the scene's materials, or what a type filter
 // admits); kinds outside it compile out, which keeps the microfacet code out of simple kernels.
@@ -948,7 +957,7 @@ constexpr int kAllLobes = 0x7f;
 constexpr int kTexturedLobes = 0x80;   // LOBES flag of the shading kernels: some material has image textures
 #define PBR_HAS(K, kind) (((K) >> (kind)) & 1)
 template <int K = kAllLobes>
-PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
+PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi, float lamWo = kNoLambda) {
     switch (l.kind) {
     case L_LAMBERT: if constexpr (PBR_HAS(K, L_LAMBERT)) return ld3(l.R) * kInvPi; break;
     case L_OREN: if constexpr (PBR_HAS(K, L_OREN)) {
@@ -970,7 +979,7 @@ PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
         if (wh.x == 0 && wh.y == 0 && wh.z == 0) return sp(0.f);
         wh = normalize(wh);
         rgb F = fresnel_eval(l, dot(wi, faceforward(wh, mk(0, 0, 1))));
-        return ld3(l.R) * tr_D(l, wh) * tr_G(l, wo, wi) * F / (4 * cI * cO);
+        return ld3(l.R) * tr_D(l, wh) * (1 / (1 + lam_or(l, wo, lamWo) + tr_lambda(l, wi))) * F / (4 * cI * cO);   // tr_G
     } break;
     case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
         if (same_hemi(wo, wi)) return sp(0.f);
@@ -984,7 +993,8 @@ PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
         float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
         float factor = 1 / eta;
         return (sp(1.f) - F) * ld3(l.T) *
-               fabsf(tr_D(l, wh) * tr_G(l, wo, wi) * eta * eta * absdot(wi, wh) * absdot(wo, wh) * factor * factor /
+               fabsf(tr_D(l, wh) * (1 / (1 + lam_or(l, wo, lamWo) + tr_lambda(l, wi))) * eta * eta * absdot(wi, wh) *
+                     absdot(wo, wh) * factor * factor /
                      (cI * cO * sqrtDenom * sqrtDenom));
     } break;
     default: break;
@@ -992,7 +1002,7 @@ PBR_HD rgb lobe_f(const Lobe& l, f3 wo, f3 wi) {
     return sp(0.f);
 }
 template <int K = kAllLobes>
-PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
+PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi, float lamWo = kNoLambda) {
     switch (l.kind) {
     case L_LAMBERT: case L_OREN:
         if constexpr (PBR_HAS(K, L_LAMBERT) || PBR_HAS(K, L_OREN)) return same_hemi(wo, wi) ? abscos_t(wi) * kInvPi : 0;
@@ -1000,7 +1010,7 @@ PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
     case L_MF_R: if constexpr (PBR_HAS(K, L_MF_R)) {
         if (!same_hemi(wo, wi)) return 0;
         f3 wh = normalize(wo + wi);
-        return tr_pdf(l, wo, wh) / (4 * dot(wo, wh));
+        return tr_pdf(l, wo, wh, lamWo) / (4 * dot(wo, wh));
     } break;
     case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
         if (same_hemi(wo, wi)) return 0;
@@ -1009,7 +1019,7 @@ PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
         if (dot(wo, wh) * dot(wi, wh) > 0) return 0;
         float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
         float dwh = fabsf((eta * eta * dot(wi, wh)) / (sqrtDenom * sqrtDenom));
-        return tr_pdf(l, wo, wh) * dwh;
+        return tr_pdf(l, wo, wh, lamWo) * dwh;
     } break;
     default: break;
     }
@@ -1022,7 +1032,7 @@ PBR_HD float lobe_pdf(const Lobe& l, f3 wo, f3 wi) {
 // the two dot products change sign together.  wantF: the caller adds f (BSDF::f's reflect /
 // transmit filter); f is then exactly what lobe_f returns, black where it returns black.
 template <int K = kAllLobes>
-PBR_HD void lobe_f_pdf(const Lobe& l, f3 wo, f3 wi, bool wantF, rgb* fOut, float* pdfOut) {
+PBR_HD void lobe_f_pdf(const Lobe& l, f3 wo, f3 wi, bool wantF, rgb* fOut, float* pdfOut, float lamWo = kNoLambda) {
     rgb f = sp(0.f);
     float pdf = 0.f;
     switch (l.kind) {
@@ -1033,7 +1043,7 @@ PBR_HD void lobe_f_pdf(const Lobe& l, f3 wo, f3 wi, bool wantF, rgb* fOut, float
         const bool fLive = wantF && !(cI == 0 || cO == 0) && !(whRaw.x == 0 && whRaw.y == 0 && whRaw.z == 0);
         if (fLive || sh) {
             const f3 wh = normalize(whRaw);
-            const float D = tr_D(l, wh), lo = tr_lambda(l, wo);
+            const float D = tr_D(l, wh), lo = lam_or(l, wo, lamWo);
             if (fLive) {
                 const rgb F = fresnel_eval(l, dot(wi, faceforward(wh, mk(0, 0, 1))));
                 const float G = 1 / (1 + lo + tr_lambda(l, wi));   // tr_G
@@ -1048,7 +1058,7 @@ PBR_HD void lobe_f_pdf(const Lobe& l, f3 wo, f3 wi, bool wantF, rgb* fOut, float
         const float eta = cos_t(wo) > 0 ? (l.etaB / l.etaA) : (l.etaA / l.etaB);
         const f3 whp = normalize(wo + wi * eta);   // lobe_pdf's half vector
         if (dot(wo, whp) * dot(wi, whp) > 0) break;
-        const float D = tr_D(l, whp), lo = tr_lambda(l, wo);
+        const float D = tr_D(l, whp), lo = lam_or(l, wo, lamWo);
         const float cO = cos_t(wo), cI = cos_t(wi);
         if (wantF && !(cI == 0 || cO == 0)) {
             const f3 wh = whp.z < 0 ? -whp : whp;   // lobe_f's
@@ -1065,8 +1075,8 @@ PBR_HD void lobe_f_pdf(const Lobe& l, f3 wo, f3 wi, bool wantF, rgb* fOut, float
         break;
     } break;
     default:
-        if (wantF) f = lobe_f<K>(l, wo, wi);
-        pdf = lobe_pdf<K>(l, wo, wi);
+        if (wantF) f = lobe_f<K>(l, wo, wi, lamWo);
+        pdf = lobe_pdf<K>(l, wo, wi, lamWo);
         break;
     }
     *fOut = f;
@@ -1093,7 +1103,7 @@ PBR_HD f3 cosine_hemisphere(float u0, float u1) {
 // the diffuse and microfacet kinds the lobe's own f(wo, wi) — which the reference evaluates and
 // then drops — is not computed here (black is returned; wi and pdf are the reference's).
 template <int K = kAllLobes>
-PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* pdf, int* st) {
+PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* pdf, int* st, float lamWo = kNoLambda) {
     switch (l.kind) {
     case L_LAMBERT: case L_OREN: if constexpr (PBR_HAS(K, L_LAMBERT) || PBR_HAS(K, L_OREN)) {
         *wi = cosine_hemisphere(u0, u1);
@@ -1138,7 +1148,7 @@ PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* 
         if (dot(wo, wh) < 0) return sp(0.f);
         *wi = reflect_(wo, wh);
         if (!same_hemi(wo, *wi)) return sp(0.f);
-        *pdf = tr_pdf(l, wo, wh) / (4 * dot(wo, wh));
+        *pdf = tr_pdf(l, wo, wh, lamWo) / (4 * dot(wo, wh));
         return sp(0.f);   // (f: dropped by bsdf_sample)
     } break;
     case L_MF_T: if constexpr (PBR_HAS(K, L_MF_T)) {
@@ -1147,7 +1157,7 @@ PBR_HD rgb lobe_sample(const Lobe& l, f3 wo, f3* wi, float u0, float u1, float* 
         if (dot(wo, wh) < 0) return sp(0.f);
         float eta = cos_t(wo) > 0 ? (l.etaA / l.etaB) : (l.etaB / l.etaA);
         if (!refract_(wo, wh, eta, wi)) return sp(0.f);
-        *pdf = lobe_pdf<K>(l, wo, *wi);
+        *pdf = lobe_pdf<K>(l, wo, *wi, lamWo);
         return sp(0.f);   // (f: dropped by bsdf_sample)
     } break;
     default: break;
@@ -1170,6 +1180,22 @@ PBR_HD int num_components(const MatTemplate& mt, int flags) {
     return k;
 }
 PBR_HD int num_components(const BSDF& b, int flags) { return num_components(*b.mt, flags); }
+// Lambda(wo) of the BSDF's microfacet lobes for a local wo, evaluated once (kNoLambda when it has
+// none, or — never for the reference's materials — lobes of different alphas, which then evaluate
+// their own)
+template <int K = kAllLobes>
+PBR_HD float mf_lambda(const BSDF& b, f3 wo) {
+    if constexpr (!(PBR_HAS(K, L_MF_R) || PBR_HAS(K, L_MF_T))) {
+        return kNoLambda;
+    } else {
+        const MatTemplate& m = *b.mt;
+        const bool mf0 = m.nLobes > 0 && (m.lobes[0].kind == L_MF_R || m.lobes[0].kind == L_MF_T);
+        const bool mf1 = m.nLobes > 1 && (m.lobes[1].kind == L_MF_R || m.lobes[1].kind == L_MF_T);
+        if (!mf0 && !mf1) return kNoLambda;
+        if (mf0 && mf1 && !(m.lobes[0].ax == m.lobes[1].ax && m.lobes[0].ay == m.lobes[1].ay)) return kNoLambda;
+        return tr_lambda(m.lobes[mf0 ? 0 : 1], wo);
+    }
+}
 template <int K = kAllLobes>
 PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cpp:56-71
     f3 wi = b.to_local(wiW), wo = b.to_local(woW);
@@ -1187,7 +1213,7 @@ PBR_HD rgb bsdf_f(const BSDF& b, f3 woW, f3 wiW, int flags) {   // Reflection.cp
 // per-lobe values and the same sums in the same order, each lobe's shared terms evaluated once
 // (lobe_f_pdf).  Returns f; *pdf as bsdf_pdf.
 template <int K = kAllLobes>
-PBR_HD rgb bsdf_f_pdf(const BSDF& b, f3 woW, f3 wiW, int flags, float* pdfOut) {
+PBR_HD rgb bsdf_f_pdf(const BSDF& b, f3 woW, f3 wiW, int flags, float* pdfOut, float lamWo = kNoLambda) {
     const f3 wi = b.to_local(wiW), wo = b.to_local(woW);
     if (wo.z == 0) { *pdfOut = 0.f; return sp(0.f); }   // both return 0 there (BSDF::Pdf also with no lobes)
     const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
@@ -1201,7 +1227,7 @@ PBR_HD rgb bsdf_f_pdf(const BSDF& b, f3 woW, f3 wiW, int flags, float* pdfOut) {
         const bool wantF = (reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION));
         rgb fl;
         float pl;
-        lobe_f_pdf<K>(l, wo, wi, wantF, &fl, &pl);
+        lobe_f_pdf<K>(l, wo, wi, wantF, &fl, &pl, lamWo);
         if (wantF) f = f + fl;
         pdf += pl;
     }
@@ -1230,10 +1256,11 @@ struct BsdfDraw {
     f3 wi;          // the sampled direction, local
     rgb fSpec;      // a specular lobe's own value
     bool specular;  // the chosen lobe is specular
+    float lamWo;    // Lambda(wo) of the microfacet lobes (mf_lambda), for the sum
 };
 template <int K = kAllLobes>
 PBR_HD bool bsdf_sample_dir(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, float* pdf, int type, int* sampledType,
-                            BsdfDraw* d) {
+                            BsdfDraw* d, float lamWo = kNoLambda) {
     int m = num_components(b, type);
     if (m == 0) { *pdf = 0; *sampledType = 0; return false; }
     int comp = (int)floorf(u0 * m);
@@ -1247,7 +1274,10 @@ PBR_HD bool bsdf_sample_dir(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, 
     if (wo.z == 0) return false;
     *pdf = 0;
     int st = bx.type;
-    d->fSpec = lobe_sample<K>(bx, wo, &wi, ur0, u1, pdf, &st);
+    const bool mfChosen = bx.kind == L_MF_R || bx.kind == L_MF_T;
+    if (lamWo != lamWo && (mfChosen || m > 1)) lamWo = mf_lambda<K>(b, wo);   // (not given: evaluated once here)
+    d->lamWo = lamWo;
+    d->fSpec = lobe_sample<K>(bx, wo, &wi, ur0, u1, pdf, &st, lamWo);
     *sampledType = st;
     if (*pdf == 0) { *sampledType = 0; return false; }
     *wiW = b.to_world(wi);
@@ -1255,7 +1285,7 @@ PBR_HD bool bsdf_sample_dir(const BSDF& b, f3 woW, f3* wiW, float u0, float u1, 
     d->specular = (bx.type & BSDF_SPECULAR) != 0;
     if (!d->specular && m > 1)
         for (int i = 0; i < b.mt->nLobes; ++i)
-            if (i != chosen && matches(b.mt->lobes[i], type)) *pdf += lobe_pdf<K>(b.mt->lobes[i], wo, wi);
+            if (i != chosen && matches(b.mt->lobes[i], type)) *pdf += lobe_pdf<K>(b.mt->lobes[i], wo, wi, lamWo);
     if (m > 1) *pdf /= m;
     return true;
 }
@@ -1268,7 +1298,7 @@ PBR_HD rgb bsdf_sample_sum(const BSDF& b, f3 woW, f3 wiW, int type, const BsdfDr
     for (int i = 0; i < b.mt->nLobes; ++i) {
         const Lobe& l = b.mt->lobes[i];
         if (matches(l, type) && ((reflect && (l.type & BSDF_REFLECTION)) || (!reflect && (l.type & BSDF_TRANSMISSION))))
-            f = f + lobe_f<K>(l, wo, d.wi);
+            f = f + lobe_f<K>(l, wo, d.wi, d.lamWo);
     }
     return f;
 }

@@ -228,13 +228,15 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0,
                             f3 wi = mk(0, 0, 0);
                             float lightPdf = 0, scatteringPdf = 0;
                             VisPt vis;
+                            // Lambda(wo) of the microfacet lobes, once for the estimate's two strategies
+                            const float lamL = mf_lambda<LOBES>(bsdf, bsdf.to_local(wo));
                             rgb Li = sample_li(S, light, isect, uL0, uL1, &wi, &lightPdf, &vis);
                             A = sp(0.f);
                             if (lightPdf > 0 && !black(Li)) {
                                 rgb f;
                                 if constexpr (PBR_DIAG_SHADE & 1) { f = sp(0.25f); scatteringPdf = 0.5f; }
                                 else {
-                                f = bsdf_f_pdf<LOBES>(bsdf, wo, wi, flagsNS, &scatteringPdf) * absdot(wi, isect.sn);
+                                f = bsdf_f_pdf<LOBES>(bsdf, wo, wi, flagsNS, &scatteringPdf, lamL) * absdot(wi, isect.sn);
                                 }
                                 if (!black(f)) {
                                     if (delta) A = f * Li / lightPdf;
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0,
                                 // a small area light and skip the sum over the lobes.
                                 int stype = 0;
                                 BsdfDraw draw;
-                                if (bsdf_sample_dir<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype, &draw) &&
+                                if (bsdf_sample_dir<LOBES>(bsdf, wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype, &draw, lamL) &&
                                     scatteringPdf > 0) {
                                     const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
                                     const float lp = sampledSpecular ? 0.f : ((PBR_DIAG_SHADE & 4) ? 0.5f : pdf_li(S, light, isect, wi));

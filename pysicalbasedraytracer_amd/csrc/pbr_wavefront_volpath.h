@@ -217,11 +217,13 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
                     float scatteringPdf = 0;
                     lightPdf = 0;
                     weightA = 0;
+                    // Lambda(wo) of the microfacet lobes, once for the estimate's two strategies
+                    const float lamL = mediumEvent ? kNoLambda : mf_lambda<LOBES>(bsdf, bsdf.to_local(ref.wo));
                     Li = sample_li(S, light, ref, uL0, uL1, &wi, &lightPdf, &vis);
                     fA = sp(0.f);
                     if (lightPdf > 0 && !black(Li)) {
                         if (!mediumEvent) {
-                            fA = bsdf_f_pdf<LOBES>(bsdf, ref.wo, wi, flagsNS, &scatteringPdf) * absdot(wi, ref.sn);
+                            fA = bsdf_f_pdf<LOBES>(bsdf, ref.wo, wi, flagsNS, &scatteringPdf, lamL) * absdot(wi, ref.sn);
                         } else {
                             fA = sp(phase_hg(dot(ref.wo, wi), g));
                         }
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
                         // a small area light and skip the sum over the lobes.
                         int stype = 0;
                         BsdfDraw draw;
-                        if (bsdf_sample_dir<LOBES>(bsdf, ref.wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype, &draw) &&
+                        if (bsdf_sample_dir<LOBES>(bsdf, ref.wo, &wi, uS0, uS1, &scatteringPdf, flagsNS, &stype, &draw, lamL) &&
                             scatteringPdf > 0) {
                             const bool sampledSpecular = (stype & BSDF_SPECULAR) != 0;
                             const float lp = sampledSpecular ? 0.f : pdf_li(S, light, ref, wi);

@@ -1,5 +1,6 @@
 #!/bin/bash
-# PMC passes over one frame of $CONFIG (default C2) (separate runs: FETCH_SIZE and WRITE_SIZE do not fit one pass).
+# PMC passes over one frame of $CONFIG (default C2) (separate runs: FETCH_SIZE and WRITE_SIZE do not fit one pass;
+# the SQ pass gives VALU instructions and wave-cycle shares, the TCC pass the L2 hit rate).
 # Kernel-trace + counters only (no sys/runtime trace domains with --pmc).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -18,4 +19,5 @@ run() {   # name counters...
 }
 run sq ${SQ_COUNTERS:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD} &&
 run fetch FETCH_SIZE &&
-run write WRITE_SIZE
+run write WRITE_SIZE &&
+run tcc TCC_HIT_sum TCC_MISS_sum

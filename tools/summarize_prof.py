@@ -37,7 +37,7 @@ def main():
         return
     frames = 2.0
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    for sub in ("sq", "fetch", "write"):
+    for sub in ("sq", "fetch", "write", "tcc"):
         p = os.path.join(pmc, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -56,14 +56,27 @@ def main():
           f"= {(rd + wr) / 1e9:.2f} GB\n")
     if js:
         import json
-        per = {k: {"read_bytes": 2 * d.get("FETCH_SIZE", 0) * 1024 / frames, "write_bytes": d.get("WRITE_SIZE", 0) * 1024 / frames}
-               for k, d in agg.items() if "k_" in k}
+        # per frame: bytes, and the SQ / TCC counts behind bench.py's issue-side roofline (VALU wave-
+        # instructions, wave-cycles and their parked / issue-stalled / active shares in quad-cycles,
+        # L2 hits and misses)
+        keys = {"SQ_INSTS_VALU": "valu_insts", "SQ_WAVES": "waves", "SQ_WAVE_CYCLES": "wave_cycles",
+                "SQ_WAIT_ANY": "wait_any", "SQ_WAIT_INST_ANY": "wait_inst_any", "SQ_ACTIVE_INST_ANY": "active_inst_any",
+                "SQ_BUSY_CYCLES": "busy_cycles", "TCC_HIT_sum": "tcc_hit", "TCC_MISS_sum": "tcc_miss"}
+        per = {}
+        for k, d in agg.items():
+            if "k_" not in k:
+                continue
+            e = {"read_bytes": 2 * d.get("FETCH_SIZE", 0) * 1024 / frames, "write_bytes": d.get("WRITE_SIZE", 0) * 1024 / frames}
+            for c, n in keys.items():
+                if c in d:
+                    e[n] = d[c] / frames
+            per[k] = e
         json.dump({"build": build, "frame_read_bytes": rd, "frame_write_bytes": wr, "per_kernel": per,
                    "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in separate passes, "
-                             "2 frames, halved"}, open(js[0], "w"), indent=1)
+                             "2 frames, halved; SQ_* and TCC_HIT/MISS_sum in passes of their own"}, open(js[0], "w"), indent=1)
     print("\n## PMC per frame (separate passes; FETCH_SIZE ×2 gfx950 correction)\n")
-    print("| kernel | HBM read GB | HBM write GB | VALU insts/wave | wave-cycles parked (SQ_WAIT_ANY) | issue-stalled | active |")
-    print("|---|---:|---:|---:|---:|---:|---:|")
+    print("| kernel | HBM read GB | HBM write GB | VALU insts/wave | VALU wave-insts (G) | wave-cycles parked (SQ_WAIT_ANY) | issue-stalled | active | L2 hit |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|")
     for k, d in agg.items():
         if "k_" not in k:
             continue
@@ -71,8 +84,10 @@ def main():
         waves = d.get("SQ_WAVES", 0) or 1
         print(f"| `{k}` | {2 * d.get('FETCH_SIZE', 0) * 1024 / 1e9 / frames:.2f} | "
               f"{d.get('WRITE_SIZE', 0) * 1024 / 1e9 / frames:.2f} | {d.get('SQ_INSTS_VALU', 0) / waves:.0f} | "
+              f"{d.get('SQ_INSTS_VALU', 0) / 1e9 / frames:.3f} | "
               f"{d.get('SQ_WAIT_ANY', 0) / wc:.2f} | {d.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | "
-              f"{d.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f} |")
+              f"{d.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f} | "
+              f"{d.get('TCC_HIT_sum', 0) / max(1.0, d.get('TCC_HIT_sum', 0) + d.get('TCC_MISS_sum', 0)):.3f} |")
 
 
 if __name__ == "__main__":
