@@ -224,7 +224,7 @@ constexpr int kCameraShort = PBR_CAMERA_SHORT;
 
 // load(i, &key) → the i-th ray of the queue (key: what store needs, e.g. its queue position);
 // store(key, hit, ray, h) → the ray's result (closest hit: ray.tMax and h; any hit: hit only).
-template <bool ANY, int SHORT, class Load, class Store>
+template <bool ANY, int SHORT, bool NF = true, class Load, class Store>
 __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store store, unsigned long long* diag = nullptr,
                                 int diagKind = 0) {
     const int lane = (int)__lane_id();
@@ -316,7 +316,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
             }
         } else {
             QuadSlots q;
-            quad_slots<ANY, true>(S, cur, r, inv, n0, n1, n2, &q);
+            quad_slots<ANY, NF>(S, cur, r, inv, n0, n1, n2, &q);
             const float tM = r.tMax;
             const bool p0 = q.k[0] && q.t[0] < tM, p1 = q.k[1] && q.t[1] < tM, p2 = q.k[2] && q.t[2] < tM,
                        p3 = q.k[3] && q.t[3] < tM;

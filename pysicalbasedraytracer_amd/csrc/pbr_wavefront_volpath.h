@@ -451,7 +451,10 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
     }
 }
 
-// VisibilityTester::Tr (Light.cpp:31-47): walk to the light sample through medium interfaces
+// VisibilityTester::Tr (Light.cpp:31-47): walk to the light sample through medium interfaces.
+// Its lane-refill walk fetches near/far plane rows (PBR_NF_ROWS) although that spills 9 VGPRs here:
+// C5 transmittance 340.8 ms/frame without the rows, 327.3 with them at 5 workgroups per CU (no
+// spill), 321.5 with them at 6 (kept; serial schedule, profiles/r6_ab_tr.log).
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_REFILL_OCC_TR) void k_wfv_tr(WfvParams V) {
     WfpParams& X = V.X;
