@@ -351,6 +351,8 @@ def main():
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
+        if rank == 0:   # progress on stderr (the one JSON line is stdout's)
+            print(f"[bench] {args.config}: {k} frame(s) in {el * 1e3:.1f} ms", file=sys.stderr, flush=True)
         return el
 
     for _ in range(args.warmup):
