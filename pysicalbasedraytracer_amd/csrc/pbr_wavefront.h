@@ -152,6 +152,9 @@ __device__ __forceinline__ int pack_dd(int dim, int depth) { return (dim & 0xfff
 // Exclusive prefix of the kWfBlocks segment counts into s_off[0..kWfBlocks] (whole workgroup of
 // 256); returns the total.
 __shared__ int s_seg_off[kWfBlocks + 1];
+constexpr int kSegCoarse = kWfBlocks / 64;     // segments per coarse bucket of seg_pos_wave
+static_assert(kSegCoarse >= 1 && kSegCoarse <= 32, "seg_pos_wave: a 64-way then a 32-way ballot");
+__shared__ int s_seg_coarse[64];                // s_seg_off[k * kSegCoarse]: conflict-free for 64 lanes
 __device__ int seg_scan(const int* counts) {
     constexpr int per = kWfBlocks / 256;
     __shared__ int s_wave[4];
@@ -167,7 +170,12 @@ __device__ int seg_scan(const int* counts) {
     __syncthreads();
     int excl = incl - sum;
     for (int k = 0; k < w; ++k) excl += s_wave[k];
-    for (int i = 0; i < per; ++i) { s_seg_off[t * per + i] = excl; excl += local[i]; }
+    for (int i = 0; i < per; ++i) {
+        const int g = t * per + i;
+        s_seg_off[g] = excl;
+        if (g % kSegCoarse == 0) s_seg_coarse[g / kSegCoarse] = excl;
+        excl += local[i];
+    }
     if (t == 255) s_seg_off[kWfBlocks] = excl;
     __syncthreads();
     return s_seg_off[kWfBlocks];
@@ -180,6 +188,43 @@ __device__ __forceinline__ int seg_pos(int segCap, int q) {
         if (s_seg_off[mid] <= q) lo = mid; else hi = mid;
     }
     return lo * segCap + (q - s_seg_off[lo]);
+}
+// seg_pos for a wave whose lanes look up dense indices in [lo, hi] (wave-uniform, 0 <= lo <= hi):
+// the same position, from two LDS round trips instead of seg_pos's 11 dependent ones.  A 64-way
+// ballot over the coarse offsets and a 32-way one over the chosen bucket's offsets (lanes 0-31 for
+// lo, 32-63 for hi) find the last segments whose offsets are <= lo and <= hi — the offsets are
+// nondecreasing, so each ballot is a prefix of lanes — and each lane bisects between the two, which
+// bracket its answer (usually one segment: no step).  Every lane of the wave must call it (full
+// exec); lanes whose q lies outside [lo, hi] get a position inside the queue that they must not use.
+#ifndef PBR_SEG_WAVE
+#define PBR_SEG_WAVE 1
+#endif
+__device__ __forceinline__ int seg_pos_wave(int segCap, int q, int lo, int hi) {
+    if constexpr (!PBR_SEG_WAVE) return seg_pos(segCap, q);
+    // (the lane's LDS addresses are formed here, not hoisted out of the caller's loop, where they
+    // would hold VGPRs across a shade kernel's whole body)
+    int lane = (int)__lane_id();
+    asm volatile("" : "+v"(lane));
+    const int cv = s_seg_coarse[lane];
+    const int cLo = __popcll(__ballot(cv <= lo)) - 1, cHi = __popcll(__ballot(cv <= hi)) - 1;   // >= 0: offset 0 is 0
+    const int k = lane & 31;
+    const int c = lane < 32 ? cLo : cHi, tgt = lane < 32 ? lo : hi;
+    const unsigned long long m = __ballot(k < kSegCoarse && s_seg_off[c * kSegCoarse + min(k, kSegCoarse - 1)] <= tgt);
+    int a = cLo * kSegCoarse + __popc((unsigned)m) - 1;             // last segment with offset <= lo
+    int b = cHi * kSegCoarse + __popc((unsigned)(m >> 32));         // one past the last with offset <= hi
+    while (b - a > 1) {                                             // offset[a] <= q < offset[b] (or b = end)
+        const int mid = (a + b) >> 1;
+        if (s_seg_off[mid] <= q) a = mid; else b = mid;
+    }
+    return a * segCap + (q - s_seg_off[a]);
+}
+// The position of dense index i in a wave-uniform loop over n entries whose wave holds 64 consecutive
+// indices (i = the wave's first + lane; every lane calls it).  Lanes with i >= n get an unusable
+// position; a wave wholly past n skips the search.
+__device__ __forceinline__ int seg_pos_dense(int segCap, int i, int n) {
+    const int w0 = __builtin_amdgcn_readfirstlane(i - (int)__lane_id());
+    if (w0 >= n) return 0;
+    return seg_pos_wave(segCap, min(i, n - 1), w0, min(w0 + 63, n - 1));
 }
 
 // Queue traversal with lane refill (Aila & Laine's "replace terminated rays").  Incoherent rays
@@ -222,11 +267,12 @@ static_assert(kRefill >= 1 && kRefill <= 64, "refill threshold: idle lanes of a 
 #endif
 constexpr int kCameraShort = PBR_CAMERA_SHORT;
 
-// load(i, &key) → the i-th ray of the queue (key: what store needs, e.g. its queue position);
-// store(key, hit, ray, h) → the ray's result (closest hit: ray.tMax and h; any hit: hit only).
+// The queue holds n rays in segments of segCap (seg_scan has run); load(q, &key) → the ray at queue
+// position q (key: what store needs, e.g. q); store(key, hit, ray, h) → the ray's result (closest
+// hit: ray.tMax and h; any hit: hit only).
 template <bool ANY, int SHORT, bool NF = true, class Load, class Store>
-__device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store store, unsigned long long* diag = nullptr,
-                                int diagKind = 0) {
+__device__ void traverse_stream(const DeviceScene& S, int n, int segCap, Load load, Store store,
+                                unsigned long long* diag = nullptr, int diagKind = 0) {
     const int lane = (int)__lane_id();
     const int stride = (int)(gridDim.x * blockDim.x);
     const int wbase = trav_block() * (int)blockDim.x + ((int)threadIdx.x & ~63);
@@ -251,14 +297,22 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
     (void)laneSteps; (void)waveSteps;
     int maxSp = 0;   // PBR_STACK_DIAG: the ray's deepest stack
     (void)maxSp;
+    // the binary root's box, read once (scalar): a refilled ray's first test waits on no fetch
+    float4 rootA = make_float4(0.f, 0.f, 0.f, 0.f), rootB = rootA;
+    if (S.nNodes > 0) {
+        const ScalarF4Ptr w = scalar_f4(S.nodes);
+        rootA = as_f4(w[0]); rootB = as_f4(w[1]);
+    }
     while (true) {
         const unsigned long long idle = __ballot(!have);
         const int nIdle = __popcll(idle);
-        if (nIdle >= kRefill && rayOf(cursor) < n) {   // wave-uniform
+        if (nIdle >= kRefill && rayOf(cursor) < n) {   // wave-uniform (every lane is here)
+            const int i = rayOf(cursor + __popcll(idle & below));   // this lane's ray if it is idle
+            const int iHi = min(rayOf(cursor + nIdle - 1), n - 1);   // the idle lanes' rays: rayOf(cursor) ..
+            const int qi = seg_pos_wave(segCap, min(i, iHi), rayOf(cursor), iHi);
             if (!have) {
-                const int i = rayOf(cursor + __popcll(idle & below));
                 if (i < n) {
-                    r = load(i, &key);
+                    r = load(qi, &key);
                     found = false;
                     h.slot = -1; h.b0 = h.b1 = h.b2 = 0.f;
                     // traverse(): the root is visited first (the binary root box)
@@ -266,7 +320,7 @@ __device__ void traverse_stream(const DeviceScene& S, int n, Load load, Store st
                     if (ok) {
                         inv = ANY ? mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z) : mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
-                        ok = node_hit(S.nodes[0], S.nodes[1], r, inv, n0, n1, n2);
+                        ok = node_hit(rootA, rootB, r, inv, n0, n1, n2);
                     }
                     if (ok) {
                         cur = S.quadRootRef;
@@ -419,9 +473,8 @@ __global__ __launch_bounds__(256, REFILL ? PBR_REFILL_OCC : PBR_TRAV_OCC) void k
     const int n = seg_scan(W.cur.segCount);
     if constexpr (REFILL && kRefill > 0 && SHORT > 0 && kQuadTraversal) {
         traverse_stream<false, kRefillShort>(
-            W.P.S, n,
-            [&](int i, int* key) {
-                const int q = seg_pos(W.segCap, i);
+            W.P.S, n, W.segCap,
+            [&](int q, int* key) {
                 *key = q;
                 const float4 o = W.cur.o[q], d = W.cur.d[q];
                 return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -433,6 +486,7 @@ __global__ __launch_bounds__(256, REFILL ? PBR_REFILL_OCC : PBR_TRAV_OCC) void k
             W.prof, KP_WF_EXTEND);
         return;
     }
+    // (per-lane seg_pos: the wave-cooperative lookup made this 63-VGPR packet walk spill 2)
     for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int q = seg_pos(W.segCap, i);
         float4 o = W.cur.o[q], d = W.cur.d[q];
@@ -720,7 +774,8 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade(WfParams W, int level0) {
     for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
         const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
         const bool active = i < n;
-        shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
+        const int q = level0 ? i : seg_pos_dense(W.segCap, i, n);
+        shade(active, active ? q : 0);
     }
     __syncthreads();
     if (threadIdx.x == 0) { W.shadowSeg[wf_block()] = s_push[0]; W.next.segCount[wf_block()] = s_push[1]; }
@@ -734,8 +789,10 @@ __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
     // Whitted's shadow rays keep the plain loop: lane refill (traverse_stream) measured 5.45 → 5.90
     // ms/frame on C2 (refill 16), 5.40 (refill 32)
-    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int q = seg_pos(W.shadowSegCap, i);
+    for (int i0 = wf_block() * blockDim.x + ((int)threadIdx.x & ~63); i0 < n; i0 += gridDim.x * blockDim.x) {   // per wave
+        const int i = i0 + (int)__lane_id();
+        const int q = seg_pos_dense(W.shadowSegCap, i, n);
+        if (i >= n) continue;
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
@@ -802,7 +859,8 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
     for (int it = 0; it < nIter; ++it) {
         const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
         const bool active = i < n;
-        const int q = !active ? 0 : (level0 ? i : seg_pos(W.segCap, i));
+        const int qd = level0 ? i : seg_pos_dense(W.segCap, i, n);
+        const int q = active ? qd : 0;
         bool pushNext = false, shading = false, nonSpecular = false;
         int id = 0, depth = 0, dim = 0;
         Ray ray, cont;
@@ -920,8 +978,10 @@ __global__ __launch_bounds__(256, OCC) void k_wf_shade_ml(WfParams W, int level0
 template <int SHORT>
 __global__ __launch_bounds__(256, PBR_TRAV_OCC) void k_wf_shadow_ml(WfParams W) {
     const int n = seg_scan(W.shadowSeg);
-    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int q = seg_pos(W.shadowSegCap, i);
+    for (int i0 = wf_block() * blockDim.x + ((int)threadIdx.x & ~63); i0 < n; i0 += gridDim.x * blockDim.x) {   // per wave
+        const int i = i0 + (int)__lane_id();
+        const int q = seg_pos_dense(W.shadowSegCap, i, n);
+        if (i >= n) continue;
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;

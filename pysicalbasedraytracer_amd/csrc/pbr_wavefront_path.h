@@ -362,7 +362,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0,
         for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
             const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
             const bool active = i < n;
-            shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)));
+            const int q = level0 ? i : seg_pos_dense(W.segCap, i, n);
+            shade(active, active ? q : 0);
         }
     } else if (pass > 0) {   // this pass's list, filed by pass 0
         const int cnt = X.passCnt[(pass - 1) * kWfBlocks + wf_block()];
@@ -384,7 +385,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfp_shade(WfpParams X, int level0,
         int head = 0;   // workgroup-uniform
         for (int it = 0; it < nIter; ++it) {
             const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-            const int q = i < n ? (level0 ? i : seg_pos(W.segCap, i)) : 0;
+            const int qd = level0 ? i : seg_pos_dense(W.segCap, i, n);
+            const int q = i < n ? qd : 0;
             const int cls = i < n ? entry_pass(X, q) : -1;
             const bool mine = cls == 0;
             for (int c = 1; c < X.nPasses; ++c) {   // file the other passes' entries (per segment, dense)
@@ -428,9 +430,8 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_ANY) void k_wfp_shadow(WfpParam
     if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
         unsigned visible = 0;   // profile field 1, added once per wave at the end
         traverse_stream<true, kAnyShort>(
-            W.P.S, n,
-            [&](int i, int* key) {
-                const int q = seg_pos(W.segCap, i);
+            W.P.S, n, W.segCap,
+            [&](int q, int* key) {
                 *key = q;
                 const float4 o = W.so[q], d = W.sd[q];
                 return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -445,8 +446,10 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_ANY) void k_wfp_shadow(WfpParam
         if (W.prof) prof_add(W.prof + KP_WFP_SHADOW * kProfFields + 1, visible);
         return;
     }
-    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int q = seg_pos(W.segCap, i);
+    for (int i0 = wf_block() * blockDim.x + ((int)threadIdx.x & ~63); i0 < n; i0 += gridDim.x * blockDim.x) {   // per wave
+        const int i = i0 + (int)__lane_id();
+        const int q = seg_pos_dense(W.segCap, i, n);
+        if (i >= n) continue;
         float4 o = W.so[q], d = W.sd[q];
         Ray r = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         HitRec h;
@@ -467,9 +470,8 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC) void k_wfp_probe(WfpParams X) 
     const int n = seg_scan(X.probeSeg);
     if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
         traverse_stream<false, kRefillShort>(
-            S, n,
-            [&](int i, int* key) {
-                const int q = seg_pos(W.segCap, i);
+            S, n, W.segCap,
+            [&](int q, int* key) {
                 *key = q;
                 const float4 o = X.po[q], d = X.pd[q];
                 return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
@@ -495,8 +497,10 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC) void k_wfp_probe(WfpParams X) 
             W.prof, KP_WFP_PROBE);
         return;
     }
-    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int q = seg_pos(W.segCap, i);
+    for (int i0 = wf_block() * blockDim.x + ((int)threadIdx.x & ~63); i0 < n; i0 += gridDim.x * blockDim.x) {   // per wave
+        const int i = i0 + (int)__lane_id();
+        const int q = seg_pos_dense(W.segCap, i, n);
+        if (i >= n) continue;
         float4 o = X.po[q], d = X.pd[q];
         Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, -1);
         const int di = X.pid[q];
@@ -535,8 +539,10 @@ __device__ __forceinline__ void add_direct(const WfpParams& X, int tgt, rgb dire
 __global__ __launch_bounds__(256) void k_wfp_resolve(WfpParams X) {
     WfParams& W = X.W;
     const int n = seg_scan(X.directSeg);
-    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int di = seg_pos(W.segCap, i);
+    for (int i0 = wf_block() * blockDim.x + ((int)threadIdx.x & ~63); i0 < n; i0 += gridDim.x * blockDim.x) {   // per wave
+        const int i = i0 + (int)__lane_id();
+        const int di = seg_pos_dense(W.segCap, i, n);
+        if (i >= n) continue;
         const int fl = X.dFlags[di];
         const float4 a = X.dA[di], bt = X.dBeta[di];
         rgb Ld = sp(0.f);

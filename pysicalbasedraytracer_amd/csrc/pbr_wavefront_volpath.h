@@ -395,7 +395,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
         for (int it = 0; it < nIter; ++it) {   // uniform trip count: wave_push needs convergent lanes
             const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
             const bool active = i < n;
-            shade(active, !active ? 0 : (level0 ? i : seg_pos(W.segCap, i)), false);
+            const int q = level0 ? i : seg_pos_dense(W.segCap, i, n);
+            shade(active, active ? q : 0, false);
         }
     } else if (pass > 0) {   // this pass's list, filed by pass 0
         const int cnt = X.passCnt[(pass - 1) * kWfBlocks + wf_block()];
@@ -415,7 +416,8 @@ __global__ __launch_bounds__(256, OCC) void k_wfv_shade(WfvParams V, int level0,
         int head = 0;
         for (int it = 0; it < nIter; ++it) {
             const int i = it * stride + wf_block() * blockDim.x + threadIdx.x;
-            const int q = i < n ? (level0 ? i : seg_pos(W.segCap, i)) : 0;
+            const int qd = level0 ? i : seg_pos_dense(W.segCap, i, n);
+            const int q = i < n ? qd : 0;
             const int cls = i < n ? entry_pass_vol(X, q) : -1;
             for (int c = 1; c < X.nPasses; ++c) {
                 const int at = wave_push(&s_list[c - 1], cls == c);
@@ -463,9 +465,8 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_TR) void k_wfv_tr(WfvParams V) 
     if constexpr (kRefill > 0 && SHORT > 0 && kQuadTraversal) {
         if (V.anyHitTr) {   // the walk is one any-hit query (below): lane-refill traversal
             traverse_stream<true, SHORT>(   // (not kAnyShort: see pbr_device.h)
-                S, n,
-                [&](int i, int* key) {
-                    const int q = seg_pos(X.W.segCap, i);
+                S, n, X.W.segCap,
+                [&](int q, int* key) {
                     *key = q;
                     const float4 o = V.to[q], d = V.td[q];
                     return mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, __float_as_int(d.w));
@@ -480,8 +481,10 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_TR) void k_wfv_tr(WfvParams V) 
             return;
         }
     }
-    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int q = seg_pos(X.W.segCap, i);
+    for (int i0 = wf_block() * blockDim.x + ((int)threadIdx.x & ~63); i0 < n; i0 += gridDim.x * blockDim.x) {   // per wave
+        const int i = i0 + (int)__lane_id();
+        const int q = seg_pos_dense(X.W.segCap, i, n);
+        if (i >= n) continue;
         float4 o = V.to[q], d = V.td[q], tp = V.tp[q], te = V.te[q], tn = V.tn[q];
         const f3 p1 = mk(tp.x, tp.y, tp.z), e1 = mk(te.x, te.y, te.z), n1 = mk(tn.x, tn.y, tn.z);
         Ray ray = mkray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, __float_as_int(d.w));
@@ -522,8 +525,10 @@ __global__ __launch_bounds__(256, PBR_REFILL_OCC_TR) void k_wfv_tr(WfvParams V) 
 __global__ __launch_bounds__(256) void k_wfv_resolve(WfvParams V) {
     WfpParams& X = V.X;
     const int n = seg_scan(X.directSeg);
-    for (int i = wf_block() * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int di = seg_pos(X.W.segCap, i);
+    for (int i0 = wf_block() * blockDim.x + ((int)threadIdx.x & ~63); i0 < n; i0 += gridDim.x * blockDim.x) {   // per wave
+        const int i = i0 + (int)__lane_id();
+        const int di = seg_pos_dense(X.W.segCap, i, n);
+        if (i >= n) continue;
         const int fl = X.dFlags[di];
         const float4 a = X.dA[di], bt = X.dBeta[di];
         rgb Ld = sp(0.f);
