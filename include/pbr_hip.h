@@ -341,8 +341,9 @@ enum pbr_fuse_mode {
 typedef struct pbr_schedule {
     int kernels;                /* pbr_kernels_mode */
     int chunk_log2;             /* at most 2^chunk_log2 samples per chunk (10..28; 0 = the default: 25 for
-                                 * Whitted, less with several lights, 26 for Path / VolPath); capped at
-                                 * the default, which bounds the queue memory per lane */
+                                 * Whitted, less with several lights; for Path / VolPath the largest of
+                                 * 2^20..2^27 whose lanes' queues fit 3/4 of the device memory free or held
+                                 * by the context); capped at 25 (Whitted) and 27 (Path / VolPath) */
     int lanes;                  /* chunk lanes, each its own stream and queues (1..4); 0 = 3 */
     int fuse_camera;            /* pbr_fuse_mode */
     int serial;                 /* 1: every launch of a frame on the caller's stream, one after another

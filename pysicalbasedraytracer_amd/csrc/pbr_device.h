@@ -223,7 +223,29 @@ __device__ __forceinline__ bool prim_hit(const DeviceScene& S, int slot, const R
 // that depends on ray.tMax.  Returns false where node_hit would whatever ray.tMax is.
 // node_slab on the box's near and far planes, already picked by the direction signs (nr = the
 // planes the ray enters through: hi on a negative axis, lo on a positive one; fr the others).
+// PBR_SLAB_BRANCHLESS: the same comparisons and selects as straight-line code (every lane computes
+// all three axes; the early exits become a mask), so a quad node's four tests are one block with no
+// exec-mask branches.  tEnter is only read where the test passes, and there it is the same value.
+#ifndef PBR_SLAB_BRANCHLESS
+#define PBR_SLAB_BRANCHLESS 1
+#endif
 __device__ __forceinline__ bool slab_nf(f3 nr, f3 fr, const Ray& r, f3 inv, float* tEnter) {
+    if constexpr (PBR_SLAB_BRANCHLESS) {
+        float tMin = (nr.x - r.o.x) * inv.x;
+        float tMax = (fr.x - r.o.x) * inv.x;
+        const float tyMin = (nr.y - r.o.y) * inv.y;
+        const float tyMax = (fr.y - r.o.y) * inv.y;
+        const float tzMin = (nr.z - r.o.z) * inv.z;
+        const float tzMax = (fr.z - r.o.z) * inv.z;
+        const bool okY = !(tMin > tyMax) & !(tyMin > tMax);
+        tMin = tyMin > tMin ? tyMin : tMin;
+        tMax = tyMax < tMax ? tyMax : tMax;
+        const bool okZ = !(tMin > tzMax) & !(tzMin > tMax);
+        tMin = tzMin > tMin ? tzMin : tMin;
+        tMax = tzMax < tMax ? tzMax : tMax;
+        *tEnter = tMin;
+        return okY & okZ & (tMax > 0);
+    }
     float tMin = (nr.x - r.o.x) * inv.x;
     float tMax = (fr.x - r.o.x) * inv.x;
     float tyMin = (nr.y - r.o.y) * inv.y;
@@ -599,10 +621,21 @@ __device__ bool traverse_packet(const DeviceScene& S, Ray& r, HitRec* h, f3 inv,
             const int meta = __float_as_int(w[7].x);
             float t[4] = {0.f, 0.f, 0.f, 0.f};
             bool p[4];
+            if constexpr (PBR_SLAB_BRANCHLESS) {   // (the lane and valid masks applied after the tests)
+                p[0] = slab_nf(mk(NX.x, NY.x, NZ.x), mk(FX.x, FY.x, FZ.x), r, inv, &t[0]) & (t[0] < r.tMax);
+                p[1] = slab_nf(mk(NX.y, NY.y, NZ.y), mk(FX.y, FY.y, FZ.y), r, inv, &t[1]) & (t[1] < r.tMax);
+                p[2] = slab_nf(mk(NX.z, NY.z, NZ.z), mk(FX.z, FY.z, FZ.z), r, inv, &t[2]) & (t[2] < r.tMax);
+                p[3] = slab_nf(mk(NX.w, NY.w, NZ.w), mk(FX.w, FY.w, FZ.w), r, inv, &t[3]) & (t[3] < r.tMax);
+                p[0] = p[0] & active & (((meta >> 8) & 1) != 0);
+                p[1] = p[1] & active & (((meta >> 9) & 1) != 0);
+                p[2] = p[2] & active & (((meta >> 10) & 1) != 0);
+                p[3] = p[3] & active & (((meta >> 11) & 1) != 0);
+            } else {
             p[0] = active && slab_nf(mk(NX.x, NY.x, NZ.x), mk(FX.x, FY.x, FZ.x), r, inv, &t[0]) && ((meta >> 8) & 1) && t[0] < r.tMax;
             p[1] = active && slab_nf(mk(NX.y, NY.y, NZ.y), mk(FX.y, FY.y, FZ.y), r, inv, &t[1]) && ((meta >> 9) & 1) && t[1] < r.tMax;
             p[2] = active && slab_nf(mk(NX.z, NY.z, NZ.z), mk(FX.z, FY.z, FZ.z), r, inv, &t[2]) && ((meta >> 10) & 1) && t[2] < r.tMax;
             p[3] = active && slab_nf(mk(NX.w, NY.w, NZ.w), mk(FX.w, FY.w, FZ.w), r, inv, &t[3]) && ((meta >> 11) & 1) && t[3] < r.tMax;
+            }
             const unsigned long long bm[4] = {__builtin_amdgcn_ballot_w64(p[0]), __builtin_amdgcn_ballot_w64(p[1]),
                                               __builtin_amdgcn_ballot_w64(p[2]), __builtin_amdgcn_ballot_w64(p[3])};
             // visit position → slot column (quad_slots' swaps; any hit: build order)
@@ -666,7 +699,8 @@ __device__ bool traverse_packet(const DeviceScene& S, Ray& r, HitRec* h, f3 inv,
             const __attribute__((address_space(4))) float* rf = (const __attribute__((address_space(4))) float*)(size_t)(wf + 24);
             float tt = 0.f;
             bool a = (m & lanebit) != 0ull && (!ANY || alive);
-            a = a && slab_nf(nr, fr, r, inv, &tt) && tt < r.tMax;
+            if constexpr (PBR_SLAB_BRANCHLESS) a = a & slab_nf(nr, fr, r, inv, &tt) & (tt < r.tMax);
+            else a = a && slab_nf(nr, fr, r, inv, &tt) && tt < r.tMax;
             if (__builtin_amdgcn_ballot_w64(a) != 0ull) {
                 active = a;
                 cur = __builtin_amdgcn_readfirstlane(__float_as_int(rf[c]));

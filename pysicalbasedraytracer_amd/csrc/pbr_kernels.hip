@@ -1119,18 +1119,33 @@ struct WfChunks {
 // shard (≤ 2^25 samples, ≈ 12 GB per lane) keeps three; a Path frame at the 2^26-sample cap (≈ 23
 // GB per lane) two; the single-frame call would run such a frame on one lane.
 constexpr double kBatchLaneBytes = 48e9;
+// The largest chunk a Whitted schedule accepts (its default is 2^25, less with several lights).
+// Measured, C2 in 5-frame batches (bit-identical): 2^25 (four chunks) 13.62-13.69 ms, 2^26 14.39-14.61,
+// 2^27 14.16-14.25 (profiles/r6_c2_chunk_ab.log).
+#ifndef PBR_WF_WHITTED_MAXLOG2
+#define PBR_WF_WHITTED_MAXLOG2 25
+#endif
+// laneBudget > 0 (the Path / VolPath schedules, lane_budget): the default chunk is the largest
+// 2^k <= 2^maxLog2 samples whose lanes' buffers fit that many bytes (not below 2^minLog2), and a
+// batch's one-chunk frames keep as many lanes as fit it; 0: the default is 2^maxLog2 and the batch
+// budget kBatchLaneBytes.  A requested chunk_log2 is capped at maxLog2 either way.
 WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25, bool batch = false,
-                   double bytesPerSample = 0) {
+                   double bytesPerSample = 0, double laneBudget = 0, int defLog2 = 0, int minLog2 = 20) {
     WfChunks c;
-    const int chunkLog2 = sch.chunk_log2 > 0 ? std::min(sch.chunk_log2, maxLog2) : maxLog2;   // the default bounds the memory
     c.lanes = sch.serial ? 1 : (sch.lanes > 0 ? sch.lanes : kWfDefaultLanes);
+    int chunkLog2 = maxLog2;
+    if (sch.chunk_log2 > 0) chunkLog2 = std::min(sch.chunk_log2, maxLog2);
+    else if (defLog2 > 0) chunkLog2 = std::min(defLog2, maxLog2);
+    else if (laneBudget > 0 && bytesPerSample > 0)
+        while (chunkLog2 > minLog2 && c.lanes * bytesPerSample * (double)(1LL << chunkLog2) > laneBudget) --chunkLog2;
     c.chunkPix = std::max(1LL, (1LL << chunkLog2) / P.spp);
     if (c.chunkPix >= P.nPixels) {   // one chunk: splitting a small frame only adds launch tails
         c.chunkPix = P.nPixels;
         if (!batch) c.lanes = 1;     // (a batch's one-chunk frames rotate over the lanes)
         else if (c.lanes > 1 && bytesPerSample > 0) {
             const double perLane = bytesPerSample * (double)P.nPixels * (double)P.spp;
-            c.lanes = (int)std::max(1.0, std::min((double)c.lanes, std::floor(kBatchLaneBytes / perLane)));
+            const double budget = laneBudget > 0 ? laneBudget : kBatchLaneBytes;
+            c.lanes = (int)std::max(1.0, std::min((double)c.lanes, std::floor(budget / perLane)));
         }
     } else {
         // Many chunks: make them equal and a whole number per lane (the count rounded down to a
@@ -1150,6 +1165,25 @@ WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25, 
     c.qcap = std::max(c.cap, (size_t)c.segCap * kWfBlocks);
     return c;
 }
+// Bytes the Path / VolPath lane buffers may take: a share of the device memory that is free or
+// already held by this context's lanes (their buffers are reused and grown, never shrunk).  On an
+// MI355X (288 GB) that is room for three lanes of 2^27-sample chunks; another large allocation on the
+// device (a second context) leaves less and the chunks shrink.  Measured (bit-identical, frame ms of
+// single frames, three lanes): C4 2^26 4379 → 2^27 4189, C5 815.6 → 771.4, C3 205.0 → 203.6; 2^24
+// and 2^23 were 25-50% slower (profiles/r6_sched_sweep*.log).
+constexpr double kLaneMemShare = 0.75;
+double lane_budget(pbr_hip_ctx* ctx) {
+    size_t freeB = 0, totalB = 0;
+    if (hipMemGetInfo(&freeB, &totalB) != hipSuccess) return 0;   // the fixed defaults
+    static_assert(sizeof(WfBufs) % sizeof(DevBuf) == 0, "WfBufs holds DevBuf members only");
+    double held = 0;
+    for (int l = 0; l < kWfLanes; ++l) {
+        const DevBuf* b = reinterpret_cast<const DevBuf*>(&ctx->wb[l]);
+        for (size_t i = 0; i < sizeof(WfBufs) / sizeof(DevBuf); ++i) held += (double)b[i].bytes;
+    }
+    return kLaneMemShare * ((double)freeB + held);
+}
+
 // The frames of one render call.  One frame (pbr_hip_render): its chunks alternate over the lanes,
 // lane 0 on the caller's stream, forked at the start and joined at the end.  A batch
 // (pbr_hip_render_frames): the frames' chunks continue one rotation over the same lanes, forked once
@@ -1265,7 +1299,7 @@ int render_wavefront(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, const FrameSet
     // the lane buffers below, per sample: two ray queues, the shadow queue(s), the records
     const double bytesPerSample = 2 * 52.0 + (52.0 + (skyDeferred ? 16.0 : 0.0)) * lightsPerShade + 16.0 +
                                   levels * (36.0 + (ml ? 17.0 * nL : 0.0)) + 8.0;
-    const WfChunks ch = wf_chunks(ctx->sched, P, maxLog2, F.batch, bytesPerSample);
+    const WfChunks ch = wf_chunks(ctx->sched, P, PBR_WF_WHITTED_MAXLOG2, F.batch, bytesPerSample, lane_budget(ctx), maxLog2);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const size_t sqcap = qcap * (size_t)lightsPerShade;   // shadow-queue entries
     const int lobes = scene_lobe_kinds(ctx->host);
@@ -1463,7 +1497,7 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
     // the lane buffers below, per sample: two ray queues with their state (84 B each), shadow and probe
     // queues, the direct records, the sample's L and index (+ VolPath's transmittance walk and
     // records), and the class pass lists (at most 5 passes)
-    const WfChunks ch = wf_chunks(ctx->sched, P, 26, F.batch, (vol ? 460.0 : 340.0) + 4.0 * 5);
+    const WfChunks ch = wf_chunks(ctx->sched, P, 27, F.batch, (vol ? 460.0 : 340.0) + 4.0 * 5, lane_budget(ctx));
     const size_t cap = ch.cap, qcap = ch.qcap;
     const long long nChunks = (P.nPixels + ch.chunkPix - 1) / ch.chunkPix;
     const int lobes = scene_lobe_kinds(ctx->host);

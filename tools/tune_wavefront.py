@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--ref-file", default=None, help=".npy frame to compare against (written if absent), "
                                                      "so experimental builds can be checked against each other")
     ap.add_argument("--profile", action="store_true", help="per-kernel-family ms per frame (HIP events)")
+    ap.add_argument("--batch", type=int, default=0, help="time K-frame pbr_hip_render_frames batches (bench.py's "
+                                                           "timed window) instead of single frames; ms per frame")
     ap.add_argument("variants", nargs="*", default=[""])
     a = ap.parse_args()
     if a.lib:
@@ -63,11 +65,18 @@ def main():
         r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
         torch.cuda.synchronize(dev)
         ms = []
+        if a.batch > 0:   # K frames per batch into K buffers; the last frame is the one compared
+            rgbs = [rgb] + [torch.empty_like(rgb) for _ in range(a.batch - 1)]
+            rgbas = [rgba] + [torch.empty_like(rgba) for _ in range(a.batch - 1)]
+            rgbs, rgbas = rgbs[::-1], rgbas[::-1]
         for _ in range(a.steps):
             t0 = time.perf_counter()
-            r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
+            if a.batch > 0:
+                r.render_frames(rd, [x.data_ptr() for x in rgbs], [x.data_ptr() for x in rgbas], stream=stream.cuda_stream)
+            else:
+                r.render_device(rd, rgb.data_ptr(), rgba.data_ptr(), stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
-            ms.append((time.perf_counter() - t0) * 1e3)
+            ms.append((time.perf_counter() - t0) * 1e3 / max(1, a.batch))
         out = rgb.cpu().numpy()
         same = "ref" if ref is None else ("identical" if np.array_equal(out.view(np.uint32), ref.view(np.uint32))
                                           else "DIFFERENT max|d|=%g" % np.abs(out - ref).max())
