@@ -344,7 +344,8 @@ typedef struct pbr_schedule {
                                  * Whitted, less with several lights; for Path / VolPath the largest of
                                  * 2^20..2^27 whose lanes' queues fit 3/4 of the device memory free or held
                                  * by the context); capped at 25 (Whitted) and 27 (Path / VolPath) */
-    int lanes;                  /* chunk lanes, each its own stream and queues (1..4); 0 = 3 */
+    int lanes;                  /* chunk lanes, each its own stream and queues (1..4); 0 = 3 (Path: 4 where
+                                 * four lanes of 2^27-sample chunks fit the memory share above) */
     int fuse_camera;            /* pbr_fuse_mode */
     int serial;                 /* 1: every launch of a frame on the caller's stream, one after another
                                  * (one lane, no shadow stream) — measures each kernel on its own */

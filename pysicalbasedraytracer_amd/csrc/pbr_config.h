@@ -16,7 +16,7 @@
     defined(PBR_CAMERA_SHORT) || defined(PBR_WF_SHADE_OCC) || defined(PBR_WF_SHADE_OCC_MM) ||                        \
     defined(PBR_WF_FUSED_OCC) || defined(PBR_WFP_OCC) || defined(PBR_WFV_OCC) || defined(PBR_LANES_DEFAULT) ||       \
     defined(PBR_INLINE_TRANS) || defined(PBR_DIAG_SHADE) || defined(PBR_STACK_DIAG) || defined(PBR_ANY_SHORT) || defined(PBR_WF_BLOCKS) || defined(PBR_CLASSED_SHADE) || defined(PBR_WF_FUSED_MATS_LDS) || defined(PBR_WFP_OCC_MM) || defined(PBR_WFP_OCC_L) || \
-    defined(PBR_NF_ROWS) || defined(PBR_SEG_WAVE) || defined(PBR_SLAB_BRANCHLESS) || defined(PBR_WF_WHITTED_MAXLOG2)
+    defined(PBR_NF_ROWS) || defined(PBR_SEG_WAVE) || defined(PBR_SLAB_BRANCHLESS) || defined(PBR_WF_WHITTED_MAXLOG2) || defined(PBR_OWN_LANES)
 #error "tuning switches are development builds only: add -DPBR_DEV_KNOBS=1"
 #endif
 #endif

@@ -873,7 +873,8 @@ struct pbr_hip_ctx {
     bool inFlight = false;
     // wavefront buffers of the two chunk lanes, and the lane-1 stream with its fork/join events
     WfBufs wb[kWfLanes];
-    hipStream_t side[kWfLanes] = {};     // lanes 1.. (lane 0 runs on the caller's stream)
+    hipStream_t side[kWfLanes] = {};     // lanes 1.. (lane 0: the caller's stream, or ctx->stream — wf_fork)
+    hipStream_t lane0 = nullptr;         // lane 0's stream in the current frame or batch (wf_fork)
     hipEvent_t evFork = nullptr, evJoin[kWfLanes] = {};
     struct FrameEv {                     // a batch: the end of frame f's last chunk on each lane it used
         hipEvent_t ev[kWfLanes] = {};
@@ -1129,10 +1130,16 @@ constexpr double kBatchLaneBytes = 48e9;
 // 2^k <= 2^maxLog2 samples whose lanes' buffers fit that many bytes (not below 2^minLog2), and a
 // batch's one-chunk frames keep as many lanes as fit it; 0: the default is 2^maxLog2 and the batch
 // budget kBatchLaneBytes.  A requested chunk_log2 is capped at maxLog2 either way.
+// wideLanes > the default lane count: the default lanes when that many lanes of 2^maxLog2-sample
+// chunks fit laneBudget (the Path schedule: 4).
 WfChunks wf_chunks(const pbr_schedule& sch, const KParams& P, int maxLog2 = 25, bool batch = false,
-                   double bytesPerSample = 0, double laneBudget = 0, int defLog2 = 0, int minLog2 = 20) {
+                   double bytesPerSample = 0, double laneBudget = 0, int defLog2 = 0, int minLog2 = 20,
+                   int wideLanes = 0) {
     WfChunks c;
     c.lanes = sch.serial ? 1 : (sch.lanes > 0 ? sch.lanes : kWfDefaultLanes);
+    if (!sch.serial && sch.lanes == 0 && wideLanes > c.lanes && sch.chunk_log2 == 0 && defLog2 == 0 &&
+        wideLanes * bytesPerSample * (double)(1LL << maxLog2) <= laneBudget)
+        c.lanes = std::min(wideLanes, kWfLanes);
     int chunkLog2 = maxLog2;
     if (sch.chunk_log2 > 0) chunkLog2 = std::min(sch.chunk_log2, maxLog2);
     else if (defLog2 > 0) chunkLog2 = std::min(defLog2, maxLog2);
@@ -1198,24 +1205,44 @@ struct FrameSet {
     uint8_t* const* rgba = nullptr;
     bool batch = false;
 };
-hipStream_t lane_stream(pbr_hip_ctx* ctx, hipStream_t s, int l) { return l ? ctx->side[l] : s; }
-// Fork the lanes off `s` at the start of a frame (a batch), join them back at the end.
-int wf_fork(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
-    if (lanes < 2) return PBR_OK;
-    if (!ctx->evFork) HIP_TRY(hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
-    for (int l = 1; l < lanes; ++l)
+// Lanes and hardware queues (PBR_OWN_LANES).  HIP gives a process a few hardware queues (4 by
+// default) and deals them to streams in creation order, so lanes only run side by side when their
+// streams hold different queues.  The context creates its stream and the lane streams 1-3 together
+// (create_lane_streams); a caller's own stream, made at some other time, may share a queue with a
+// lane, whose launches then wait behind the other's.  So with four lanes (as many as the default
+// queues) and a caller's stream, lane 0 runs on the context's stream, forked from and joined back
+// into the caller's.  With fewer lanes the caller's stream keeps lane 0: its fork/join waits would
+// otherwise sit in a queue it may share with a lane.  Measured (bit-identical, frame ms in batches
+// on a torch stream as bench.py's, profiles/r6_own_lanes_ab.log): four lanes, C3 206.8-207.4 →
+// 194.7-196.0, C4 4310 → 4156; three lanes, C5 772.1 → 772.8, C2 13.57-13.59 → 13.75-13.89.
+#ifndef PBR_OWN_LANES
+#define PBR_OWN_LANES 1
+#endif
+int create_lane_streams(pbr_hip_ctx* ctx) {
+    for (int l = 1; l < kWfLanes; ++l)
         if (!ctx->side[l]) {
             HIP_TRY(hipStreamCreateWithFlags(&ctx->side[l], hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&ctx->evJoin[l], hipEventDisableTiming));
         }
+    if (!ctx->evJoin[0]) HIP_TRY(hipEventCreateWithFlags(&ctx->evJoin[0], hipEventDisableTiming));
+    if (!ctx->evFork) HIP_TRY(hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
+    return PBR_OK;
+}
+hipStream_t lane_stream(pbr_hip_ctx* ctx, hipStream_t s, int l) { return l ? ctx->side[l] : (ctx->lane0 ? ctx->lane0 : s); }
+// Fork the lanes off `s` at the start of a frame (a batch), join them back at the end.
+int wf_fork(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
+    const bool own = PBR_OWN_LANES && lanes >= kWfLanes && s != ctx->stream;
+    ctx->lane0 = own ? ctx->stream : s;
+    if (lanes < 2) return PBR_OK;
+    if (int rc = create_lane_streams(ctx)) return rc;
     HIP_TRY(hipEventRecord(ctx->evFork, s));
-    for (int l = 1; l < lanes; ++l) HIP_TRY(hipStreamWaitEvent(ctx->side[l], ctx->evFork, 0));
+    for (int l = own ? 0 : 1; l < lanes; ++l) HIP_TRY(hipStreamWaitEvent(lane_stream(ctx, s, l), ctx->evFork, 0));
     return PBR_OK;
 }
 int wf_join(pbr_hip_ctx* ctx, hipStream_t s, int lanes) {
     if (lanes < 2) return PBR_OK;
-    for (int l = 1; l < lanes; ++l) {
-        HIP_TRY(hipEventRecord(ctx->evJoin[l], ctx->side[l]));
+    for (int l = ctx->lane0 != s ? 0 : 1; l < lanes; ++l) {
+        HIP_TRY(hipEventRecord(ctx->evJoin[l], lane_stream(ctx, s, l)));
         HIP_TRY(hipStreamWaitEvent(s, ctx->evJoin[l], 0));
     }
     return PBR_OK;
@@ -1497,7 +1524,11 @@ int render_wavefront_path(pbr_hip_ctx* ctx, KParams& P, hipStream_t s, bool vol,
     // the lane buffers below, per sample: two ray queues with their state (84 B each), shadow and probe
     // queues, the direct records, the sample's L and index (+ VolPath's transmittance walk and
     // records), and the class pass lists (at most 5 passes)
-    const WfChunks ch = wf_chunks(ctx->sched, P, 27, F.batch, (vol ? 460.0 : 340.0) + 4.0 * 5, lane_budget(ctx));
+    // Path: four lanes where four lanes of 2^27-sample chunks fit the budget (bit-identical, 2^27
+    // chunks, frame ms in batches: C3 204.5 → 195.8, C4 4217 → 4160; VolPath's four lanes would have to
+    // drop to 2^26 chunks: C5 776.6 → 806.0, profiles/r6_lanes4_batch.log)
+    const WfChunks ch = wf_chunks(ctx->sched, P, 27, F.batch, (vol ? 460.0 : 340.0) + 4.0 * 5, lane_budget(ctx), 0, 20,
+                                  vol ? 0 : 4);
     const size_t cap = ch.cap, qcap = ch.qcap;
     const long long nChunks = (P.nPixels + ch.chunkPix - 1) / ch.chunkPix;
     const int lobes = scene_lobe_kinds(ctx->host);
@@ -1973,6 +2004,7 @@ int pbr_hip_create(int device, pbr_hip_ctx** out) {
     pbr_hip_ctx* c = ctx.get();
     {
         pbr_hip_ctx* ctx = c;   // for HIP_TRY
+        if (PBR_OWN_LANES) { if (int rc = create_lane_streams(ctx)) return rc; }   // right after ctx->stream
         HIP_TRY(hipHostMalloc((void**)&ctx->guardHost, sizeof(int), hipHostMallocDefault));
         *ctx->guardHost = 0;
         HIP_TRY(ctx->dGuard.ensure(sizeof(int)));

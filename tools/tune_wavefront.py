@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--profile", action="store_true", help="per-kernel-family ms per frame (HIP events)")
     ap.add_argument("--batch", type=int, default=0, help="time K-frame pbr_hip_render_frames batches (bench.py's "
                                                            "timed window) instead of single frames; ms per frame")
+    ap.add_argument("--user-stream", action="store_true", help="render on a torch-created stream (as bench.py) "
+                                                                   "instead of torch's null stream (the context's own)")
     ap.add_argument("variants", nargs="*", default=[""])
     a = ap.parse_args()
     if a.lib:
@@ -48,7 +50,9 @@ def main():
     r = HipRenderer(0)
     r.upload(scene)
     dev = torch.device("cuda", 0)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev) if a.user_stream else torch.cuda.current_stream(dev)
+    if a.user_stream:
+        torch.cuda.set_stream(stream)
     rgb = torch.empty((npx, 3), dtype=torch.float32, device=dev)
     rgba = torch.empty((npx, 4), dtype=torch.uint8, device=dev)
     ref = None
@@ -95,6 +99,9 @@ def main():
             r.set_profiling(0)
             kern = "  [" + ", ".join(f"{k.replace('k_', '')} {v['ms'] / a.steps:.2f}" for k, v in prof.items()) + "]"
         tag = f" shard {a.shard} tile {a.tile} ({npx} px)" if a.shard else ""
+        if a.batch > 0:   # device memory in use after the variant (the lanes' buffers dominate)
+            fr, tot = torch.cuda.mem_get_info(dev)
+            tag += f" [device memory in use {(tot - fr) / 1e9:.1f} of {tot / 1e9:.1f} GB]"
         print(f"{a.config}{tag} {os.path.basename(a.lib or 'lib')} {v or 'default':30s} {m:8.2f} ms  "
               f"{npx * spp / m / 1e3:8.1f} Msamples/s  {same}{kern}", flush=True)
         r.set_schedule()
